@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark: Goldilocks NTT throughput on MI355X (BASELINE config 2, n = 2^20).
+
+A step = one forward NTT of a batch of B synthetic polynomials (uniform in
+[0, p), seeded splitmix64, generated on the device) that are already resident in
+HBM. At N GPUs each polynomial has N * 2^20 coefficients, sharded by coefficient
+stride (rank g holds a[g::N]): local 2^20-point NTT + RCCL all-to-all + radix-N
+combine (DESIGN.md "Multi-GPU"), so per-GPU work is fixed (weak scaling).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+`roofline` (HBM-bound, algorithmic bytes 16*n per transform) and `cpu_baseline`
+(the oracle's recursion-faithful restatement of src/fft.rs:90-106, 1 core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "plonk-by-fingers_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import pbf  # noqa: E402
+
+GOLD = pbf.GOLDILOCKS
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def root_of_unity(n: int) -> int:
+    return pow(7, (GOLD - 1) // n, GOLD)
+
+
+def cpu_baseline(log_n: int, budget_s: float) -> dict:
+    """The oracle's recursion-faithful restatement of fft.rs:90-106 on one core,
+    timed on this host over a bounded sample (whole 2^log_n transforms)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker/baseline only (never on the GPU path)
+
+    n = 1 << log_n
+    w = root_of_unity(n)
+    a = oracle.splitmix_field(GOLD, 0x5EED0002, n)
+    oracle.ntt_ct(GOLD, w, a)  # warm-up run (page-in, allocator), not timed
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        oracle.ntt_ct(GOLD, w, a)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and runs >= 2:
+            break
+    return {"value": runs * n / el, "unit": "elements/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} x 2^{log_n}-point Goldilocks NTT, oracle ntt_ct (recursion-faithful "
+                      f"restatement of src/fft.rs:90-106, 1 thread), {el:.1f} s"}
+
+
+def load_traffic(log_n: int, batch: int):
+    """HBM bytes per NTT from the committed PMC pass (profiles/pmc_ntt_2p{log_n}.json), if any."""
+    p = os.path.join(ROOT, "profiles", f"pmc_ntt_2p{log_n}_b{batch}.json")
+    if os.path.exists(p):
+        with open(p) as fh:
+            return json.load(fh).get("hbm_bytes_per_step")
+    return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=20, help="per-GPU transform size (2^log_n)")
+    ap.add_argument("--batch", type=int, default=32, help="polynomials per step")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)",
+                  file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    n_local = 1 << args.log_n
+    B = args.batch
+    ctx = pbf.Context(local_rank)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    ctx.set_stream(sp)
+
+    if world == 1:
+        step_fn, n_global = _single_gpu(ctx, n_local, B, sp)
+    else:
+        from multigpu import ShardedNtt  # plonk-by-fingers_amd/multigpu.py
+
+        sh = ShardedNtt(ctx, dist, rank, world, args.log_n, B, sp)
+        step_fn, n_global = sh.step, sh.n_global
+
+    for _ in range(args.warmup):
+        step_fn()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step_fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max, ev_max = float(t[0]), float(t[1])
+
+    elements = B * n_global * args.steps  # all ranks together
+    value = elements / wall_max
+    ms_per_step = wall_max / args.steps * 1e3
+    # roofline of the per-GPU NTT kernels: algorithmic bytes 16 * n per transform
+    alg_bytes_step = 16.0 * n_local * B
+    achieved = alg_bytes_step / (ev_max / args.steps) / 1e9
+    if rank == 0:
+        out = {
+            "metric": "NTT elements/sec (Goldilocks, n=2^20 per GPU, natural order, bit-exact vs src/fft.rs)",
+            "value": value,
+            "unit": "elements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64 (Goldilocks p=2^64-2^32+1)",
+            "data": "synthetic: splitmix64 seed 0x5EED0002, uniform in [0,p), generated on device",
+            "config": {"workload": f"Goldilocks forward NTT, batch {B} x 2^{args.log_n}"
+                                   + (f" per GPU (global n = {world} x 2^{args.log_n}, stride-sharded)"
+                                      if world > 1 else ""),
+                       "n_per_gpu": n_local, "n_global": n_global, "batch": B,
+                       "passes": os.environ.get("PBF_NTT_PASSES", "default")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.log_n, B),
+                         "kernel": "ntt_pass_kernel (all passes of one batched NTT; 16*n bytes per transform)"},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+    return 0
+
+
+def _single_gpu(ctx, n, B, sp):
+    w = root_of_unity(n)
+    buf_in = torch.empty(B * n, dtype=torch.int64, device="cuda")
+    buf_out = torch.empty_like(buf_in)
+    ctx.fill_random_dev(GOLD, 0x5EED0002, buf_in.data_ptr(), B * n, stream=sp)
+
+    def step():
+        ctx.ntt_batch_dev(GOLD, w, buf_in.data_ptr(), buf_out.data_ptr(), n, B, stream=sp)
+
+    return step, n
+
+
+if __name__ == "__main__":
+    sys.exit(main())

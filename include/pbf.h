@@ -1,0 +1,89 @@
+/*
+ * pbf.h — C-ABI of the MI355X-native PLONK hot path (libpbf.so, gfx950).
+ *
+ * Drop-in boundary for adria0/plonk-by-fingers (Rust). The reference has no FFI;
+ * every entry point below replaces one of its trait methods / free functions and
+ * cites it as file:line relative to the reference root. A Rust caller binds these
+ * with an `extern "C"` block; here they are exercised from C++
+ * and from Python (ctypes) tests.
+ *
+ * Conventions:
+ *   - Field elements cross the ABI canonical, in [0, modulus), one uint64_t each
+ *     (the reference's U64Field<M> is one u64, u64field.rs:27-28). 256-bit
+ *     elements are 4 x uint64_t little-endian limbs, canonical (never Montgomery).
+ *   - Vectors are natural order (fft.rs:98-104 writes o[i] / o[i+len/2]).
+ *   - Host-pointer entry points are synchronous: copy in, compute, copy out.
+ *     `_dev` entry points take device pointers and a hipStream_t (void*; NULL =
+ *     the context's stream) and only enqueue work.
+ *   - Input and output may alias (in-place is allowed).
+ *   - Supported moduli for the u64 entry points: Goldilocks p = 2^64-2^32+1, and any
+ *     odd M < 2^32 (the range where the reference's `(a*b)%M` in u64 is exact,
+ *     u64field.rs:177).
+ *   - Errors are returned, never aborted on. pbf_last_error() gives the text.
+ *   - One pbf_ctx per host thread; distinct contexts are independent.
+ */
+#ifndef PBF_H
+#define PBF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum pbf_status {
+  PBF_OK = 0,
+  PBF_EINVAL = 1,      /* bad size / not a power of two / omega order != n / non-canonical input */
+  PBF_ENOINV = 2,      /* n has no inverse mod M: the reference panics at fft.rs:73 `.unwrap()` */
+  PBF_EDEVICE = 3,     /* HIP error (allocation, launch, copy) */
+  PBF_ECOMM = 4,       /* RCCL / multi-GPU exchange error */
+  PBF_EUNSUPPORTED = 5 /* modulus outside the supported set */
+};
+
+typedef struct pbf_ctx pbf_ctx;
+
+/* ---- context ------------------------------------------------------------ */
+/* Owns the device, a stream, twiddle tables (cached per (modulus, omega, n)) and
+ * scratch buffers. Replaces nothing in the reference (its types are plain values). */
+int pbf_ctx_create(int device, pbf_ctx** out);
+void pbf_ctx_destroy(pbf_ctx* ctx);
+const char* pbf_last_error(void);
+/* hipStream_t used when a `_dev` call passes stream == NULL. */
+int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream);
+int pbf_device_sync(pbf_ctx* ctx);
+
+/* ---- FFT trait ------------------------------------------------------------ */
+/* CooleyTurkey::new(EvaluationDomainGenerator{omega, size: n}) + fft / fft_inv
+ * (fft.rs:6-21, 55-78). out[k] = sum_j in[j] * omega^(j*k)           (inverse = 0)
+ *                       out[j] = n^-1 * sum_k in[k] * omega^(-j*k)    (inverse = 1)
+ * omega must have multiplicative order exactly n (the reference assumes it).   */
+int pbf_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* in, uint64_t* out,
+                size_t n, int inverse);
+/* Device-pointer, batched: `batch` independent transforms, polynomial b at
+ * d_in + b*n. Inputs must already be canonical (not checked on this path).   */
+int pbf_ntt_u64_batch_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* d_in,
+                          uint64_t* d_out, size_t n, size_t batch, int inverse, void* stream);
+
+/* ---- mul_ntt ---------------------------------------------------------------- */
+/* fft.rs:109-132: zero-pad a (la) and b (lb) to la+lb (= the domain size, a power
+ * of two), forward NTT both, multiply pointwise, inverse NTT. out has la+lb entries
+ * and is NOT normalised (the reference's caller wraps it in Poly::new, fft.rs:180). */
+int pbf_mul_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* a, size_t la,
+                    const uint64_t* b, size_t lb, uint64_t* out);
+
+/* ---- Poly ------------------------------------------------------------------- */
+/* Poly::eval (poly.rs:71-79) at nx points: ys[i] = sum_j coeffs[j] * xs[i]^j. */
+int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, size_t n,
+                      const uint64_t* xs, size_t nx, uint64_t* ys);
+
+/* ---- synthetic inputs (bench / tests) ------------------------------------- */
+/* d_out[i] = splitmix64 stream of (seed, i) with rejection of values >= modulus;
+ * identical to tests/golden/gen_golden.py:splitmix_field.                     */
+int pbf_fill_random_u64_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t seed, uint64_t* d_out,
+                            size_t count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBF_H */

@@ -1,0 +1,255 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of liboracle.so, the CPU restatement of adria0/plonk-by-fingers
+(field.hpp / fft.hpp / pbh.hpp cite the reference file:line they follow).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker; the product path (libpbf.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+GOLDILOCKS = 0xFFFFFFFF00000001
+
+_u64 = ctypes.c_uint64
+_p64 = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+_pint = ctypes.POINTER(ctypes.c_int)
+
+_SIG = [
+    ("oracle_f_add", _u64, [_u64, _u64, _u64]),
+    ("oracle_f_sub", _u64, [_u64, _u64, _u64]),
+    ("oracle_f_mul", _u64, [_u64, _u64, _u64]),
+    ("oracle_f_neg", _u64, [_u64, _u64]),
+    ("oracle_f_pow", _u64, [_u64, _u64, _u64]),
+    ("oracle_f_from_i64", _u64, [_u64, ctypes.c_int64]),
+    ("oracle_f_inv", ctypes.c_int, [_u64, _u64, _p64]),
+    ("oracle_ntt_ct", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("oracle_ntt_vandermonde", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("oracle_ntt_iter", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("oracle_mul_ntt", ctypes.c_int, [_u64, _u64, _p64, _sz, _p64, _sz, _p64]),
+    ("oracle_poly_mul", _sz, [_u64, _p64, _sz, _p64, _sz, _p64]),
+    ("oracle_poly_eval", _u64, [_u64, _p64, _sz, _u64]),
+    ("oracle_poly_div", ctypes.c_int, [_u64, _p64, _sz, _p64, _sz, _p64, ctypes.POINTER(_sz), _p64,
+                                       ctypes.POINTER(_sz)]),
+    ("oracle_g1_add", ctypes.c_int, [_p64, _p64, _p64]),
+    ("oracle_g1_mul", ctypes.c_int, [_p64, _u64, _p64]),
+    ("oracle_g1_neg", ctypes.c_int, [_p64, _p64]),
+    ("oracle_g1_in_curve", ctypes.c_int, [_p64]),
+    ("oracle_g2_add", ctypes.c_int, [_p64, _p64, _p64]),
+    ("oracle_g2_mul", ctypes.c_int, [_p64, _u64, _p64]),
+    ("oracle_gt_mul", None, [_p64, _p64, _p64]),
+    ("oracle_gt_pow", None, [_p64, _u64, _p64]),
+    ("oracle_pairing", ctypes.c_int, [_p64, _p64, _p64]),
+    ("oracle_pbh_prove", ctypes.c_int, [_sz, _p64, _p64, _p64, _p64, _p64, _u64, _u64, _u64, _u64, _p64, _p64,
+                                        _pint]),
+]
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIG:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _a(x) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_p64)
+
+
+def ntt_ct(m: int, omega: int, values, inverse: bool = False) -> np.ndarray:
+    """Recursion-faithful CooleyTurkey::fft / fft_inv (fft.rs:55-106)."""
+    a = _a(values)
+    out = np.empty_like(a)
+    rc = lib().oracle_ntt_ct(m, omega, _p(a), _p(out), a.size, int(inverse))
+    if rc:
+        raise ValueError(f"oracle_ntt_ct rc={rc}")
+    return out
+
+
+def ntt_vandermonde(m: int, omega: int, values, inverse: bool = False) -> np.ndarray:
+    a = _a(values)
+    out = np.empty_like(a)
+    rc = lib().oracle_ntt_vandermonde(m, omega, _p(a), _p(out), a.size, int(inverse))
+    if rc:
+        raise ValueError(f"oracle_ntt_vandermonde rc={rc}")
+    return out
+
+
+def ntt_iter(m: int, omega: int, values, inverse: bool = False) -> np.ndarray:
+    a = _a(values)
+    out = np.empty_like(a)
+    rc = lib().oracle_ntt_iter(m, omega, _p(a), _p(out), a.size, int(inverse))
+    if rc:
+        raise ValueError(f"oracle_ntt_iter rc={rc}")
+    return out
+
+
+def mul_ntt(m: int, omega: int, a, b) -> np.ndarray:
+    a = _a(a)
+    b = _a(b)
+    out = np.empty(a.size + b.size, dtype=np.uint64)
+    rc = lib().oracle_mul_ntt(m, omega, _p(a), a.size, _p(b), b.size, _p(out))
+    if rc:
+        raise ValueError(f"oracle_mul_ntt rc={rc}")
+    return out
+
+
+def poly_mul(m: int, a, b) -> np.ndarray:
+    a = _a(a)
+    b = _a(b)
+    out = np.empty(a.size + b.size, dtype=np.uint64)
+    k = lib().oracle_poly_mul(m, _p(a), a.size, _p(b), b.size, _p(out))
+    return out[:k].copy()
+
+
+def poly_eval(m: int, coeffs, x: int) -> int:
+    c = _a(coeffs)
+    return int(lib().oracle_poly_eval(m, _p(c), c.size, x))
+
+
+def poly_div(m: int, num, den):
+    n = _a(num)
+    d = _a(den)
+    q = np.empty(max(n.size, 1) + 1, dtype=np.uint64)
+    r = np.empty(max(n.size, 1) + d.size + 1, dtype=np.uint64)
+    lq, lr = _sz(), _sz()
+    rc = lib().oracle_poly_div(m, _p(n), n.size, _p(d), d.size, _p(q), ctypes.byref(lq), _p(r), ctypes.byref(lr))
+    if rc:
+        raise ValueError("oracle_poly_div failed")
+    return q[: lq.value].copy(), r[: lr.value].copy()
+
+
+def f(name: str, *args) -> int:
+    return int(getattr(lib(), "oracle_f_" + name)(*args))
+
+
+def f_inv(m: int, a: int):
+    out = _u64()
+    ok = lib().oracle_f_inv(m, a, ctypes.byref(out))
+    return int(out.value) if ok else None
+
+
+# ---- toy curve (pbh/*.rs); G1 points are (x, y, inf)
+def _pt(v):
+    return _a(list(v))
+
+
+def g1_add(p, q):
+    o = np.zeros(3, np.uint64)
+    if lib().oracle_g1_add(_p(_pt(p)), _p(_pt(q)), _p(o)):
+        raise ValueError("g1_add panicked")
+    return tuple(int(x) for x in o)
+
+
+def g1_mul(p, s):
+    o = np.zeros(3, np.uint64)
+    if lib().oracle_g1_mul(_p(_pt(p)), s, _p(o)):
+        raise ValueError("g1_mul panicked")
+    return tuple(int(x) for x in o)
+
+
+def g1_neg(p):
+    o = np.zeros(3, np.uint64)
+    lib().oracle_g1_neg(_p(_pt(p)), _p(o))
+    return tuple(int(x) for x in o)
+
+
+def g2_add(p, q):
+    o = np.zeros(2, np.uint64)
+    if lib().oracle_g2_add(_p(_pt(p)), _p(_pt(q)), _p(o)):
+        raise ValueError("g2_add panicked")
+    return tuple(int(x) for x in o)
+
+
+def g2_mul(p, s):
+    o = np.zeros(2, np.uint64)
+    if lib().oracle_g2_mul(_p(_pt(p)), s, _p(o)):
+        raise ValueError("g2_mul panicked")
+    return tuple(int(x) for x in o)
+
+
+def gt_mul(a, b):
+    o = np.zeros(2, np.uint64)
+    lib().oracle_gt_mul(_p(_pt(a)), _p(_pt(b)), _p(o))
+    return tuple(int(x) for x in o)
+
+
+def gt_pow(a, e):
+    o = np.zeros(2, np.uint64)
+    lib().oracle_gt_pow(_p(_pt(a)), e, _p(o))
+    return tuple(int(x) for x in o)
+
+
+def pairing(p, q):
+    o = np.zeros(2, np.uint64)
+    if lib().oracle_pairing(_p(_pt(p)), _p(_pt(q)), _p(o)):
+        raise ValueError("pairing panicked")
+    return tuple(int(x) for x in o)
+
+
+def pbh_prove(gates, copies, abc, chal, rnd, s=2, srs_n=6, omega_pows=4, verify_u=None):
+    """plonk.rs:191-466 over PlonkByHandTypes; returns (points[9], fields[7], verified)."""
+    n = len(gates)
+    g = _a([x for row in gates for x in row])
+    c = _a([x for col in copies for pair in col for x in pair])
+    w = _a([x for col in abc for x in col])
+    pts = np.zeros(27, np.uint64)
+    fs = np.zeros(7, np.uint64)
+    ver = ctypes.c_int()
+    rc = lib().oracle_pbh_prove(n, _p(g), _p(c), _p(w), _p(_a(chal)), _p(_a(rnd)), s, srs_n, omega_pows,
+                                17 if verify_u is None else verify_u, _p(pts), _p(fs), ctypes.byref(ver))
+    if rc:
+        raise ValueError("oracle_pbh_prove failed (reference would panic)")
+    points = [tuple(int(x) for x in pts[3 * i: 3 * i + 3]) for i in range(9)]
+    return points, [int(x) for x in fs], (None if verify_u is None else bool(ver.value))
+
+
+# ---- synthetic inputs (mirrors fill_random_kernel in csrc/ntt_launch.hip)
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def splitmix_field(modulus: int, seed: int, count: int, offset: int = 0) -> np.ndarray:
+    """Element i = mix(seed + (i+1)*golden); Goldilocks re-mixes values >= p,
+    other moduli reduce % M."""
+    with np.errstate(over="ignore"):
+        i = np.arange(offset, offset + count, dtype=np.uint64)
+        z = _mix(np.uint64(seed) + (i + np.uint64(1)) * _G)
+        if modulus == GOLDILOCKS:
+            bad = z >= np.uint64(modulus)
+            while bad.any():
+                z[bad] = _mix(z[bad] + _G)
+                bad = z >= np.uint64(modulus)
+        else:
+            z = z % np.uint64(modulus)
+    return z

@@ -1,0 +1,162 @@
+// C-ABI entry points of libpbf.so (include/pbf.h). Each cites the reference
+// function it replaces (paths relative to the adria0/plonk-by-fingers root).
+#include <cstring>
+#include "../../include/pbf.h"
+#include "internal.hpp"
+
+namespace pbf {
+static thread_local std::string g_last_error;
+void set_error(const std::string& s) { g_last_error = s; }
+int fail(int code, const std::string& s) {
+  g_last_error = s;
+  return code;
+}
+static bool all_canonical(const uint64_t* v, size_t n, uint64_t m) {
+  for (size_t i = 0; i < n; ++i)
+    if (v[i] >= m) return false;
+  return true;
+}
+}  // namespace pbf
+
+using namespace pbf;
+
+int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan** out) {
+  auto key = std::make_tuple(m, omega, n, inverse ? 1 : 0);
+  auto it = plans.find(key);
+  if (it != plans.end()) { *out = it->second.get(); return 0; }
+  std::unique_ptr<NttPlan> p(new NttPlan());
+  PBF_HIP(hipSetDevice(device));
+  int rc = make_plan(m, omega, n, inverse ? 1 : 0, p.get());
+  if (rc) return rc;
+  *out = p.get();
+  plans[key] = std::move(p);
+  return 0;
+}
+
+extern "C" {
+
+const char* pbf_last_error(void) { return g_last_error.c_str(); }
+
+int pbf_ctx_create(int device, pbf_ctx** out) {
+  if (!out) return fail(PBF_EINVAL, "null out");
+  int count = 0;
+  PBF_HIP(hipGetDeviceCount(&count));
+  if (device < 0 || device >= count) return fail(PBF_EINVAL, "device index out of range");
+  PBF_HIP(hipSetDevice(device));
+  pbf_ctx* c = new pbf_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(PBF_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return PBF_OK;
+}
+
+void pbf_ctx_destroy(pbf_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream) {
+  if (!ctx) return fail(PBF_EINVAL, "null ctx");
+  ctx->user_stream = (hipStream_t)stream;
+  return PBF_OK;
+}
+
+int pbf_device_sync(pbf_ctx* ctx) {
+  if (!ctx) return fail(PBF_EINVAL, "null ctx");
+  PBF_HIP(hipSetDevice(ctx->device));
+  PBF_HIP(hipDeviceSynchronize());
+  return PBF_OK;
+}
+
+// fft.rs:66-78 CooleyTurkey::fft / fft_inv (host buffers, synchronous)
+int pbf_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* in, uint64_t* out, size_t n,
+                int inverse) {
+  if (!ctx || (!in && n) || (!out && n)) return fail(PBF_EINVAL, "null argument");
+  NttPlan* p;
+  int rc = ctx->plan(modulus, omega, n, inverse, &p);
+  if (rc) return rc;
+  if (!all_canonical(in, n, modulus)) return fail(PBF_EINVAL, "input not canonical");
+  hipStream_t s = ctx->stream;
+  if ((rc = ctx->io0.ensure(n * 8))) return rc;
+  PBF_HIP(hipMemcpyAsync(ctx->io0.p, in, n * 8, hipMemcpyHostToDevice, s));
+  rc = run_plan(*p, (const uint64_t*)ctx->io0.p, (uint64_t*)ctx->io0.p, 1, ctx->scratch0, ctx->scratch1, s);
+  if (rc) return rc;
+  PBF_HIP(hipMemcpyAsync(out, ctx->io0.p, n * 8, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return PBF_OK;
+}
+
+int pbf_ntt_u64_batch_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* d_in, uint64_t* d_out,
+                          size_t n, size_t batch, int inverse, void* stream) {
+  if (!ctx || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  NttPlan* p;
+  int rc = ctx->plan(modulus, omega, n, inverse, &p);
+  if (rc) return rc;
+  return run_plan(*p, d_in, d_out, batch, ctx->scratch0, ctx->scratch1, ctx->pick(stream));
+}
+
+// fft.rs:109-132 mul_ntt
+int pbf_mul_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* a, size_t la, const uint64_t* b,
+                    size_t lb, uint64_t* out) {
+  if (!ctx || !out || (!a && la) || (!b && lb)) return fail(PBF_EINVAL, "null argument");
+  const size_t n = la + lb;
+  NttPlan *fw, *iv;
+  int rc = ctx->plan(modulus, omega, n, 0, &fw);
+  if (!rc) rc = ctx->plan(modulus, omega, n, 1, &iv);
+  if (rc) return rc;
+  if (!all_canonical(a, la, modulus) || !all_canonical(b, lb, modulus)) return fail(PBF_EINVAL, "input not canonical");
+  hipStream_t s = ctx->stream;
+  if ((rc = ctx->io0.ensure(2 * n * 8))) return rc;
+  uint64_t* d = (uint64_t*)ctx->io0.p;  // [a | 0 ... | b | 0 ...], two polynomials of n
+  PBF_HIP(hipMemsetAsync(d, 0, 2 * n * 8, s));
+  if (la) PBF_HIP(hipMemcpyAsync(d, a, la * 8, hipMemcpyHostToDevice, s));
+  if (lb) PBF_HIP(hipMemcpyAsync(d + n, b, lb * 8, hipMemcpyHostToDevice, s));
+  if ((rc = run_plan(*fw, d, d, 2, ctx->scratch0, ctx->scratch1, s))) return rc;
+  if ((rc = launch_pointwise_mul(fw->kind, fw->fa, d, d + n, d, n, s))) return rc;
+  if ((rc = run_plan(*iv, d, d, 1, ctx->scratch0, ctx->scratch1, s))) return rc;
+  PBF_HIP(hipMemcpyAsync(out, d, n * 8, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return PBF_OK;
+}
+
+// poly.rs:71-79 Poly::eval, batched over points
+int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, size_t n, const uint64_t* xs, size_t nx,
+                      uint64_t* ys) {
+  if (!ctx || (!coeffs && n) || (!xs && nx) || (!ys && nx)) return fail(PBF_EINVAL, "null argument");
+  if (n == 0) return fail(PBF_EINVAL, "a Poly has at least one coefficient (poly.rs:17-21)");
+  FieldKind k;
+  FieldArgs fa;
+  if (!field_for(modulus, &k, &fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
+  if (!all_canonical(coeffs, n, modulus) || !all_canonical(xs, nx, modulus)) return fail(PBF_EINVAL, "input not canonical");
+  if (nx == 0) return PBF_OK;
+  PBF_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  int rc;
+  if ((rc = ctx->io0.ensure(n * 8)) || (rc = ctx->io1.ensure(nx * 8)) || (rc = ctx->io2.ensure(nx * 8))) return rc;
+  PBF_HIP(hipMemcpyAsync(ctx->io0.p, coeffs, n * 8, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(ctx->io1.p, xs, nx * 8, hipMemcpyHostToDevice, s));
+  if ((rc = launch_poly_eval(k, fa, (const uint64_t*)ctx->io0.p, n, (const uint64_t*)ctx->io1.p, nx,
+                             (uint64_t*)ctx->io2.p, ctx->partial, s)))
+    return rc;
+  PBF_HIP(hipMemcpyAsync(ys, ctx->io2.p, nx * 8, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return PBF_OK;
+}
+
+int pbf_fill_random_u64_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t seed, uint64_t* d_out, size_t count,
+                            void* stream) {
+  if (!ctx || (!d_out && count)) return fail(PBF_EINVAL, "null argument");
+  FieldKind k;
+  FieldArgs fa;
+  if (!field_for(modulus, &k, &fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
+  return launch_fill_random(fa, k, seed, d_out, count, ctx->pick(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// Device field arithmetic for the u64 NTT path (gfx950).
+//
+// Two element types, both one uint64_t per element at rest in HBM (the layout of
+// the reference's U64Field<M>, src/utils/u64field.rs:27-28), canonical in [0, M):
+//   Goldilocks  p = 2^64 - 2^32 + 1   (BASELINE config 2 field)
+//   Mod32       any odd M < 2^32      (the range where the reference's
+//                                      `(a*b) % M` in u64 is exact, u64field.rs:177)
+// Results are canonical after every op, so GPU outputs are bit-identical to the
+// reference formulas (add u64field.rs:107-112, sub = add(neg) :147-165, mul :174-179).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pbf {
+
+struct FieldArgs {
+  uint64_t m;   // modulus
+  uint64_t mu;  // Mod32 only: floor(2^64 / m)
+};
+
+struct Goldilocks {
+  static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+  static constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p = 2^32 - 1
+
+  __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs&) {
+    uint64_t s = a + b;
+    // wrap (s < a) means the true sum is s + 2^64 = s + EPS (mod p); s + EPS cannot
+    // wrap again because a + b - 2^64 < p - 2^32. Otherwise subtract p when s >= p.
+    uint64_t t = s + EPS;
+    return (s < a || s >= P) ? t : s;
+  }
+  __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
+    uint64_t d = a - b;
+    return (a < b) ? d - EPS : d;  // d + p (mod 2^64)
+  }
+  // 128-bit product reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
+  __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {
+    uint64_t hh = hi >> 32;
+    uint64_t hl = hi & EPS;
+    uint64_t t0 = lo - hh;
+    if (lo < hh) t0 -= EPS;               // borrow: + p
+    uint64_t t1 = (hl << 32) - hl;        // hl * (2^32 - 1), < 2^64
+    uint64_t r = t0 + t1;
+    if (r < t1) r += EPS;                 // wrap: + 2^64 = + EPS (cannot wrap again)
+    return (r >= P) ? r - P : r;
+  }
+  __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs&) {
+    return reduce128(a * b, __umul64hi(a, b));
+  }
+};
+
+struct Mod32 {
+  __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs& f) {
+    uint64_t s = a + b;  // < 2^33
+    return s >= f.m ? s - f.m : s;
+  }
+  __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs& f) {
+    return a >= b ? a - b : a + f.m - b;
+  }
+  // Barrett: x < 2^64, q = floor(x * mu / 2^64) <= floor(x / m), remainder < 3m.
+  __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs& f) {
+    uint64_t x = a * b;
+    uint64_t q = __umul64hi(x, f.mu);
+    uint64_t r = x - q * f.m;
+    if (r >= f.m) r -= f.m;
+    if (r >= f.m) r -= f.m;
+    return r;
+  }
+};
+
+}  // namespace pbf

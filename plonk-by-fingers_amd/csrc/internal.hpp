@@ -1,0 +1,94 @@
+// Host-side internals of libpbf.so shared by the translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+#include "field.hpp"
+
+struct pbf_ctx;
+
+namespace pbf {
+
+typedef unsigned __int128 u128;
+static const uint64_t GOLDILOCKS = 0xFFFFFFFF00000001ull;
+
+enum FieldKind { FIELD_GOLDILOCKS = 0, FIELD_MOD32 = 1 };
+
+void set_error(const std::string& s);
+int fail(int code, const std::string& s);
+
+#define PBF_HIP(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return ::pbf::fail(3 /*PBF_EDEVICE*/, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// ---- host modular arithmetic (table generation, validation) ----
+inline uint64_t hmul(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)(((u128)a * b) % m); }
+inline uint64_t hpow(uint64_t a, uint64_t e, uint64_t m) {
+  uint64_t r = 1 % m;
+  while (e) {
+    if (e & 1) r = hmul(r, a, m);
+    a = hmul(a, a, m);
+    e >>= 1;
+  }
+  return r;
+}
+// extended gcd inverse; false when gcd != 1 (u64field.rs:52-63 returns None)
+bool hinv(uint64_t a, uint64_t m, uint64_t* out);
+
+// Classify a modulus into a device field; false if unsupported.
+bool field_for(uint64_t m, FieldKind* kind, FieldArgs* fa);
+
+// Device buffer that grows on demand (freed by the context).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need);
+  ~DevBuf();
+};
+
+// A planned NTT: (modulus, omega, n, direction) -> passes + device twiddle tables.
+struct NttPlan {
+  uint64_t m = 0, omega = 0, n = 0;
+  int inverse = 0;
+  FieldKind kind = FIELD_GOLDILOCKS;
+  FieldArgs fa{};
+  uint32_t log_n = 0;
+  uint64_t n_inv = 1;
+  std::vector<int> logr;   // radix per pass (empty => small kernel)
+  int w = 16;              // columns per workgroup
+  uint32_t tw_bits = 0;
+  DevBuf tw0, tw1, small_tw;
+  std::vector<std::shared_ptr<DevBuf>> rtab;  // per pass
+};
+
+// Build a plan (validates omega's order and n^-1). Returns PBF status.
+int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p);
+// Enqueue a batched transform of a planned size on `stream` (d_in may equal d_out).
+int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
+             hipStream_t stream);
+// Kernel launchers (ntt_launch.hip)
+int launch_pointwise_mul(FieldKind k, const FieldArgs& fa, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                         uint64_t count, hipStream_t s);
+int launch_poly_eval(FieldKind k, const FieldArgs& fa, const uint64_t* d_coeffs, uint64_t n, const uint64_t* d_xs,
+                     uint64_t nx, uint64_t* d_ys, DevBuf& partial, hipStream_t s);
+int launch_fill_random(const FieldArgs& fa, FieldKind k, uint64_t seed, uint64_t* d_out, uint64_t count,
+                       hipStream_t s);
+
+}  // namespace pbf
+
+struct pbf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t user_stream = nullptr;
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t, int>, std::unique_ptr<pbf::NttPlan>> plans;
+  pbf::DevBuf scratch0, scratch1, io0, io1, io2, partial;
+  hipStream_t pick(void* s) const { return s ? (hipStream_t)s : (user_stream ? user_stream : stream); }
+  int plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, pbf::NttPlan** out);
+};

@@ -1,0 +1,315 @@
+// Kernel instantiation, NTT planning and launchers for libpbf.so (gfx950).
+#include <cstdlib>
+#include <cstring>
+#include "internal.hpp"
+#include "ntt_kernels.hpp"
+
+namespace pbf {
+
+// ---------------------------------------------------------------- plans
+bool hinv(uint64_t a, uint64_t m, uint64_t* out) {
+  // extended gcd in i128 (u64field.rs:10-25 uses i64; the inverse is unique)
+  __int128 s = 0, old_s = 1, r = m, old_r = a % m;
+  while (r != 0) {
+    __int128 q = old_r / r, t;
+    t = old_r - q * r; old_r = r; r = t;
+    t = old_s - q * s; old_s = s; s = t;
+  }
+  if (old_r != 1) return false;
+  if (old_s < 0) old_s += m;
+  *out = (uint64_t)old_s;
+  return true;
+}
+
+bool field_for(uint64_t m, FieldKind* kind, FieldArgs* fa) {
+  fa->m = m;
+  fa->mu = 0;
+  if (m == GOLDILOCKS) { *kind = FIELD_GOLDILOCKS; return true; }
+  if (m >= 3 && m < (1ull << 32) && (m & 1)) {
+    *kind = FIELD_MOD32;
+    fa->mu = (uint64_t)(((u128)1 << 64) / m);
+    return true;
+  }
+  return false;
+}
+
+int DevBuf::ensure(size_t need) {
+  if (need <= bytes) return 0;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+  hipError_t e = hipMalloc(&p, need);
+  if (e != hipSuccess) { p = nullptr; return fail(3, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+  bytes = need;
+  return 0;
+}
+DevBuf::~DevBuf() {
+  if (p) (void)hipFree(p);
+}
+
+static int upload(DevBuf& b, const std::vector<uint64_t>& v) {
+  int rc = b.ensure(v.size() * 8);
+  if (rc) return rc;
+  PBF_HIP(hipMemcpy(b.p, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+static std::vector<int> default_passes(uint32_t log_n) {
+  const char* env = getenv("PBF_NTT_PASSES");  // e.g. "12,12" (benchmarking override)
+  if (env && *env) {
+    std::vector<int> v;
+    int sum = 0;
+    for (const char* c = env; *c;) {
+      int x = atoi(c);
+      v.push_back(x);
+      sum += x;
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+    bool ok = sum == (int)log_n;
+    for (int x : v) ok = ok && x >= 6 && x <= 12;
+    if (ok) return v;
+  }
+  int p = (log_n + 9) / 10;
+  std::vector<int> v(p, log_n / p);
+  for (int i = 0; i < (int)(log_n % p); ++i) v[i] += 1;
+  return v;
+}
+
+static int cols_for(int logr) { return logr <= 10 ? 16 : (logr == 11 ? 8 : 4); }
+
+int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
+  if (!field_for(m, &p->kind, &p->fa)) return fail(5, "unsupported modulus");
+  if (n == 0 || (n & (n - 1))) return fail(1, "n must be a power of two");
+  if (n > (1ull << 32)) return fail(1, "n too large");
+  if (omega >= m) return fail(1, "omega not canonical");
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < n) ++log_n;
+  if (n > 1) {
+    // omega must have order exactly n (the reference assumes it; fft.rs:55-65)
+    if (hpow(omega, n, m) != 1 || hpow(omega, n / 2, m) == 1) return fail(1, "omega does not have order n");
+  }
+  p->m = m; p->omega = omega; p->n = n; p->inverse = inverse; p->log_n = log_n;
+  uint64_t w = omega;
+  if (inverse) {
+    if (!hinv(n % m, m, &p->n_inv)) return fail(2, "n has no inverse modulo M (fft.rs:73 unwrap)");
+    if (!hinv(omega, m, &w)) return fail(1, "omega not invertible");
+  }
+  if (n <= 4096) {
+    std::vector<uint64_t> t(n);
+    uint64_t x = 1 % m;
+    for (uint64_t i = 0; i < n; ++i) { t[i] = x; x = hmul(x, w, m); }
+    return upload(p->small_tw, t);
+  }
+  p->logr = default_passes(log_n);
+  p->tw_bits = (log_n + 1) / 2;
+  std::vector<uint64_t> t0(1ull << p->tw_bits), t1(n >> p->tw_bits);
+  uint64_t x = 1 % m;
+  for (size_t i = 0; i < t0.size(); ++i) { t0[i] = x; x = hmul(x, w, m); }
+  uint64_t step = x;  // w^(2^tw_bits)
+  x = 1 % m;
+  for (size_t i = 0; i < t1.size(); ++i) { t1[i] = x; x = hmul(x, step, m); }
+  int rc = upload(p->tw0, t0);
+  if (!rc) rc = upload(p->tw1, t1);
+  if (rc) return rc;
+  for (int lr : p->logr) {
+    uint64_t R = 1ull << lr;
+    uint64_t wr = hpow(w, n / R, m);
+    std::vector<uint64_t> rt(R);
+    uint64_t y = 1 % m;
+    for (uint64_t i = 0; i < R; ++i) { rt[i] = y; y = hmul(y, wr, m); }
+    auto b = std::make_shared<DevBuf>();
+    rc = upload(*b, rt);
+    if (rc) return rc;
+    p->rtab.push_back(b);
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- dispatch
+typedef void (*PassFn)(PassArgs);
+
+template <class F>
+static PassFn pass_fn(int logr) {
+  switch (logr) {
+    case 6: return ntt_pass_kernel<F, 6, 16, 64>;
+    case 7: return ntt_pass_kernel<F, 7, 16, 128>;
+    case 8: return ntt_pass_kernel<F, 8, 16, 256>;
+    case 9: return ntt_pass_kernel<F, 9, 16, 512>;
+    case 10: return ntt_pass_kernel<F, 10, 16, 1024>;
+    case 11: return ntt_pass_kernel<F, 11, 8, 1024>;
+    case 12: return ntt_pass_kernel<F, 12, 4, 1024>;
+    default: return nullptr;
+  }
+}
+
+int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
+             hipStream_t stream) {
+  if (batch == 0) return 0;
+  if (p.n == 1) {
+    if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * 8, hipMemcpyDeviceToDevice, stream));
+    return 0;  // size-1 DFT is the identity; n^-1 = 1
+  }
+  if (p.logr.empty()) {
+    if (p.kind == FIELD_GOLDILOCKS)
+      hipLaunchKernelGGL(ntt_small_kernel<Goldilocks>, dim3(batch), dim3(256), 0, stream, d_in, d_out,
+                         (const uint64_t*)p.small_tw.p, p.log_n, p.n_inv, (uint32_t)p.inverse, p.fa);
+    else
+      hipLaunchKernelGGL(ntt_small_kernel<Mod32>, dim3(batch), dim3(256), 0, stream, d_in, d_out,
+                         (const uint64_t*)p.small_tw.p, p.log_n, p.n_inv, (uint32_t)p.inverse, p.fa);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  const size_t P = p.logr.size();
+  const size_t bytes = batch * p.n * 8;
+  int rc = s0.ensure(bytes);
+  if (!rc && P > 2) rc = s1.ensure(bytes);
+  if (rc) return rc;
+  uint32_t log_ns = 0;
+  for (size_t i = 0; i < P; ++i) {
+    const int lr = p.logr[i];
+    const int W = cols_for(lr);
+    PassArgs a;
+    a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p);
+    a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p);
+    a.tw0 = (const uint64_t*)p.tw0.p;
+    a.tw1 = (const uint64_t*)p.tw1.p;
+    a.rtab = (const uint64_t*)p.rtab[i]->p;
+    a.n = p.n;
+    a.n_inv = p.n_inv;
+    a.log_n = p.log_n;
+    a.log_ns = log_ns;
+    a.tw_bits = p.tw_bits;
+    a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
+    a.scale = (p.inverse && i == P - 1) ? 1 : 0;
+    a.f = p.fa;
+    const int nt = (W << lr) / 16;
+    const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
+    if (blocks > 0x7fffffffull) return fail(1, "batch too large");
+    PassFn fn = (p.kind == FIELD_GOLDILOCKS) ? pass_fn<Goldilocks>(lr) : pass_fn<Mod32>(lr);
+    if (!fn) return fail(1, "no kernel for this radix");
+    hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(nt), 0, stream, a);
+    PBF_HIP(hipGetLastError());
+    log_ns += lr;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- pointwise
+int launch_pointwise_mul(FieldKind k, const FieldArgs& fa, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                         uint64_t count, hipStream_t s) {
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return 0;
+  if (k == FIELD_GOLDILOCKS)
+    hipLaunchKernelGGL(pointwise_mul_kernel<Goldilocks>, dim3(blocks), dim3(256), 0, s, a, b, c, count, fa);
+  else
+    hipLaunchKernelGGL(pointwise_mul_kernel<Mod32>, dim3(blocks), dim3(256), 0, s, a, b, c, count, fa);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- poly eval
+// Poly::eval (poly.rs:71-79): y = sum_j c_j x^j. Block (point, chunk) computes
+// x^start * Horner(chunk) and tree-reduces; a second kernel sums the chunks.
+template <class F>
+__device__ uint64_t dpow(uint64_t x, uint64_t e, const FieldArgs& f) {
+  uint64_t r = 1 % f.m;
+  while (e) {
+    if (e & 1) r = F::mul(r, x, f);
+    x = F::mul(x, x, f);
+    e >>= 1;
+  }
+  return r;
+}
+
+constexpr int EVAL_PER_THREAD = 64;
+constexpr int EVAL_THREADS = 256;
+
+template <class F>
+__global__ void __launch_bounds__(EVAL_THREADS) poly_eval_partial(const uint64_t* c, uint64_t n, const uint64_t* xs,
+                                                                  uint64_t chunks, uint64_t* partial, FieldArgs f) {
+  __shared__ uint64_t red[EVAL_THREADS];
+  const uint64_t pt = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const uint64_t x = xs[pt];
+  const uint64_t start = (ch * EVAL_THREADS + threadIdx.x) * EVAL_PER_THREAD;
+  uint64_t acc = 0;
+  if (start < n) {
+    uint64_t end = start + EVAL_PER_THREAD;
+    if (end > n) end = n;
+    for (uint64_t j = end; j-- > start;) acc = F::add(F::mul(acc, x, f), c[j], f);
+    acc = F::mul(acc, dpow<F>(x, start, f), f);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = EVAL_THREADS / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = F::add(red[threadIdx.x], red[threadIdx.x + s], f);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+template <class F>
+__global__ void poly_eval_final(const uint64_t* partial, uint64_t chunks, uint64_t nx, uint64_t* ys, FieldArgs f) {
+  uint64_t pt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pt >= nx) return;
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < chunks; ++i) acc = F::add(acc, partial[pt * chunks + i], f);
+  ys[pt] = acc;
+}
+
+int launch_poly_eval(FieldKind k, const FieldArgs& fa, const uint64_t* d_coeffs, uint64_t n, const uint64_t* d_xs,
+                     uint64_t nx, uint64_t* d_ys, DevBuf& partial, hipStream_t s) {
+  const uint64_t per_block = (uint64_t)EVAL_THREADS * EVAL_PER_THREAD;
+  const uint64_t chunks = (n + per_block - 1) / per_block;
+  int rc = partial.ensure(chunks * nx * 8);
+  if (rc) return rc;
+  if (k == FIELD_GOLDILOCKS) {
+    hipLaunchKernelGGL(poly_eval_partial<Goldilocks>, dim3(chunks * nx), dim3(EVAL_THREADS), 0, s, d_coeffs, n, d_xs,
+                       chunks, (uint64_t*)partial.p, fa);
+    hipLaunchKernelGGL(poly_eval_final<Goldilocks>, dim3((nx + 255) / 256), dim3(256), 0, s,
+                       (const uint64_t*)partial.p, chunks, nx, d_ys, fa);
+  } else {
+    hipLaunchKernelGGL(poly_eval_partial<Mod32>, dim3(chunks * nx), dim3(EVAL_THREADS), 0, s, d_coeffs, n, d_xs,
+                       chunks, (uint64_t*)partial.p, fa);
+    hipLaunchKernelGGL(poly_eval_final<Mod32>, dim3((nx + 255) / 256), dim3(256), 0, s, (const uint64_t*)partial.p,
+                       chunks, nx, d_ys, fa);
+  }
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- synthetic inputs
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Element i: z = mix(seed + (i+1)*golden); Goldilocks rejects z >= p by re-mixing
+// z + golden; Mod32 reduces z % M. Mirrors tests/golden/gen_golden.py:splitmix_field.
+__global__ void fill_random_kernel(uint64_t seed, uint64_t* out, uint64_t count, FieldArgs f, int gold) {
+  const uint64_t G = 0x9E3779B97F4A7C15ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t z = splitmix64(seed + (i + 1) * G);
+    if (gold) {
+      while (z >= f.m) z = splitmix64(z + G);
+    } else {
+      z %= f.m;
+    }
+    out[i] = z;
+  }
+}
+
+int launch_fill_random(const FieldArgs& fa, FieldKind k, uint64_t seed, uint64_t* d_out, uint64_t count,
+                       hipStream_t s) {
+  if (count == 0) return 0;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(fill_random_kernel, dim3(blocks), dim3(256), 0, s, seed, d_out, count, fa,
+                     k == FIELD_GOLDILOCKS ? 1 : 0);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace pbf

@@ -1,0 +1,192 @@
+"""Python host binding of libpbf.so (the MI355X PLONK hot path, gfx950).
+
+Mirrors the reference's FFT trait surface (src/fft.rs:6-21,109-132) and
+Poly::eval (src/poly.rs:71-79) over the C-ABI declared in include/pbf.h.
+This module is plumbing for tests and bench.py: every call goes through the HIP
+library; there is no CPU fallback, and importing it without a built libpbf.so
+raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libpbf.so")
+
+GOLDILOCKS = 0xFFFFFFFF00000001
+
+PBF_OK, PBF_EINVAL, PBF_ENOINV, PBF_EDEVICE, PBF_ECOMM, PBF_EUNSUPPORTED = range(6)
+_NAMES = {1: "PBF_EINVAL", 2: "PBF_ENOINV", 3: "PBF_EDEVICE", 4: "PBF_ECOMM", 5: "PBF_EUNSUPPORTED"}
+
+
+class PbfError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_u64 = ctypes.c_uint64
+_p64 = ctypes.POINTER(ctypes.c_uint64)
+_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) for every entry point in include/pbf.h
+SIGNATURES = [
+    ("pbf_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    ("pbf_ctx_destroy", None, [_vp]),
+    ("pbf_last_error", ctypes.c_char_p, []),
+    ("pbf_ctx_set_stream", ctypes.c_int, [_vp, _vp]),
+    ("pbf_device_sync", ctypes.c_int, [_vp]),
+    ("pbf_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("pbf_ntt_u64_batch_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
+    ("pbf_mul_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_poly_eval_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_fill_random_u64_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _sz, _vp]),
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libpbf.so (raises if it was not built: no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise ImportError(f"libpbf.so not built at {path}; run __graft_entry__.build()")
+        lib = ctypes.CDLL(path)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != PBF_OK:
+        msg = load_library().pbf_last_error()
+        raise PbfError(rc, msg.decode() if msg else "")
+
+
+def _as_u64(x: Sequence[int] | np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+    return a
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_p64)
+
+
+class Context:
+    """pbf_ctx: one device, one stream, cached twiddle tables and scratch."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        h = _vp()
+        _check(lib.pbf_ctx_create(device, ctypes.byref(h)))
+        self.h = h
+        self.lib = lib
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.pbf_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int) -> None:
+        _check(self.lib.pbf_ctx_set_stream(self.h, _vp(stream_ptr)))
+
+    def sync(self) -> None:
+        _check(self.lib.pbf_device_sync(self.h))
+
+    # fft.rs:66-78
+    def ntt(self, modulus: int, omega: int, values, inverse: bool = False) -> np.ndarray:
+        a = _as_u64(values)
+        out = np.empty_like(a)
+        _check(self.lib.pbf_ntt_u64(self.h, modulus, omega, _ptr(a), _ptr(out), a.size, int(inverse)))
+        return out
+
+    def ntt_batch_dev(self, modulus: int, omega: int, d_in: int, d_out: int, n: int, batch: int,
+                      inverse: bool = False, stream: int = 0) -> None:
+        _check(self.lib.pbf_ntt_u64_batch_dev(self.h, modulus, omega, _vp(d_in), _vp(d_out), n, batch,
+                                              int(inverse), _vp(stream) if stream else None))
+
+    # fft.rs:109-132
+    def mul_ntt(self, modulus: int, omega: int, a, b) -> np.ndarray:
+        a = _as_u64(a)
+        b = _as_u64(b)
+        out = np.empty(a.size + b.size, dtype=np.uint64)
+        _check(self.lib.pbf_mul_ntt_u64(self.h, modulus, omega, _ptr(a), a.size, _ptr(b), b.size, _ptr(out)))
+        return out
+
+    # poly.rs:71-79
+    def poly_eval(self, modulus: int, coeffs, xs) -> np.ndarray:
+        c = _as_u64(coeffs)
+        x = _as_u64(xs)
+        y = np.empty_like(x)
+        _check(self.lib.pbf_poly_eval_u64(self.h, modulus, _ptr(c), c.size, _ptr(x), x.size, _ptr(y)))
+        return y
+
+    def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,
+                                                _vp(stream) if stream else None))
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+# ---- the reference's FFT trait surface (fft.rs:6-21) ------------------------
+class EvaluationDomainGenerator:
+    """fft.rs:6-15"""
+
+    def __init__(self, omega: int, size: int):
+        self.omega = int(omega)
+        self.size = int(size)
+
+
+class CooleyTurkey:
+    """FFT<F> for U64Field<modulus> on the GPU (fft.rs:51-79). `fft` and
+    `fft_inv` take and return canonical residues, natural order."""
+
+    def __init__(self, modulus: int, domain: EvaluationDomainGenerator, ctx: Context | None = None):
+        self.modulus = int(modulus)
+        self.domain = domain
+        self.ctx = ctx or default_context()
+
+    @classmethod
+    def new(cls, modulus: int, domain: EvaluationDomainGenerator, ctx: Context | None = None) -> "CooleyTurkey":
+        return cls(modulus, domain, ctx)
+
+    def fft(self, values) -> np.ndarray:
+        return self.ctx.ntt(self.modulus, self.domain.omega, values, inverse=False)
+
+    def fft_inv(self, freq) -> np.ndarray:
+        return self.ctx.ntt(self.modulus, self.domain.omega, freq, inverse=True)
+
+
+def mul_ntt(fft: CooleyTurkey, a_vals, b_vals) -> np.ndarray:
+    """fft.rs:109-132: length la+lb, not normalised."""
+    return fft.ctx.mul_ntt(fft.modulus, fft.domain.omega, a_vals, b_vals)
+
+
+def normalize(coeffs: np.ndarray) -> np.ndarray:
+    """poly.rs:96-105 Poly::new normalisation (strip trailing zeros, keep one)."""
+    c = np.asarray(coeffs, dtype=np.uint64)
+    nz = np.nonzero(c)[0]
+    return c[: (nz[-1] + 1 if nz.size else 1)].copy()

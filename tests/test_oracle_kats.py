@@ -1,0 +1,186 @@
+"""Pin the oracle to the reference's own known-answer tests (CPU only).
+
+Every expected value comes from tests/golden/reference_kats.json, transcribed
+from the reference's #[cfg(test)] modules (file:line in each entry)."""
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = oracle.GOLDILOCKS
+
+
+def test_u64field_vectors(kats):
+    # u64field.rs:239-254 test_base / test_vectors
+    k = kats["u64field_f101"]
+    m = k["modulus"]
+    for a, b, r in k["add"]:
+        assert oracle.f("add", m, a, b) == r
+    for a, b, r in k["sub"]:
+        assert oracle.f("sub", m, a, b) == r
+    for a, r in k["neg"]:
+        assert oracle.f("neg", m, a) == r
+    for a, b in k["div_by_zero_is_none"]:
+        assert oracle.f_inv(m, b) is None
+    for a, b in k["mul_div_roundtrip"]:  # f101(4) == f101(12) * (f101(4)/f101(12))
+        q = oracle.f("mul", m, oracle.f_inv(m, a), b)
+        assert oracle.f("mul", m, a, q) == b
+    for a, b, r in k["neg_div"]:
+        assert oracle.f("neg", m, oracle.f("mul", m, a, oracle.f_inv(m, b))) == r
+    for a, e, r in k["pow"]:
+        assert oracle.f("pow", m, a, e) == r
+
+
+def test_fft_cooley_turkey_kat(kats):
+    # fft.rs:154-168
+    k = kats["fft_337"]
+    fwd = oracle.ntt_ct(k["modulus"], k["omega"], k["values"])
+    assert fwd.tolist() == k["freq"]
+    assert oracle.ntt_ct(k["modulus"], k["omega"], fwd, inverse=True).tolist() == k["values"]
+
+
+def test_fft_vandermonde_kat(kats):
+    # fft.rs:139-152
+    k = kats["fft_337"]
+    fwd = oracle.ntt_vandermonde(k["modulus"], k["omega"], k["values"])
+    assert fwd.tolist() == k["freq"]
+    assert oracle.ntt_vandermonde(k["modulus"], k["omega"], fwd, inverse=True).tolist() == k["values"]
+
+
+def test_ntt_poly_mul_kat(kats):
+    # fft.rs:170-183: Poly::new(mul_ntt(..)) == schoolbook product
+    k = kats["mul_ntt_337"]
+    m = k["modulus"]
+    c = oracle.mul_ntt(m, k["omega"], k["a"], k["b"])
+    school = oracle.poly_mul(m, k["a"], k["b"])
+    nz = np.nonzero(c)[0]
+    assert c[: nz[-1] + 1].tolist() == school.tolist()
+
+
+def _norm(v):
+    v = list(v)
+    while len(v) > 1 and v[-1] == 0:
+        v.pop()
+    return v
+
+
+def test_poly_vectors(kats):
+    # poly.rs:402-487
+    k = kats["poly_15485863"]
+    m = k["modulus"]
+    red = lambda v: [x % m for x in v]  # noqa: E731  (From<i64> of small literals)
+    for a, b, r in k["mul"]:
+        assert oracle.poly_mul(m, a, b).tolist() == _norm(r)
+    for num, den in k["div_roundtrip"]:
+        q, r = oracle.poly_div(m, num, den)
+        back = oracle.poly_mul(m, q, den).tolist()
+        back = back + [0] * (len(r) - len(back))
+        s = [(back[i] + (int(r[i]) if i < len(r) else 0)) % m for i in range(max(len(back), len(r)))]
+        assert _norm(s) == _norm(num)
+    for (p1, p2), zz in k["z"]:
+        # (x - p1)(x - p2)
+        z = oracle.poly_mul(m, [(-p1) % m, 1], [(-p2) % m, 1]).tolist()
+        assert z == red(zz)
+    for c, x, y in k["eval"]:
+        assert oracle.poly_eval(m, c, x) == y
+
+
+def test_g1_vectors(kats):
+    # g1.rs:357-385
+    k = kats["g1"]
+    g = (1, 2, 0)
+    P = lambda xy: (xy[0], xy[1], 0)  # noqa: E731
+    two = oracle.g1_add(g, g)
+    four = oracle.g1_add(two, two)
+    eight = oracle.g1_add(four, four)
+    sixteen = oracle.g1_add(eight, eight)
+    assert oracle.g1_neg(g) == P(k["neg_g"])
+    assert two == P(k["2g"]) and oracle.g1_neg(two) == P(k["neg_2g"])
+    assert four == P(k["4g"]) and oracle.g1_neg(four) == P(k["neg_4g"])
+    assert eight == P(k["8g"]) and oracle.g1_neg(eight) == P(k["neg_8g"])
+    assert sixteen == P(k["16g"])
+    assert oracle.g1_add(two, g) == P(k["3g"])
+    assert oracle.g1_add(four, g) == P(k["5g"])
+    assert oracle.g1_add(eight, g) == P(k["9g"])
+    assert oracle.g1_mul(g, 1) == g
+    assert oracle.g1_mul(g, 2) == two
+    six = g
+    for _ in range(5):
+        six = oracle.g1_add(six, g)
+    assert oracle.g1_mul(g, 6) == six
+
+
+def test_g2_vectors(kats):
+    # g2.rs:493-505
+    k = kats["g2"]
+    g = tuple(k["generator"])
+    g2 = oracle.g2_add(g, g)
+    assert g2 == tuple(k["2g"])
+    assert oracle.g2_add(g2, g2) == oracle.g2_add(oracle.g2_add(oracle.g2_add(g, g), g), g)
+    six = g
+    for _ in range(5):
+        six = oracle.g2_add(six, g)
+    assert oracle.g2_mul(g, 6) == six
+
+
+def test_gt_vectors(kats):
+    # gt.rs:593-603
+    k = kats["gt"]
+    for a, b, r in k["mul"]:
+        assert oracle.gt_mul(a, b) == tuple(r)
+    for a, e, r in k["pow"]:
+        assert oracle.gt_pow(a, e) == tuple(r)
+    x = tuple(k["pow101_is_conj"])
+    conj = (x[0], (101 - x[1]) % 101)
+    assert oracle.gt_pow(x, 101) == conj
+    assert oracle.gt_pow(x, 102) == oracle.gt_mul(conj, x)
+
+
+def test_pairing_bilinear(kats):
+    # pairing.rs:659-679
+    k = kats["pairing"]
+    g1 = (1, 2, 0)
+    p = oracle.g1_mul(g1, k["p_mul"])
+    r = oracle.g1_mul(g1, k["r_mul"])
+    q = oracle.g2_mul((36, 31), k["q_mul"])
+    a = k["a"]
+    e = oracle.pairing
+    assert e(oracle.g1_mul(p, a), q) == e(p, oracle.g2_mul(q, a))
+    assert e(oracle.g1_mul(p, a), q) == oracle.gt_pow(e(p, q), a)
+    assert e(oracle.g1_add(p, r), q) == oracle.gt_mul(e(p, q), e(r, q))
+
+
+def test_plonk_by_hand_proof_kat(kats):
+    # pbh/mod.rs:44-124: the full 16-field proof and verify == true
+    k = kats["plonk_by_hand"]
+    pts, fs, ok = oracle.pbh_prove(k["gates_qlqrqoqmqc"], k["copies_kind_idx"], k["abc"],
+                                   k["challenge_alpha_beta_gamma_z_v"], k["rand"], k["s"], k["srs_n"],
+                                   k["omega_pows"], verify_u=k["verify_u"])
+    assert [p[:2] for p in pts] == [tuple(x) for x in k["expected_points"]]
+    assert all(p[2] == 0 for p in pts)
+    assert fs == k["expected_fields"]
+    assert ok is True
+
+
+def test_plonk_by_hand_rejects_tampered_proof(kats):
+    # a different verifier randomness still verifies; a wrong witness panics (plonk.rs:199)
+    k = kats["plonk_by_hand"]
+    bad = [list(col) for col in k["abc"]]
+    bad[2][0] = (bad[2][0] + 1) % 17
+    with pytest.raises(ValueError):
+        oracle.pbh_prove(k["gates_qlqrqoqmqc"], k["copies_kind_idx"], bad, k["challenge_alpha_beta_gamma_z_v"],
+                         k["rand"])
+
+
+@pytest.mark.parametrize("m", [GOLD, 3221225473, 337])
+def test_oracle_ntt_variants_agree(m):
+    # recursion-faithful (fft.rs:90-106) == Vandermonde (fft.rs:27-49) == iterative checker
+    for logn in (1, 2, 3, 4):
+        n = 1 << logn
+        g = 7 if m == GOLD else (5 if m == 3221225473 else 10)
+        w = pow(g, (m - 1) // n, m)
+        a = oracle.splitmix_field(m, 99 + logn, n)
+        ct = oracle.ntt_ct(m, w, a)
+        assert np.array_equal(ct, oracle.ntt_vandermonde(m, w, a))
+        assert np.array_equal(ct, oracle.ntt_iter(m, w, a))
+        assert np.array_equal(oracle.ntt_ct(m, w, ct, inverse=True), a)
