@@ -102,9 +102,9 @@ def main() -> int:
     if world == 1:
         step_fn, n_global = _single_gpu(ctx, n_local, B, sp)
     else:
-        from multigpu import ShardedNtt  # plonk-by-fingers_amd/multigpu.py
+        from multigpu import BenchSharded  # plonk-by-fingers_amd/multigpu.py
 
-        sh = ShardedNtt(ctx, dist, rank, world, args.log_n, B, sp)
+        sh = BenchSharded(ctx, dist, rank, world, args.log_n, B, sp)
         step_fn, n_global = sh.step, sh.n_global
 
     for _ in range(args.warmup):

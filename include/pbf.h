@@ -77,6 +77,24 @@ int pbf_mul_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64
 int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, size_t n,
                       const uint64_t* xs, size_t nx, uint64_t* ys);
 
+/* ---- multi-GPU stride-sharded NTT ---------------------------
+ * A transform of N = G * nl points (G = world size 2, 4 or 8; omega of order N) is
+ * sharded by coefficient stride: rank g holds a[g + G*m], m < nl, for `batch`
+ * polynomials ([b][m] layout). This is the top log2(G) levels of the reference's
+ * even/odd recursion (fft.rs:94-96) assigned to ranks. Forward on every rank:
+ *   pbf_ntt_shard_local_dev(fwd):  [b][m] stride shard -> send [dst][b][kk]   (S = nl/G)
+ *   all-to-all (RCCL, nl*batch/G elements per peer): send -> recv [src][b][kk]
+ *   pbf_ntt_shard_combine_dev(fwd): recv -> out[b][q*S + kk] = X[q*nl + rank*S + kk]
+ * Inverse runs the same steps backwards with the same omega:
+ *   combine(inv): out-layout X -> send [dst][b][kk]; all-to-all; local(inv): recv -> [b][m]
+ * and returns the stride shard a[g + G*m] (scaled by N^-1 overall).                  */
+int pbf_ntt_shard_local_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, uint32_t world,
+                            const uint64_t* d_in, uint64_t* d_out, size_t nl, size_t batch, int inverse,
+                            void* stream);
+int pbf_ntt_shard_combine_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, uint32_t world,
+                              uint32_t rank, const uint64_t* d_in, uint64_t* d_out, size_t nl,
+                              size_t batch, int inverse, void* stream);
+
 /* ---- synthetic inputs (bench / tests) ------------------------------------- */
 /* d_out[i] = splitmix64 stream of (seed, i) with rejection of values >= modulus;
  * identical to tests/golden/gen_golden.py:splitmix_field.                     */

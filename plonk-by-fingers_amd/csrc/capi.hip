@@ -33,6 +33,30 @@ int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan**
   return 0;
 }
 
+int pbf_ctx::roots(uint64_t m, uint64_t root, uint64_t n, TwoLevel** out) {
+  auto key = std::make_tuple(m, root, n);
+  auto it = two_level.find(key);
+  if (it != two_level.end()) { *out = it->second.get(); return 0; }
+  std::unique_ptr<TwoLevel> t(new TwoLevel());
+  PBF_HIP(hipSetDevice(device));
+  int rc = make_two_level(m, root, n, t.get());
+  if (rc) return rc;
+  *out = t.get();
+  two_level[key] = std::move(t);
+  return 0;
+}
+
+// Validate (modulus, omega, G, nl) of a stride-sharded transform of N = G*nl points.
+static int shard_check(uint64_t modulus, uint64_t omega, uint32_t G, size_t nl, FieldKind* k, FieldArgs* fa) {
+  if (!field_for(modulus, k, fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
+  if (G != 2 && G != 4 && G != 8) return fail(PBF_EINVAL, "world size must be 2, 4 or 8");
+  if (nl < G || (nl & (nl - 1))) return fail(PBF_EINVAL, "per-rank size must be a power of two >= G");
+  const uint64_t N = (uint64_t)G * nl;
+  if (omega >= modulus || hpow(omega, N, modulus) != 1 || hpow(omega, N / 2, modulus) == 1)
+    return fail(PBF_EINVAL, "omega does not have order G*nl");
+  return 0;
+}
+
 extern "C" {
 
 const char* pbf_last_error(void) { return g_last_error.c_str(); }
@@ -157,6 +181,48 @@ int pbf_fill_random_u64_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t seed, uint6
   FieldArgs fa;
   if (!field_for(modulus, &k, &fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
   return launch_fill_random(fa, k, seed, d_out, count, ctx->pick(stream));
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Multi-GPU stride-sharded NTT, local step (the top log2(G) levels of
+// the even/odd recursion at fft.rs:94-96 become the rank index).
+int pbf_ntt_shard_local_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, uint32_t world, const uint64_t* d_in,
+                            uint64_t* d_out, size_t nl, size_t batch, int inverse, void* stream) {
+  if (!ctx || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  FieldKind k;
+  FieldArgs fa;
+  int rc = shard_check(modulus, omega, world, nl, &k, &fa);
+  if (rc) return rc;
+  const uint64_t wl = hpow(omega, world, modulus);  // local root, order nl
+  NttPlan* p;
+  if ((rc = ctx->plan(modulus, wl, nl, inverse, &p))) return rc;
+  hipStream_t s = ctx->pick(stream);
+  if (!inverse)
+    return run_plan_split(*p, d_in, d_out, batch, world, ctx->scratch0, ctx->scratch1, ctx->scratch2, s);
+  if ((rc = ctx->scratch2.ensure(batch * nl * 8))) return rc;
+  if ((rc = launch_shard_unsplit(d_in, (uint64_t*)ctx->scratch2.p, nl, (uint32_t)batch, world, s))) return rc;
+  return run_plan(*p, (const uint64_t*)ctx->scratch2.p, d_out, batch, ctx->scratch0, ctx->scratch1, s);
+}
+
+// Multi-GPU stride-sharded NTT, combine step (twiddle w^(g*k) + radix-G butterfly).
+int pbf_ntt_shard_combine_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, uint32_t world, uint32_t rank,
+                              const uint64_t* d_in, uint64_t* d_out, size_t nl, size_t batch, int inverse,
+                              void* stream) {
+  if (!ctx || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  if (d_in == d_out) return fail(PBF_EINVAL, "combine is out-of-place");
+  FieldKind k;
+  FieldArgs fa;
+  int rc = shard_check(modulus, omega, world, nl, &k, &fa);
+  if (rc) return rc;
+  if (rank >= world) return fail(PBF_EINVAL, "rank out of range");
+  uint64_t root = omega;
+  if (inverse && !hinv(omega, modulus, &root)) return fail(PBF_EINVAL, "omega not invertible");
+  TwoLevel* tl;
+  if ((rc = ctx->roots(modulus, root, (uint64_t)world * nl, &tl))) return rc;
+  return launch_shard_combine(k, fa, *tl, world, rank, d_in, d_out, nl, (uint32_t)batch, inverse, ctx->pick(stream));
 }
 
 }  // extern "C"

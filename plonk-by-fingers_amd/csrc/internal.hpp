@@ -78,6 +78,19 @@ int launch_pointwise_mul(FieldKind k, const FieldArgs& fa, const uint64_t* a, co
                          uint64_t count, hipStream_t s);
 int launch_poly_eval(FieldKind k, const FieldArgs& fa, const uint64_t* d_coeffs, uint64_t n, const uint64_t* d_xs,
                      uint64_t nx, uint64_t* d_ys, DevBuf& partial, hipStream_t s);
+// Multi-GPU stride-sharded NTT pieces
+struct TwoLevel {
+  DevBuf t0, t1;
+  uint64_t root = 0;
+  uint32_t bits = 0;
+};
+int make_two_level(uint64_t m, uint64_t root, uint64_t n, TwoLevel* t);
+int run_plan_split(const NttPlan& p, const uint64_t* d_in, uint64_t* d_send, size_t batch, uint32_t G, DevBuf& s0,
+                   DevBuf& s1, DevBuf& s2, hipStream_t stream);
+int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, uint32_t G, uint64_t rank,
+                         const uint64_t* in, uint64_t* out, uint64_t nl, uint32_t batch, int inverse, hipStream_t s);
+int launch_shard_unsplit(const uint64_t* recv, uint64_t* out, uint64_t nl, uint32_t batch, uint32_t G,
+                         hipStream_t s);
 int launch_fill_random(const FieldArgs& fa, FieldKind k, uint64_t seed, uint64_t* d_out, uint64_t count,
                        hipStream_t s);
 
@@ -88,7 +101,9 @@ struct pbf_ctx {
   hipStream_t stream = nullptr;
   hipStream_t user_stream = nullptr;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, int>, std::unique_ptr<pbf::NttPlan>> plans;
-  pbf::DevBuf scratch0, scratch1, io0, io1, io2, partial;
+  pbf::DevBuf scratch0, scratch1, scratch2, io0, io1, io2, partial;
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::unique_ptr<pbf::TwoLevel>> two_level;
+  int roots(uint64_t m, uint64_t root, uint64_t n, pbf::TwoLevel** out);
   hipStream_t pick(void* s) const { return s ? (hipStream_t)s : (user_stream ? user_stream : stream); }
   int plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, pbf::NttPlan** out);
 };

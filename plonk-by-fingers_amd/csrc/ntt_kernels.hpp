@@ -29,6 +29,8 @@ struct PassArgs {
   uint32_t tw_bits;
   uint32_t blocks_per_poly;
   uint32_t scale;
+  uint32_t out_split_log;  // != 0: last pass stores destination-major [n/S][batch][S], S = 2^out_split_log
+  uint32_t batch;
   FieldArgs f;
 };
 
@@ -151,7 +153,15 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* lds, const uint
         } else {
           const uint64_t j = j0 + w;
           const uint64_t ns_mask = (1ull << a.log_ns) - 1;
-          out[((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) + ((uint64_t)r << a.log_ns)] = y;
+          const uint64_t k = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) + ((uint64_t)r << a.log_ns);
+          if (a.out_split_log == 0) {
+            out[k] = y;
+          } else {
+            // multi-GPU send layout: block k/S goes to rank k/S, polynomials contiguous per rank
+            const uint64_t poly = blockIdx.x / a.blocks_per_poly;
+            const uint64_t sl = a.out_split_log;
+            a.out[((((k >> sl) * a.batch) + poly) << sl) + (k & ((1ull << sl) - 1))] = y;
+          }
         }
       }
     }
@@ -229,6 +239,98 @@ __global__ void __launch_bounds__(256) ntt_small_kernel(const uint64_t* in, uint
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
     uint64_t y = lds[i];
     dst[i] = scale ? F::mul(y, n_inv, f) : y;
+  }
+}
+
+// Multi-GPU combine (DESIGN.md "Multi-GPU"), forward direction. The global
+// transform of N = G * nl points is stride-sharded: rank g held a[g + G*m] and
+// computed Y_g = NTT_nl(a[g::G]) with root w^G. After the all-to-all, rank r holds
+// recv[g][b][kk] = Y_g[r*S + kk] (S = nl/G) and produces, for k = r*S + kk,
+//   X[k + q*nl] = sum_g w_G^(g*q) * (w^(g*k) * Y_g[k]),   q < G,
+// stored as out[b][q*S + kk]. Inverse: the same butterfly with w^-1 applied in the
+// opposite order (twiddle after the G-point DFT), see shard_split_inv_kernel.
+struct CombineArgs {
+  const uint64_t* recv;
+  uint64_t* out;
+  const uint64_t* tw0;   // two-level table of the global root (forward: w, inverse: w^-1)
+  const uint64_t* tw1;
+  uint64_t nl;           // per-rank transform size
+  uint64_t s;            // nl / G
+  uint64_t rank;
+  uint64_t n_mask;       // G*nl - 1
+  uint64_t scale;        // multiplier applied to every output (1, or G^-1 for the inverse)
+  uint32_t tw_bits;
+  uint32_t batch;
+  uint64_t wg[8];        // w_G^m (forward) or w_G^-m (inverse), m < G
+  FieldArgs f;
+};
+
+template <class F>
+__device__ __forceinline__ uint64_t tw_pow2(const uint64_t* tw0, const uint64_t* tw1, uint32_t bits, uint64_t e,
+                                            const FieldArgs& f) {
+  return F::mul(tw0[e & ((1ull << bits) - 1)], tw1[e >> bits], f);
+}
+
+template <class F, int G>
+__global__ void __launch_bounds__(256) shard_combine_kernel(CombineArgs a) {
+  const uint64_t total = a.s * a.batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / a.s, kk = id % a.s;
+    const uint64_t k = a.rank * a.s + kk;
+    uint64_t t[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      uint64_t y = a.recv[((uint64_t)g * a.batch + b) * a.s + kk];
+      const uint64_t e = ((uint64_t)g * k) & a.n_mask;
+      t[g] = (g == 0 || e == 0) ? y : F::mul(y, tw_pow2<F>(a.tw0, a.tw1, a.tw_bits, e, a.f), a.f);
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      uint64_t acc = t[0];
+#pragma unroll
+      for (int g = 1; g < G; ++g) acc = F::add(acc, F::mul(t[g], a.wg[(g * q) % G], a.f), a.f);
+      if (a.scale != 1) acc = F::mul(acc, a.scale, a.f);
+      a.out[b * a.nl + (uint64_t)q * a.s + kk] = acc;
+    }
+  }
+}
+
+// Inverse of the combine: rank r holds X (blocked, out[b][q*S + kk] layout) and
+// produces send[g][b][kk] = G^-1 * w^(-g*k) * sum_q w_G^(-g*q) X[k + q*nl].
+template <class F, int G>
+__global__ void __launch_bounds__(256) shard_split_inv_kernel(CombineArgs a) {
+  const uint64_t total = a.s * a.batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / a.s, kk = id % a.s;
+    const uint64_t k = a.rank * a.s + kk;
+    uint64_t x[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) x[q] = a.recv[b * a.nl + (uint64_t)q * a.s + kk];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      uint64_t acc = x[0];
+#pragma unroll
+      for (int q = 1; q < G; ++q) acc = F::add(acc, F::mul(x[q], a.wg[(g * q) % G], a.f), a.f);
+      const uint64_t e = ((uint64_t)g * k) & a.n_mask;
+      if (g != 0 && e != 0) acc = F::mul(acc, tw_pow2<F>(a.tw0, a.tw1, a.tw_bits, e, a.f), a.f);
+      if (a.scale != 1) acc = F::mul(acc, a.scale, a.f);
+      a.out[((uint64_t)g * a.batch + b) * a.s + kk] = acc;
+    }
+  }
+}
+
+// Gather the inverse's received blocks recv[g][b][kk] (from rank g, block of this
+// rank r) into per-polynomial natural order y[b][g*S + kk] for the local INTT.
+__global__ void shard_unsplit_kernel(const uint64_t* recv, uint64_t* out, uint64_t s, uint64_t nl, uint32_t batch,
+                                     uint32_t G) {
+  const uint64_t total = nl * batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / nl, k = id % nl;
+    const uint64_t g = k / s, kk = k % s;
+    out[id] = recv[(g * batch + b) * s + kk];
   }
 }
 

@@ -143,8 +143,105 @@ static PassFn pass_fn(int logr) {
   }
 }
 
+static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log);
+
 int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
              hipStream_t stream) {
+  return run_plan_impl(p, d_in, d_out, batch, s0, s1, stream, 0);
+}
+
+// Split a natural-order batch [b][g*S + kk] into the send layout [g][b][kk].
+__global__ void shard_split_kernel(const uint64_t* in, uint64_t* out, uint64_t s, uint64_t nl, uint32_t batch) {
+  const uint64_t total = nl * batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / nl, k = id % nl;
+    out[((k / s) * batch + b) * s + (k % s)] = in[id];
+  }
+}
+
+static uint64_t grid_for(uint64_t count) {
+  uint64_t b = (count + 255) / 256;
+  return b > 8192 ? 8192 : (b ? b : 1);
+}
+
+int run_plan_split(const NttPlan& p, const uint64_t* d_in, uint64_t* d_send, size_t batch, uint32_t G, DevBuf& s0,
+                   DevBuf& s1, DevBuf& s2, hipStream_t stream) {
+  const uint64_t S = p.n / G;
+  uint32_t sl = 0;
+  while ((1ull << sl) < S) ++sl;
+  // the last Stockham pass can store the send layout directly when S >= its W columns
+  if (!p.logr.empty() && S >= 16 && p.logr.size() >= 2) return run_plan_impl(p, d_in, d_send, batch, s0, s1, stream, sl);
+  int rc = s2.ensure(batch * p.n * 8);
+  if (rc) return rc;
+  if ((rc = run_plan_impl(p, d_in, (uint64_t*)s2.p, batch, s0, s1, stream, 0))) return rc;
+  hipLaunchKernelGGL(shard_split_kernel, dim3(grid_for(p.n * batch)), dim3(256), 0, stream, (const uint64_t*)s2.p,
+                     d_send, S, p.n, (uint32_t)batch);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_shard_unsplit(const uint64_t* recv, uint64_t* out, uint64_t nl, uint32_t batch, uint32_t G,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(shard_unsplit_kernel, dim3(grid_for(nl * batch)), dim3(256), 0, s, recv, out, nl / G, nl, batch,
+                     G);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+int make_two_level(uint64_t m, uint64_t root, uint64_t n, TwoLevel* t) {
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < n) ++log_n;
+  t->bits = (log_n + 1) / 2;
+  t->root = root;
+  std::vector<uint64_t> t0(1ull << t->bits), t1((n >> t->bits) ? (n >> t->bits) : 1);
+  uint64_t x = 1 % m;
+  for (size_t i = 0; i < t0.size(); ++i) { t0[i] = x; x = hmul(x, root, m); }
+  uint64_t step = x, y = 1 % m;
+  for (size_t i = 0; i < t1.size(); ++i) { t1[i] = y; y = hmul(y, step, m); }
+  int rc = upload(t->t0, t0);
+  return rc ? rc : upload(t->t1, t1);
+}
+
+template <class F>
+static int combine_typed(const FieldArgs& fa, const TwoLevel& tl, uint32_t G, uint64_t rank, const uint64_t* in,
+                         uint64_t* out, uint64_t nl, uint32_t batch, int inverse, hipStream_t s) {
+  CombineArgs a;
+  a.recv = in; a.out = out;
+  a.tw0 = (const uint64_t*)tl.t0.p; a.tw1 = (const uint64_t*)tl.t1.p; a.tw_bits = tl.bits;
+  a.nl = nl; a.s = nl / G; a.rank = rank; a.n_mask = (uint64_t)G * nl - 1; a.batch = batch; a.f = fa;
+  a.scale = 1;
+  if (inverse) {
+    uint64_t ginv;
+    if (!hinv(G % fa.m, fa.m, &ginv)) return fail(2, "G has no inverse");
+    a.scale = ginv;
+  }
+  for (int i = 0; i < 8; ++i) a.wg[i] = 0;
+  const uint64_t wG = hpow(tl.root, nl, fa.m);  // primitive G-th root (direction-specific)
+  uint64_t x = 1 % fa.m;
+  for (uint32_t i = 0; i < G; ++i) { a.wg[i] = x; x = hmul(x, wG, fa.m); }
+  const uint64_t total = (nl / G) * batch;
+  void (*fn)(CombineArgs) = nullptr;
+  switch (G) {
+    case 2: fn = inverse ? shard_split_inv_kernel<F, 2> : shard_combine_kernel<F, 2>; break;
+    case 4: fn = inverse ? shard_split_inv_kernel<F, 4> : shard_combine_kernel<F, 4>; break;
+    case 8: fn = inverse ? shard_split_inv_kernel<F, 8> : shard_combine_kernel<F, 8>; break;
+    default: return fail(1, "world size must be 2, 4 or 8");
+  }
+  hipLaunchKernelGGL(fn, dim3(grid_for(total)), dim3(256), 0, s, a);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, uint32_t G, uint64_t rank,
+                         const uint64_t* in, uint64_t* out, uint64_t nl, uint32_t batch, int inverse, hipStream_t s) {
+  if (k == FIELD_GOLDILOCKS) return combine_typed<Goldilocks>(fa, tl, G, rank, in, out, nl, batch, inverse, s);
+  return combine_typed<Mod32>(fa, tl, G, rank, in, out, nl, batch, inverse, s);
+}
+
+static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log) {
   if (batch == 0) return 0;
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * 8, hipMemcpyDeviceToDevice, stream));
@@ -182,6 +279,8 @@ int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t bat
     a.tw_bits = p.tw_bits;
     a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
     a.scale = (p.inverse && i == P - 1) ? 1 : 0;
+    a.out_split_log = (i == P - 1) ? split_log : 0;
+    a.batch = (uint32_t)batch;
     a.f = p.fa;
     const int nt = (W << lr) / 16;
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;

@@ -1,0 +1,94 @@
+"""Multi-GPU stride-sharded NTT — one process per GPU.
+
+A transform of N = G * nl points is sharded by coefficient stride: rank g holds
+a[g + G*m] (the top log2(G) levels of the reference's even/odd recursion,
+src/fft.rs:94-96, become the rank index). Forward, on every rank:
+
+    libpbf  pbf_ntt_shard_local_dev   local nl-point NTT (root w^G), stored in the
+                                      destination-major send layout [dst][b][kk]
+    RCCL    all_to_all_single         nl*batch/G elements to each peer over xGMI
+    libpbf  pbf_ntt_shard_combine_dev twiddle w^(g*k) + radix-G butterfly:
+                                      out[b][q*S + kk] = X[q*nl + rank*S + kk], S = nl/G
+
+The inverse runs the same three steps backwards. The exchange is the only
+collective; there is no other data-path communication.
+"""
+from __future__ import annotations
+
+import torch
+
+GOLD = 0xFFFFFFFF00000001
+
+
+class GpuShardOps:
+    """The HIP kernels of libpbf.so, enqueued on `stream` (torch's stream)."""
+
+    def __init__(self, ctx, stream: int):
+        self.ctx = ctx
+        self.stream = stream
+
+    def local(self, modulus, omega, world, src: torch.Tensor, dst: torch.Tensor, nl, batch, inverse):
+        self.ctx.shard_local_dev(modulus, omega, world, src.data_ptr(), dst.data_ptr(), nl, batch, inverse,
+                                 stream=self.stream)
+
+    def combine(self, modulus, omega, world, rank, src: torch.Tensor, dst: torch.Tensor, nl, batch, inverse):
+        self.ctx.shard_combine_dev(modulus, omega, world, rank, src.data_ptr(), dst.data_ptr(), nl, batch, inverse,
+                                   stream=self.stream)
+
+
+class ShardedNtt:
+    """Batched forward / inverse NTT of `batch` polynomials of N = world * nl points."""
+
+    def __init__(self, ops, comm, rank: int, world: int, nl: int, batch: int, modulus: int = GOLD,
+                 omega: int | None = None, device: str | torch.device = "cuda"):
+        if world not in (2, 4, 8):
+            raise ValueError("world size must be 2, 4 or 8")
+        self.ops, self.comm = ops, comm
+        self.rank, self.world, self.nl, self.batch = rank, world, nl, batch
+        self.modulus = modulus
+        self.n_global = world * nl
+        self.omega = omega if omega is not None else pow(7, (modulus - 1) // self.n_global, modulus)
+        shape = (batch * nl,)
+        self.send = torch.empty(shape, dtype=torch.int64, device=device)
+        self.recv = torch.empty(shape, dtype=torch.int64, device=device)
+
+    def _exchange(self):
+        # equal splits along dim 0: chunk r of `send` goes to rank r, chunk g of `recv` came from rank g
+        self.comm.all_to_all_single(self.recv, self.send)
+
+    def forward(self, shard: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """shard[b][m] = a_b[rank + world*m]  ->  out[b][q*S + kk] = X_b[q*nl + rank*S + kk]."""
+        self.ops.local(self.modulus, self.omega, self.world, shard, self.send, self.nl, self.batch, False)
+        self._exchange()
+        self.ops.combine(self.modulus, self.omega, self.world, self.rank, self.recv, out, self.nl, self.batch, False)
+        return out
+
+    def inverse(self, blocked: torch.Tensor, shard_out: torch.Tensor) -> torch.Tensor:
+        """Exact inverse of forward(): blocked outputs -> the stride shard of the coefficients."""
+        self.ops.combine(self.modulus, self.omega, self.world, self.rank, blocked, self.send, self.nl, self.batch,
+                         True)
+        self._exchange()
+        self.ops.local(self.modulus, self.omega, self.world, self.recv, shard_out, self.nl, self.batch, True)
+        return shard_out
+
+    # ---- layout helpers (host side, for tests and the whole-vector entry point)
+    @staticmethod
+    def output_indices(rank: int, world: int, nl: int):
+        """Global output index held at out[q*S + kk] on `rank`."""
+        s = nl // world
+        return [q * nl + rank * s + kk for q in range(world) for kk in range(s)]
+
+
+class BenchSharded:
+    """bench.py driver: synthetic shards resident in HBM, one forward per step."""
+
+    def __init__(self, ctx, dist, rank: int, world: int, log_n: int, batch: int, stream: int):
+        nl = 1 << log_n
+        self.nt = ShardedNtt(GpuShardOps(ctx, stream), dist, rank, world, nl, batch)
+        self.n_global = self.nt.n_global
+        self.shard = torch.empty(batch * nl, dtype=torch.int64, device="cuda")
+        self.out = torch.empty_like(self.shard)
+        ctx.fill_random_dev(GOLD, 0x5EED0002 + rank, self.shard.data_ptr(), batch * nl, stream=stream)
+
+    def step(self):
+        self.nt.forward(self.shard, self.out)

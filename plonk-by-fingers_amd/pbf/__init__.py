@@ -46,6 +46,10 @@ SIGNATURES = [
     ("pbf_mul_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_poly_eval_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_fill_random_u64_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _sz, _vp]),
+    ("pbf_ntt_shard_local_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _vp, _vp, _sz, _sz, ctypes.c_int,
+                                               _vp]),
+    ("pbf_ntt_shard_combine_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
+                                                 _sz, ctypes.c_int, _vp]),
 ]
 
 _lib = None
@@ -55,6 +59,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load libpbf.so (raises if it was not built: no fallback path exists)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so (SONAME
+        # libamdhip64.so.7). Loading torch first makes libpbf.so's NEEDED
+        # libamdhip64.so.7 bind to that copy instead of mapping /opt/rocm's as a
+        # second runtime (two runtimes in one process cannot both own the GPU).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(path):
             raise ImportError(f"libpbf.so not built at {path}; run __graft_entry__.build()")
         lib = ctypes.CDLL(path)
@@ -135,6 +147,17 @@ class Context:
         y = np.empty_like(x)
         _check(self.lib.pbf_poly_eval_u64(self.h, modulus, _ptr(c), c.size, _ptr(x), x.size, _ptr(y)))
         return y
+
+    # multi-GPU stride-sharded NTT pieces (include/pbf.h)
+    def shard_local_dev(self, modulus: int, omega: int, world: int, d_in: int, d_out: int, nl: int, batch: int,
+                        inverse: bool = False, stream: int = 0) -> None:
+        _check(self.lib.pbf_ntt_shard_local_dev(self.h, modulus, omega, world, _vp(d_in), _vp(d_out), nl, batch,
+                                                int(inverse), _vp(stream) if stream else None))
+
+    def shard_combine_dev(self, modulus: int, omega: int, world: int, rank: int, d_in: int, d_out: int, nl: int,
+                          batch: int, inverse: bool = False, stream: int = 0) -> None:
+        _check(self.lib.pbf_ntt_shard_combine_dev(self.h, modulus, omega, world, rank, _vp(d_in), _vp(d_out), nl,
+                                                  batch, int(inverse), _vp(stream) if stream else None))
 
     def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
         _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,

@@ -70,3 +70,12 @@ def test_last_error_callable_without_gpu():
     h = ctypes.c_void_p()
     rc = lib.pbf_ctx_create(-1, ctypes.byref(h))
     assert rc != 0  # invalid device index (or no device here) is an error code, not a crash
+
+
+def test_single_hip_runtime_in_process():
+    import pbf
+
+    pbf.load_library()
+    maps = open("/proc/self/maps").read()
+    paths = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert len(paths) == 1, paths
