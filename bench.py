@@ -97,7 +97,6 @@ def main() -> int:
     ctx = pbf.Context(local_rank)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
-    ctx.set_stream(sp)
 
     if world == 1:
         step_fn, n_global = _single_gpu(ctx, n_local, B, sp)

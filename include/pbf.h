@@ -12,9 +12,10 @@
  *     (the reference's U64Field<M> is one u64, u64field.rs:27-28). 256-bit
  *     elements are 4 x uint64_t little-endian limbs, canonical (never Montgomery).
  *   - Vectors are natural order (fft.rs:98-104 writes o[i] / o[i+len/2]).
- *   - Host-pointer entry points are synchronous: copy in, compute, copy out.
- *     `_dev` entry points take device pointers and a hipStream_t (void*; NULL =
- *     the context's stream) and only enqueue work.
+ *   - Host-pointer entry points are synchronous: copy in, compute, copy out, on
+ *     the context's host stream. `_dev` entry points take device pointers and a
+ *     hipStream_t (void*) and only enqueue work on exactly that stream (NULL = the
+ *     HIP null stream, as everywhere in HIP).
  *   - Input and output may alias (in-place is allowed).
  *   - Supported moduli for the u64 entry points: Goldilocks p = 2^64-2^32+1, and any
  *     odd M < 2^32 (the range where the reference's `(a*b)%M` in u64 is exact,
@@ -49,7 +50,8 @@ typedef struct pbf_ctx pbf_ctx;
 int pbf_ctx_create(int device, pbf_ctx** out);
 void pbf_ctx_destroy(pbf_ctx* ctx);
 const char* pbf_last_error(void);
-/* hipStream_t used when a `_dev` call passes stream == NULL. */
+/* Stream used by the synchronous host-pointer entry points (default: a private
+ * non-blocking stream created with the context). `_dev` calls ignore it.     */
 int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream);
 int pbf_device_sync(pbf_ctx* ctx);
 

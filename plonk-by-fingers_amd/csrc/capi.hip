@@ -107,7 +107,7 @@ int pbf_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64_t* 
   int rc = ctx->plan(modulus, omega, n, inverse, &p);
   if (rc) return rc;
   if (!all_canonical(in, n, modulus)) return fail(PBF_EINVAL, "input not canonical");
-  hipStream_t s = ctx->stream;
+  hipStream_t s = ctx->host_stream();
   if ((rc = ctx->io0.ensure(n * 8))) return rc;
   PBF_HIP(hipMemcpyAsync(ctx->io0.p, in, n * 8, hipMemcpyHostToDevice, s));
   rc = run_plan(*p, (const uint64_t*)ctx->io0.p, (uint64_t*)ctx->io0.p, 1, ctx->scratch0, ctx->scratch1, s);
@@ -136,7 +136,7 @@ int pbf_mul_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64
   if (!rc) rc = ctx->plan(modulus, omega, n, 1, &iv);
   if (rc) return rc;
   if (!all_canonical(a, la, modulus) || !all_canonical(b, lb, modulus)) return fail(PBF_EINVAL, "input not canonical");
-  hipStream_t s = ctx->stream;
+  hipStream_t s = ctx->host_stream();
   if ((rc = ctx->io0.ensure(2 * n * 8))) return rc;
   uint64_t* d = (uint64_t*)ctx->io0.p;  // [a | 0 ... | b | 0 ...], two polynomials of n
   PBF_HIP(hipMemsetAsync(d, 0, 2 * n * 8, s));
@@ -161,7 +161,7 @@ int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, si
   if (!all_canonical(coeffs, n, modulus) || !all_canonical(xs, nx, modulus)) return fail(PBF_EINVAL, "input not canonical");
   if (nx == 0) return PBF_OK;
   PBF_HIP(hipSetDevice(ctx->device));
-  hipStream_t s = ctx->stream;
+  hipStream_t s = ctx->host_stream();
   int rc;
   if ((rc = ctx->io0.ensure(n * 8)) || (rc = ctx->io1.ensure(nx * 8)) || (rc = ctx->io2.ensure(nx * 8))) return rc;
   PBF_HIP(hipMemcpyAsync(ctx->io0.p, coeffs, n * 8, hipMemcpyHostToDevice, s));

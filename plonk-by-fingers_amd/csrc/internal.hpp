@@ -104,6 +104,9 @@ struct pbf_ctx {
   pbf::DevBuf scratch0, scratch1, scratch2, io0, io1, io2, partial;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::unique_ptr<pbf::TwoLevel>> two_level;
   int roots(uint64_t m, uint64_t root, uint64_t n, pbf::TwoLevel** out);
-  hipStream_t pick(void* s) const { return s ? (hipStream_t)s : (user_stream ? user_stream : stream); }
+  // `_dev` entry points enqueue on exactly the stream they are given (NULL = the
+  // HIP null stream); the synchronous host-pointer entry points use host_stream().
+  static hipStream_t pick(void* s) { return (hipStream_t)s; }
+  hipStream_t host_stream() const { return user_stream ? user_stream : stream; }
   int plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, pbf::NttPlan** out);
 };

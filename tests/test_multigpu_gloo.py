@@ -105,7 +105,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_ntt_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
