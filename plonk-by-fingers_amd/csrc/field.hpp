@@ -47,6 +47,34 @@ struct Goldilocks {
   __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs&) {
     return reduce128(a * b, __umul64hi(a, b));
   }
+  // lo + t (mod p) for any lo < 2^64 and t <= (2^32-1)*EPS: one wrap/one
+  // conditional subtraction suffice (see DESIGN.md "Goldilocks arithmetic").
+  __device__ __forceinline__ static uint64_t add_small(uint64_t lo, uint64_t t) {
+    uint64_t s = lo + t;
+    uint64_t u = s + EPS;
+    return (s < t || s >= P) ? u : s;
+  }
+  // x * 2^S (mod p) for a compile-time 0 <= S < 96, x canonical.
+  template <int S>
+  __device__ __forceinline__ static uint64_t mul_pow2(uint64_t x) {
+    static_assert(S >= 0 && S < 96, "shift out of range");
+    if constexpr (S == 0) {
+      return x;
+    } else if constexpr (S <= 32) {
+      // x*2^S = lo + hi*2^64 with hi < 2^S <= 2^32, and hi*2^64 = hi*EPS (mod p)
+      const uint64_t hi = x >> (64 - S);
+      const uint64_t lo = x << S;
+      return add_small(lo, (hi << 32) - hi);
+    } else if constexpr (S < 64) {
+      return reduce128(x << S, x >> (64 - S));
+    } else {
+      // 2^S = 2^(S-64) * 2^64 and 2^64 = 2^32 - 1 (mod p)
+      const uint64_t y = mul_pow2<S - 64>(x);
+      const uint64_t z = mul_pow2<32>(y);
+      const uint64_t d = z - y;
+      return (z < y) ? d - EPS : d;
+    }
+  }
 };
 
 struct Mod32 {

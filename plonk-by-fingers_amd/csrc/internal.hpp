@@ -62,6 +62,9 @@ struct NttPlan {
   uint32_t log_n = 0;
   uint64_t n_inv = 1;
   std::vector<int> logr;   // radix per pass (empty => small kernel)
+  int e64 = -1;            // w_64 = 2^e64 for a standard Goldilocks root, else -1
+  DevBuf twfull;           // w^m for m < n (A/B only, PBF_NTT_TWFULL)
+  std::vector<std::shared_ptr<DevBuf>> twpass;  // per-pass [r][k] twiddles (empty buffer => two-level)
   int w = 16;              // columns per workgroup
   uint32_t tw_bits = 0;
   DevBuf tw0, tw1, small_tw;

@@ -22,6 +22,8 @@ struct PassArgs {
   const uint64_t* tw0;   // w^m for m < 2^tw_bits            (two-level table, low part)
   const uint64_t* tw1;   // w^(m << tw_bits) for m < n>>tw_bits (high part)
   const uint64_t* rtab;  // w_R^m = w^(m*n/R) for m < R
+  const uint64_t* twfull; // w^m for m < n (small n only; null => two-level table)
+  const uint64_t* twpass; // this pass's twiddles T[r][k] = w^((n/(Ns*R))*r*k), or null
   uint64_t n;            // transform size
   uint64_t n_inv;        // n^-1, applied to outputs when scale != 0
   uint32_t log_n;
@@ -29,20 +31,23 @@ struct PassArgs {
   uint32_t tw_bits;
   uint32_t blocks_per_poly;
   uint32_t scale;
+  uint32_t dbg;            // 0; 1 = no HBM traffic (timing), 2 = no arithmetic (timing)
+  uint32_t cur_poly;       // set per tile inside the kernel
   uint32_t out_split_log;  // != 0: last pass stores destination-major [n/S][batch][S], S = 2^out_split_log
   uint32_t batch;
   FieldArgs f;
 };
 
 // ---- compile-time helpers ----------------------------------------------------
-__host__ __device__ constexpr int ntt_nstages(int logr) { return (logr + 3) / 4; }
-// remainder radix first, then radix-16 stages
-__host__ __device__ constexpr int ntt_stage_logq(int logr, int s) {
-  return (logr % 4 == 0) ? 4 : (s == 0 ? logr % 4 : 4);
+// In-workgroup stages: radix 2^LQ (LQ = log2 of the largest register radix), the
+// remainder radix first.
+__host__ __device__ constexpr int ntt_nstages(int logr, int lq) { return (logr + lq - 1) / lq; }
+__host__ __device__ constexpr int ntt_stage_logq(int logr, int s, int lq) {
+  return (logr % lq == 0) ? lq : (s == 0 ? logr % lq : lq);
 }
-__host__ __device__ constexpr int ntt_stage_logl(int logr, int s) {
+__host__ __device__ constexpr int ntt_stage_logl(int logr, int s, int lq) {
   int l = 0;
-  for (int i = 0; i < s; ++i) l += ntt_stage_logq(logr, i);
+  for (int i = 0; i < s; ++i) l += ntt_stage_logq(logr, i, lq);
   return l;
 }
 __host__ __device__ constexpr int bitrev_c(int x, int bits) {
@@ -60,40 +65,120 @@ __device__ __forceinline__ uint64_t tw_pow(const PassArgs& a, uint64_t e) {
 }
 
 // In-register q-point DFT (decimation in frequency, natural in, bit-reversed out).
-// wq[m] = w_q^m for m < q/2 (w_q a primitive q-th root of unity).
-template <class F, int LOGQ>
-__device__ __forceinline__ void dft_reg(uint64_t* v, const uint64_t* wq, const FieldArgs& f) {
+// E < 0: twiddles from wq[m] = w_q^m (m < q/2), full multiplications.
+// E >= 0: w_q = 2^E (mod p) — Goldilocks standard roots of order <= 64 are powers
+// of two — so every twiddle is a shift-reduction; a twiddle -2^(S-96) folds its
+// sign into the butterfly's subtraction.
+template <int E, int LOGQ, int H, int A>
+struct TwShift {
+  static constexpr int Q = 1 << LOGQ;
+  static constexpr int RAW = (E * A * (Q / (2 * H))) % 192;
+  static constexpr bool NEG = RAW >= 96;
+  static constexpr int S = NEG ? RAW - 96 : RAW;
+};
+
+template <class F, int LOGQ, int E, int H, int A>
+__device__ __forceinline__ void dif_bfly(uint64_t* v, int blk, const uint64_t* wq, const FieldArgs& f) {
   constexpr int Q = 1 << LOGQ;
-#pragma unroll
-  for (int h = Q / 2; h >= 1; h >>= 1) {
-#pragma unroll
-    for (int blk = 0; blk < Q; blk += 2 * h) {
-#pragma unroll
-      for (int a = 0; a < h; ++a) {
-        uint64_t x = v[blk + a], y = v[blk + a + h];
-        v[blk + a] = F::add(x, y, f);
-        uint64_t d = F::sub(x, y, f);
-        // w_(2h)^a = w_q^(a * q/(2h))
-        v[blk + a + h] = (a == 0) ? d : F::mul(d, wq[a * (Q / (2 * h))], f);
-      }
-    }
+  const uint64_t x = v[blk + A], y = v[blk + A + H];
+  v[blk + A] = F::add(x, y, f);
+  if constexpr (A == 0) {
+    v[blk + A + H] = F::sub(x, y, f);
+  } else if constexpr (E < 0) {
+    v[blk + A + H] = F::mul(F::sub(x, y, f), wq[A * (Q / (2 * H))], f);
+  } else {
+    using T = TwShift<E, LOGQ, H, A>;
+    const uint64_t d = T::NEG ? F::sub(y, x, f) : F::sub(x, y, f);
+    v[blk + A + H] = F::template mul_pow2<T::S>(d);
   }
 }
 
+template <class F, int LOGQ, int E, int H, int A>
+__device__ __forceinline__ void dif_row(uint64_t* v, const uint64_t* wq, const FieldArgs& f) {
+  if constexpr (A < H) {
+    constexpr int Q = 1 << LOGQ;
+#pragma unroll
+    for (int blk = 0; blk < Q; blk += 2 * H) dif_bfly<F, LOGQ, E, H, A>(v, blk, wq, f);
+    dif_row<F, LOGQ, E, H, A + 1>(v, wq, f);
+  }
+}
+
+template <class F, int LOGQ, int E, int H>
+__device__ __forceinline__ void dif_levels(uint64_t* v, const uint64_t* wq, const FieldArgs& f) {
+  if constexpr (H >= 1) {
+    dif_row<F, LOGQ, E, H, 0>(v, wq, f);
+    dif_levels<F, LOGQ, E, H / 2>(v, wq, f);
+  }
+}
+
+template <class F, int LOGQ, int E>
+__device__ __forceinline__ void dft_reg(uint64_t* v, const uint64_t* wq, const FieldArgs& f) {
+  dif_levels<F, LOGQ, E, (1 << LOGQ) / 2>(v, wq, f);
+}
+
+// Exponent of w_q = 2^E given w_64 = 2^E64 (E64 < 0: table twiddles).
+__host__ __device__ constexpr int sub_root_exp(int e64, int logq) {
+  return e64 < 0 ? -1 : (e64 * (64 >> logq)) % 192;
+}
+
+// Workgroup barrier of the in-tile stages. DB (LDS-DMA double-buffered) kernels use a
+// raw s_barrier with lgkmcnt(0) only, so the next tile's LDS-DMA stays in flight
+// (hipcc's __syncthreads() would emit vmcnt(0) and drain it: guide "Pipelining
+// across barriers").
+template <bool DB>
+__device__ __forceinline__ void tile_barrier() {
+  if constexpr (DB) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+// LDS-DMA of one tile: R rows x W columns of the pass input into buf ([r][w] image,
+// 16-B chunks, lane-linear destination, per-lane global source).
+template <int LOGR, int W, int NT>
+__device__ __forceinline__ void tile_dma(uint64_t* buf, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
+  constexpr int R = 1 << LOGR;
+  constexpr int CPR = W / 2;               // 16-B chunks per row
+  constexpr int CHUNKS = R * CPR;
+  const int wave = t >> 6, lane = t & 63;
+  const uint64_t stride = a.n >> LOGR;
+#pragma unroll
+  for (int q0 = wave * 64; q0 < CHUNKS; q0 += NT) {
+    const int q = q0 + lane;
+    const int row = q / CPR, col = 2 * (q % CPR);
+    const uint64_t* g = in + (j0 + col) + (uint64_t)row * stride;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)(buf + 2 * q0), 16, 0, 0);
+  }
+}
+
+struct NextTile {
+  bool valid;
+  uint64_t* buf;
+  const uint64_t* in;
+  uint64_t j0;
+};
+
 // One register/LDS stage S of the in-workgroup R-point Stockham (radix Q = 2^logq).
-template <class F, int LOGR, int W, int NT, int S>
-__device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* lds, const uint64_t* wq, const PassArgs& a,
-                                          const uint64_t* in, uint64_t* out, uint64_t j0, int t) {
+// Stage 0 reads the raw tile (registers v when !DB, the LDS image `buf` when DB) and
+// applies the pass twiddle; later stages read the exchange buffer and apply the stage
+// twiddle from `rt` (LDS when DB).
+template <class F, int LOGR, int W, int NT, int LQ, int E64, bool DB, int S>
+__device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint64_t* rt, const uint64_t* wq,
+                                          const PassArgs& a, uint64_t* out, uint64_t j0, int t,
+                                          const NextTile& nx) {
   constexpr int R = 1 << LOGR;
   constexpr int PER = (R * W) / NT;
-  constexpr int NST = ntt_nstages(LOGR);
-  constexpr int LOGQ = ntt_stage_logq(LOGR, S);
+  constexpr int NST = ntt_nstages(LOGR, LQ);
+  constexpr int LOGQ = ntt_stage_logq(LOGR, S, LQ);
   constexpr int Q = 1 << LOGQ;
-  constexpr int L = 1 << ntt_stage_logl(LOGR, S);
+  constexpr int L = 1 << ntt_stage_logl(LOGR, S, LQ);
   constexpr int NSUB = PER / Q;
   constexpr bool LAST = (S == NST - 1);
   const uint64_t n = a.n;
-  // ---- gather inputs (stage 0 straight from HBM with the pass pre-twiddle)
+  // ---- gather inputs
 #pragma unroll
   for (int u = 0; u < NSUB; ++u) {
     const int sub = t + NT * u;
@@ -103,37 +188,41 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* lds, const uint
       const int r = i + c * (R / Q);
       uint64_t x;
       if constexpr (S == 0) {
-        x = in[(j0 + w) + (uint64_t)r * (n >> LOGR)];
+        x = DB ? buf[r * W + w] : v[u * Q + c];
         if (a.log_ns > 0) {
           const uint64_t k = (j0 + w) & ((1ull << a.log_ns) - 1);
           const uint64_t e = (((uint64_t)r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1);
-          if (e) x = F::mul(x, tw_pow<F>(a, e), a.f);
+          if (a.twpass) {
+            // per-pass table [r][k] (k contiguous across lanes: one coalesced load)
+            if (e) x = F::mul(x, a.twpass[((uint64_t)r << a.log_ns) + k], a.f);
+          } else if (e) {
+            x = F::mul(x, a.twfull ? a.twfull[e] : tw_pow<F>(a, e), a.f);
+          }
         }
       } else {
-        x = lds[r * W + w];
+        x = buf[r * W + w];
         const int k = i % L;  // stage twiddle w_(L*Q)^(c*k) = w_R^((R/(L*Q))*c*k)
-        if (c != 0 && k != 0) x = F::mul(x, a.rtab[(R / (L * Q)) * c * k], a.f);
+        if (c != 0 && k != 0) x = F::mul(x, rt[(R / (L * Q)) * c * k], a.f);
       }
       v[u * Q + c] = x;
     }
   }
-  // ---- radix-Q DFTs in registers
+  if constexpr (DB && S == 0) {
+    // this tile's pass-twiddle loads are consumed: start the next tile's LDS-DMA now
+    if (nx.valid) tile_dma<LOGR, W, NT>(nx.buf, a, nx.in, nx.j0, t);
+  }
+  // ---- radix-Q DFTs in registers (wq[m] = w_QMAX^m; w_Q = w_QMAX^(QMAX/Q))
+  constexpr int QMAX = 1 << LQ;
 #pragma unroll
   for (int u = 0; u < NSUB; ++u) {
-    if constexpr (LOGQ == 4) {
-      dft_reg<F, 4>(v + u * Q, wq, a.f);
-    } else if constexpr (LOGQ == 3) {
-      const uint64_t w8[4] = {wq[0], wq[2], wq[4], wq[6]};
-      dft_reg<F, 3>(v + u * Q, w8, a.f);
-    } else if constexpr (LOGQ == 2) {
-      const uint64_t w4[2] = {wq[0], wq[4]};
-      dft_reg<F, 2>(v + u * Q, w4, a.f);
-    } else {
-      const uint64_t w2[1] = {wq[0]};
-      dft_reg<F, 1>(v + u * Q, w2, a.f);
+    uint64_t wloc[Q / 2 > 0 ? Q / 2 : 1];
+    if constexpr (E64 < 0) {
+#pragma unroll
+      for (int m = 0; m < Q / 2; ++m) wloc[m] = wq[m * (QMAX / Q)];
     }
+    if (!(a.dbg & 2)) dft_reg<F, LOGQ, sub_root_exp(E64, LOGQ)>(v + u * Q, wloc, a.f);
   }
-  if constexpr (S > 0) __syncthreads();  // all reads of the exchange buffer are done
+  if constexpr (S > 0 || DB) tile_barrier<DB>();  // all reads of the exchange buffer are done
   // ---- scatter outputs
 #pragma unroll
   for (int u = 0; u < NSUB; ++u) {
@@ -145,41 +234,81 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* lds, const uint
       uint64_t y = v[u * Q + bitrev_c(d, LOGQ)];
       const int r = (i / L) * L * Q + k + d * L;  // Stockham output slot
       if constexpr (!LAST) {
-        lds[r * W + w] = y;
+        buf[r * W + w] = y;
       } else {
         if (a.scale) y = F::mul(y, a.n_inv, a.f);
         if (a.log_ns == 0) {
-          lds[w * (R + 1) + r] = y;  // transposed image, stored linearly by the caller
+          buf[w * (R + 1) + r] = y;  // transposed image, stored linearly by the caller
         } else {
           const uint64_t j = j0 + w;
           const uint64_t ns_mask = (1ull << a.log_ns) - 1;
-          const uint64_t k = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) + ((uint64_t)r << a.log_ns);
-          if (a.out_split_log == 0) {
-            out[k] = y;
+          const uint64_t kk = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) + ((uint64_t)r << a.log_ns);
+          if (a.dbg & 1) {
+            if (y == 0x123456789ull) out[kk] = y;  // keeps the arithmetic live, never true in practice
+          } else if (a.out_split_log == 0) {
+            out[kk] = y;
           } else {
-            // multi-GPU send layout: block k/S goes to rank k/S, polynomials contiguous per rank
-            const uint64_t poly = blockIdx.x / a.blocks_per_poly;
+            // multi-GPU send layout: block kk/S goes to rank kk/S, polynomials contiguous per rank
+            const uint64_t poly = a.cur_poly;
             const uint64_t sl = a.out_split_log;
-            a.out[((((k >> sl) * a.batch) + poly) << sl) + (k & ((1ull << sl) - 1))] = y;
+            a.out[((((kk >> sl) * a.batch) + poly) << sl) + (kk & ((1ull << sl) - 1))] = y;
           }
         }
       }
     }
   }
   if constexpr (!LAST) {
-    __syncthreads();
-    ntt_stage<F, LOGR, W, NT, S + 1>(v, lds, wq, a, in, out, j0, t);
+    tile_barrier<DB>();
+    ntt_stage<F, LOGR, W, NT, LQ, E64, DB, S + 1>(v, buf, rt, wq, a, out, j0, t, nx);
   }
 }
 
-// One Stockham pass over HBM. NT threads, W columns of R = 2^LOGR points each.
-template <class F, int LOGR, int W, int NT>
+// Store the first pass's transposed [w][r] image: outputs y[j0*R .. (j0+W)*R) are contiguous.
+template <int LOGR, int W, int NT, bool DB>
+__device__ __forceinline__ void store_transposed(const uint64_t* buf, uint64_t* out, uint64_t j0, int t,
+                                                 const PassArgs& a) {
+  constexpr int R = 1 << LOGR;
+  constexpr int PER = (R * W) / NT;
+  tile_barrier<DB>();
+  uint64_t* o = out + j0 * R;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int m = t + NT * u;
+    const uint64_t y = buf[(m / R) * (R + 1) + (m % R)];
+    if (!(a.dbg & 1) || y == 0x123456789ull) o[m] = y;
+  }
+}
+
+// Raw stage-0 inputs of one tile into registers (the same thread -> element map as stage 0).
+template <int LOGR, int W, int NT, int LQ>
+__device__ __forceinline__ void tile_load(uint64_t* v, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
+  constexpr int R = 1 << LOGR;
+  constexpr int PER = (R * W) / NT;
+  constexpr int Q = 1 << ntt_stage_logq(LOGR, 0, LQ);
+#pragma unroll
+  for (int u = 0; u < PER / Q; ++u) {
+    const int sub = t + NT * u;
+    const int w = sub % W, i = sub / W;
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+      const int r = i + c * (R / Q);
+      v[u * Q + c] = (a.dbg & 1) ? (uint64_t)(t * 0x9E3779B9u + r) * 0x100000001ull
+                                 : in[(j0 + w) + (uint64_t)r * (a.n >> LOGR)];
+    }
+  }
+}
+
+// One Stockham pass over HBM, one tile per workgroup (tiles too large to double-buffer).
+// NT threads, W columns of R = 2^LOGR points, register sub-DFTs of radix up to 2^LQ;
+// E64 >= 0 selects shift twiddles for a standard Goldilocks root (w_64 = 2^E64).
+template <class F, int LOGR, int W, int NT, int LQ, int E64>
 __global__ void __launch_bounds__(NT) ntt_pass_kernel(PassArgs a) {
   constexpr int R = 1 << LOGR;
   constexpr int E = R * W;
   constexpr int PER = E / NT;
-  static_assert(LOGR >= 4, "radix-16 register sub-DFTs need R >= 16");
-  static_assert(PER >= 16 && PER % 16 == 0, "each thread must own whole radix-16 sub-DFTs");
+  constexpr int QMAX = 1 << LQ;
+  static_assert(LOGR >= LQ, "register sub-DFTs need R >= 2^LQ");
+  static_assert(PER >= QMAX && PER % QMAX == 0, "each thread must own whole register sub-DFTs");
   static_assert(E <= 16384, "LDS budget: 128 KiB of elements per workgroup");
   // +W pad keeps the transposed [w][r] image of the first pass bank-conflict free
   __shared__ uint64_t lds[E + W];
@@ -189,23 +318,73 @@ __global__ void __launch_bounds__(NT) ntt_pass_kernel(PassArgs a) {
   const uint64_t* in = a.in + (uint64_t)poly * a.n;
   uint64_t* out = a.out + (uint64_t)poly * a.n;
   const int t = threadIdx.x;
+  PassArgs b = a;
+  b.cur_poly = poly;
 
+  uint64_t wq[QMAX / 2];  // w_QMAX^m (table-twiddle variant only)
+  if constexpr (E64 < 0) {
+#pragma unroll
+    for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
+  }
   uint64_t v[PER];
-  uint64_t wq[8];  // w_16^m, m < 8 (the roots for q < 16 are sub-powers)
-#pragma unroll
-  for (int m = 0; m < 8; ++m) wq[m] = a.rtab[m * (R / 16)];
+  tile_load<LOGR, W, NT, LQ>(v, a, in, j0, t);
+  const NextTile none{false, nullptr, nullptr, 0};
+  ntt_stage<F, LOGR, W, NT, LQ, E64, false, 0>(v, lds, a.rtab, wq, b, out, j0, t, none);
+  if (a.log_ns == 0) store_transposed<LOGR, W, NT, false>(lds, out, j0, t, a);
+}
 
-  ntt_stage<F, LOGR, W, NT, 0>(v, lds, wq, a, in, out, j0, t);
+// Double-buffered persistent pass (tiles of <= 64 KiB): each workgroup walks tiles
+// blockIdx.x, +gridDim.x, ...; the next tile is LDS-DMA'd into the other buffer while
+// this one is computed, so HBM reads overlap the arithmetic. Stage twiddles live in LDS.
+template <class F, int LOGR, int W, int NT, int LQ, int E64>
+__global__ void __launch_bounds__(NT) ntt_pass_db_kernel(PassArgs a) {
+  constexpr int R = 1 << LOGR;
+  constexpr int E = R * W;
+  constexpr int PER = E / NT;
+  constexpr int QMAX = 1 << LQ;
+  constexpr int BUF = E + W;  // element image (+pad for the transposed first-pass image)
+  static_assert(LOGR >= LQ && PER >= QMAX && PER % QMAX == 0, "bad tile shape");
+  static_assert(PER <= 63, "counted vmcnt must fit");
+  static_assert(2 * BUF + R <= 20480, "LDS budget: two tiles + stage twiddles in 160 KiB");
+  __shared__ __attribute__((aligned(16))) uint64_t lds[2 * BUF + R];
+  uint64_t* rt = lds + 2 * BUF;
 
-  if (a.log_ns == 0) {
-    // first pass: this workgroup's outputs are y[j0*R .. (j0+W)*R), contiguous
-    __syncthreads();
-    uint64_t* o = out + j0 * R;
+  const int t = threadIdx.x;
+  const uint32_t total = a.blocks_per_poly * a.batch;
+  uint32_t blk = blockIdx.x;
+  if (blk >= total) return;
+  for (int i = t; i < R; i += NT) rt[i] = a.rtab[i];
+  uint64_t wq[QMAX / 2];
+  if constexpr (E64 < 0) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int m = t + NT * u;
-      o[m] = lds[(m / R) * (R + 1) + (m % R)];
-    }
+    for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
+  }
+  // prologue: first tile
+  tile_dma<LOGR, W, NT>(lds, a, a.in + (uint64_t)(blk / a.blocks_per_poly) * a.n,
+                        (uint64_t)(blk % a.blocks_per_poly) * W, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tile_barrier<true>();
+  int cur = 0;
+  for (; blk < total; blk += gridDim.x) {
+    const uint32_t poly = blk / a.blocks_per_poly;
+    const uint64_t j0 = (uint64_t)(blk % a.blocks_per_poly) * W;
+    uint64_t* out = a.out + (uint64_t)poly * a.n;
+    PassArgs b = a;
+    b.cur_poly = poly;
+    const uint32_t nb = blk + gridDim.x;
+    NextTile nx;
+    nx.valid = nb < total;
+    nx.buf = lds + (cur ^ 1) * BUF;
+    nx.in = a.in + (uint64_t)(nb / a.blocks_per_poly) * a.n;
+    nx.j0 = (uint64_t)(nb % a.blocks_per_poly) * W;
+    uint64_t* buf = lds + cur * BUF;
+    uint64_t v[PER];
+    ntt_stage<F, LOGR, W, NT, LQ, E64, true, 0>(v, buf, rt, wq, b, out, j0, t, nx);
+    if (a.log_ns == 0) store_transposed<LOGR, W, NT, true>(buf, out, j0, t, a);
+    // retire the next tile's LDS-DMA (issued before this tile's PER output stores)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    tile_barrier<true>();
+    cur ^= 1;
   }
 }
 

@@ -76,7 +76,6 @@ static std::vector<int> default_passes(uint32_t log_n) {
   return v;
 }
 
-static int cols_for(int logr) { return logr <= 10 ? 16 : (logr == 11 ? 8 : 4); }
 
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   if (!field_for(m, &p->kind, &p->fa)) return fail(5, "unsupported modulus");
@@ -103,6 +102,21 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   }
   p->logr = default_passes(log_n);
   p->tw_bits = (log_n + 1) / 2;
+  // standard Goldilocks root => shift twiddles in the register sub-DFTs
+  p->e64 = -1;
+  if (p->kind == FIELD_GOLDILOCKS && !getenv("PBF_NTT_NO_SHIFT")) {
+    const uint64_t w64 = hpow(w, n / 64, m);
+    if (w64 == hpow(2, 39, m)) p->e64 = 39;
+    else if (w64 == hpow(2, 153, m)) p->e64 = 153;
+  }
+  // scattered full twiddle table: measured slower than the two-level table (kept for A/B)
+  if (log_n <= 22 && getenv("PBF_NTT_TWFULL")) {
+    std::vector<uint64_t> tf(n);
+    uint64_t z = 1 % m;
+    for (uint64_t i = 0; i < n; ++i) { tf[i] = z; z = hmul(z, w, m); }
+    int rc0 = upload(p->twfull, tf);
+    if (rc0) return rc0;
+  }
   std::vector<uint64_t> t0(1ull << p->tw_bits), t1(n >> p->tw_bits);
   uint64_t x = 1 % m;
   for (size_t i = 0; i < t0.size(); ++i) { t0[i] = x; x = hmul(x, w, m); }
@@ -112,6 +126,28 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   int rc = upload(p->tw0, t0);
   if (!rc) rc = upload(p->tw1, t1);
   if (rc) return rc;
+  // per-pass [r][k] twiddle tables while R*Ns <= 2^22 (shared by every polynomial of a
+  // batch, so they stay in the Infinity Cache); larger passes use the two-level table
+  {
+    uint64_t ns = 1;
+    for (size_t i = 0; i < p->logr.size(); ++i) {
+      const uint64_t R = 1ull << p->logr[i];
+      auto b = std::make_shared<DevBuf>();
+      if (ns > 1 && R * ns <= (1ull << 22) && !getenv("PBF_NTT_TWO_LEVEL")) {
+        const uint64_t step = n / (ns * R);
+        std::vector<uint64_t> t(R * ns);
+        for (uint64_t r = 0; r < R; ++r) {
+          const uint64_t wr = hpow(w, step * r, m);  // (w^(step*r))^k
+          uint64_t z = 1 % m;
+          for (uint64_t kk = 0; kk < ns; ++kk) { t[r * ns + kk] = z; z = hmul(z, wr, m); }
+        }
+        int rc1 = upload(*b, t);
+        if (rc1) return rc1;
+      }
+      p->twpass.push_back(b);
+      ns *= R;
+    }
+  }
   for (int lr : p->logr) {
     uint64_t R = 1ull << lr;
     uint64_t wr = hpow(w, n / R, m);
@@ -129,18 +165,65 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
 // ---------------------------------------------------------------- dispatch
 typedef void (*PassFn)(PassArgs);
 
-template <class F>
-static PassFn pass_fn(int logr) {
-  switch (logr) {
-    case 6: return ntt_pass_kernel<F, 6, 16, 64>;
-    case 7: return ntt_pass_kernel<F, 7, 16, 128>;
-    case 8: return ntt_pass_kernel<F, 8, 16, 256>;
-    case 9: return ntt_pass_kernel<F, 9, 16, 512>;
-    case 10: return ntt_pass_kernel<F, 10, 16, 1024>;
-    case 11: return ntt_pass_kernel<F, 11, 8, 1024>;
-    case 12: return ntt_pass_kernel<F, 12, 4, 1024>;
-    default: return nullptr;
+static int cols_for(int logr) {
+  const char* env = getenv("PBF_NTT_WIDE");  // A/B: widest tile (W*R = 16384) for small radices
+  if (env && logr <= 9) return 16384 >> logr > 64 ? 64 : 16384 >> logr;
+  return logr <= 10 ? 16 : (logr == 11 ? 8 : 4);
+}
+
+// Kernel configuration of one pass: W columns, register radix 2^LQ, double-buffered
+// persistent (DB) or one tile per workgroup.
+struct PassCfg {
+  int w, lq, db;
+};
+
+static PassCfg pass_cfg(int logr) {
+  // default: one 128-KiB tile per workgroup (measured faster than the LDS-DMA
+  // double-buffered kernel, whose two tiles halve occupancy: DESIGN.md "NTT")
+  PassCfg def = PassCfg{cols_for(logr), 4, 0};
+  const char* env = getenv("PBF_NTT_CFG");  // "W,LQ,DB" e.g. "16,4,0" (benchmarking override)
+  if (env && *env) {
+    int v[3] = {def.w, def.lq, def.db}, i = 0;
+    for (const char* c = env; *c && i < 3;) {
+      v[i++] = atoi(c);
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+    return PassCfg{v[0], v[1], v[2]};
   }
+  return def;
+}
+
+#define PBF_PASS(F, LR, W, LQ, E)                                                              \
+  if (logr == LR && c.w == W && c.lq == LQ && !c.db) return ntt_pass_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+#define PBF_PASS_DB(F, LR, W, LQ, E)                                                           \
+  if (logr == LR && c.w == W && c.lq == LQ && c.db) return ntt_pass_db_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+
+template <class F, int E>
+static PassFn pass_fn_e(int logr, PassCfg c) {
+  PBF_PASS_DB(F, 6, 64, 4, E)
+  PBF_PASS_DB(F, 7, 64, 4, E)
+  PBF_PASS_DB(F, 8, 32, 4, E)
+  PBF_PASS_DB(F, 9, 16, 4, E)
+  PBF_PASS_DB(F, 10, 8, 4, E)
+  PBF_PASS(F, 10, 16, 4, E)
+  PBF_PASS(F, 11, 8, 4, E)
+  PBF_PASS(F, 12, 4, 4, E)
+  PBF_PASS(F, 8, 64, 4, E)
+  PBF_PASS(F, 9, 32, 4, E)
+  // single-tile fallbacks for every radix (used when a DB shape is not instantiated)
+  PBF_PASS(F, 6, 16, 4, E)
+  PBF_PASS(F, 7, 16, 4, E)
+  PBF_PASS(F, 8, 16, 4, E)
+  PBF_PASS(F, 9, 16, 4, E)
+  return nullptr;
+}
+
+static PassFn pass_fn(FieldKind k, int e64, int logr, PassCfg c) {
+  if (k == FIELD_MOD32) return pass_fn_e<Mod32, -1>(logr, c);
+  if (e64 == 39) return pass_fn_e<Goldilocks, 39>(logr, c);
+  if (e64 == 153) return pass_fn_e<Goldilocks, 153>(logr, c);
+  return pass_fn_e<Goldilocks, -1>(logr, c);
 }
 
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
@@ -240,6 +323,29 @@ int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, u
   return combine_typed<Mod32>(fa, tl, G, rank, in, out, nl, batch, inverse, s);
 }
 
+// Persistent grid: every resident workgroup slot once (blocks per CU from the
+// occupancy query x CUs), never more than there are tiles.
+static uint32_t persistent_grid(PassFn fn, int nt, uint64_t tiles) {
+  static std::map<std::pair<PassFn, int>, uint32_t> cache;
+  auto key = std::make_pair(fn, nt);
+  auto it = cache.find(key);
+  uint32_t slots;
+  if (it != cache.end()) {
+    slots = it->second;
+  } else {
+    int dev = 0, cus = 256, per_cu = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, nt, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    slots = (uint32_t)(cus * per_cu);
+    cache[key] = slots;
+  }
+  const char* env = getenv("PBF_NTT_GRID_MULT");  // A/B: oversubscribe the persistent grid
+  if (env) slots *= (uint32_t)atoi(env);
+  return (uint32_t)(tiles < slots ? tiles : slots);
+}
+
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log) {
   if (batch == 0) return 0;
@@ -265,13 +371,23 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   uint32_t log_ns = 0;
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
-    const int W = cols_for(lr);
+    PassCfg cfg = pass_cfg(lr);
+    PassFn fn = pass_fn(p.kind, p.e64, lr, cfg);
+    for (int w : {16, 8, 4}) {  // robust fallback: any instantiated single-tile shape
+      if (fn) break;
+      cfg = PassCfg{w, 4, 0};
+      fn = pass_fn(p.kind, p.e64, lr, cfg);
+    }
+    if (!fn) return fail(1, "no kernel for this radix");
+    const int W = cfg.w;
     PassArgs a;
     a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p);
     a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p);
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;
     a.rtab = (const uint64_t*)p.rtab[i]->p;
+    a.twfull = (const uint64_t*)p.twfull.p;
+    a.twpass = (const uint64_t*)p.twpass[i]->p;
     a.n = p.n;
     a.n_inv = p.n_inv;
     a.log_n = p.log_n;
@@ -280,14 +396,14 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
     a.scale = (p.inverse && i == P - 1) ? 1 : 0;
     a.out_split_log = (i == P - 1) ? split_log : 0;
+    a.dbg = getenv("PBF_NTT_DBG") ? (uint32_t)atoi(getenv("PBF_NTT_DBG")) : 0;
     a.batch = (uint32_t)batch;
     a.f = p.fa;
-    const int nt = (W << lr) / 16;
+    const int nt = (W << lr) >> cfg.lq;
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
     if (blocks > 0x7fffffffull) return fail(1, "batch too large");
-    PassFn fn = (p.kind == FIELD_GOLDILOCKS) ? pass_fn<Goldilocks>(lr) : pass_fn<Mod32>(lr);
-    if (!fn) return fail(1, "no kernel for this radix");
-    hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(nt), 0, stream, a);
+    const uint32_t grid = cfg.db ? persistent_grid(fn, nt, blocks) : (uint32_t)blocks;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(nt), 0, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;
   }
