@@ -97,6 +97,21 @@ int pbf_ntt_shard_combine_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, ui
                               uint32_t rank, const uint64_t* d_in, uint64_t* d_out, size_t nl,
                               size_t batch, int inverse, void* stream);
 
+/* ---- BN254 scalar field (BASELINE config 3) ----------------------------------
+ * r = 21888242871839275222246405745257275088548364400416034343698204186575808495617,
+ * elements 4 x uint64_t little-endian, canonical; n a power of two <= 2^28.
+ * The reference has no 256-bit field: these are fft.rs:66-78 and fft.rs:109-132
+ * instantiated for the field SURVEY.md §0.5 picks for configs 3-5.              */
+int pbf_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* in, uint64_t* out, size_t n,
+                  int inverse);
+int pbf_ntt_fr256_batch_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_in, uint64_t* d_out,
+                            size_t n, size_t batch, int inverse, void* stream);
+int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, size_t la,
+                      const uint64_t* b, size_t lb, uint64_t* out);
+/* batched device mul_ntt: a, b already zero-padded to n = la + lb; out = batch x n  */
+int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_a, const uint64_t* d_b,
+                          uint64_t* d_out, size_t n, size_t batch, void* stream);
+
 /* ---- synthetic inputs (bench / tests) ------------------------------------- */
 /* d_out[i] = splitmix64 stream of (seed, i) with rejection of values >= modulus;
  * identical to tests/golden/gen_golden.py:splitmix_field.                     */

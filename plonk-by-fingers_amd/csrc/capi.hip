@@ -19,6 +19,7 @@ static bool all_canonical(const uint64_t* v, size_t n, uint64_t m) {
 }  // namespace pbf
 
 using namespace pbf;
+void pbf_internal_drop_plans256(const void* ctx);  // ntt256.hip
 
 int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan** out) {
   auto key = std::make_tuple(m, omega, n, inverse ? 1 : 0);
@@ -80,6 +81,7 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
 
 void pbf_ctx_destroy(pbf_ctx* ctx) {
   if (!ctx) return;
+  pbf_internal_drop_plans256(ctx);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamDestroy(ctx->stream);

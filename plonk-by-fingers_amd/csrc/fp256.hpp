@@ -1,0 +1,158 @@
+// 256-bit prime fields for the BN254 path (BASELINE configs 3-5): Fr (the scalar field,
+// NTT / polynomial multiply) and Fq (the base field of G1, MSM).
+//
+// At the ABI an element is 4 x uint64_t little-endian, canonical. Inside
+// kernels elements are in Montgomery form (R = 2^256) as 8 x 32-bit limbs, so the
+// 32x32+64 `v_mad_u64_u32` is the multiply-accumulate primitive of the CIOS product.
+// Both moduli are < 2^254, so a CIOS result is < 2p and one conditional subtraction
+// keeps every value canonical (bit-exact parity needs no lazy state).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "field.hpp"
+
+namespace pbf {
+
+struct U256 {
+  uint32_t w[8];
+};
+
+struct Bn254FrParams {  // r = 0x30644e72...f0000001
+  static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t NP = 0xefffffffu;  // -p^-1 mod 2^32
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+};
+
+struct Bn254FqParams {  // q = 0x30644e72...d87cfd47
+  static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t NP = 0xe4866389u;
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+};
+
+template <class Prm>
+struct Fp256 {
+  typedef U256 T;
+
+  __host__ __device__ __forceinline__ static bool geq_p(const U256& a) {
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      if (a.w[i] != Prm::P[i]) return a.w[i] > Prm::P[i];
+    }
+    return true;
+  }
+  // a - p (assumes a >= p)
+  __host__ __device__ __forceinline__ static U256 sub_p(const U256& a) {
+    U256 r;
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t d = (uint64_t)a.w[i] - Prm::P[i] - borrow;
+      r.w[i] = (uint32_t)d;
+      borrow = (d >> 63) & 1;
+    }
+    return r;
+  }
+  __host__ __device__ __forceinline__ static U256 add(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    U256 s;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t t = (uint64_t)a.w[i] + b.w[i] + c;
+      s.w[i] = (uint32_t)t;
+      c = t >> 32;
+    }
+    // a, b < p < 2^254: no carry out of 256 bits
+    return geq_p(s) ? sub_p(s) : s;
+  }
+  __host__ __device__ __forceinline__ static U256 sub(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    U256 d;
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t t = (uint64_t)a.w[i] - b.w[i] - borrow;
+      d.w[i] = (uint32_t)t;
+      borrow = (t >> 63) & 1;
+    }
+    if (borrow) {  // d + p
+      uint64_t c = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint64_t t = (uint64_t)d.w[i] + Prm::P[i] + c;
+        d.w[i] = (uint32_t)t;
+        c = t >> 32;
+      }
+    }
+    return d;
+  }
+  // CIOS Montgomery product a*b*2^-256 mod p.
+  __host__ __device__ __forceinline__ static U256 mul(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    uint32_t t[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t C = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint64_t s = (uint64_t)a.w[j] * b.w[i] + t[j] + C;
+        t[j] = (uint32_t)s;
+        C = s >> 32;
+      }
+      uint64_t s = (uint64_t)t[8] + C;
+      t[8] = (uint32_t)s;
+      t[9] = (uint32_t)(s >> 32);
+      const uint32_t m = t[0] * Prm::NP;
+      s = (uint64_t)m * Prm::P[0] + t[0];
+      C = s >> 32;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) {
+        s = (uint64_t)m * Prm::P[j] + t[j] + C;
+        t[j - 1] = (uint32_t)s;
+        C = s >> 32;
+      }
+      s = (uint64_t)t[8] + C;
+      t[7] = (uint32_t)s;
+      t[8] = t[9] + (uint32_t)(s >> 32);
+    }
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = t[i];
+    return geq_p(r) ? sub_p(r) : r;
+  }
+  __host__ __device__ __forceinline__ static U256 r2() {
+    U256 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v.w[i] = Prm::R2[i];
+    return v;
+  }
+  __host__ __device__ __forceinline__ static U256 one_plain() {
+    U256 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v.w[i] = i == 0 ? 1u : 0u;
+    return v;
+  }
+  // canonical <-> Montgomery (the ABI never sees Montgomery form)
+  __host__ __device__ __forceinline__ static U256 to_mont(const U256& a) { return mul(a, r2()); }
+  __host__ __device__ __forceinline__ static U256 from_mont(const U256& a) { return mul(a, one_plain()); }
+  __host__ __device__ __forceinline__ static bool is_zero(const U256& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i];
+    return o == 0;
+  }
+  __host__ __device__ __forceinline__ static bool eq(const U256& a, const U256& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i] ^ b.w[i];
+    return o == 0;
+  }
+};
+
+typedef Fp256<Bn254FrParams> Fr;
+typedef Fp256<Bn254FqParams> Fq;
+
+}  // namespace pbf

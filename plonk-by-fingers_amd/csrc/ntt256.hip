@@ -1,0 +1,542 @@
+// BN254-Fr NTT and mul_ntt (BASELINE config 3: "Polynomial multiply via NTT,
+// 256-bit scalar field, degree 2^22"). Same Stockham decomposition as the u64 path
+// (ntt_kernels.hpp): P passes of radix R over HBM, an in-LDS Stockham of radix-2^LQ
+// register sub-DFTs per workgroup; elements are 32 B, Montgomery form inside the
+// kernels (canonical at the ABI: converted on the first pass's load and the last
+// pass's store). Replaces fft.rs:66-78 and fft.rs:109-132 for the 256-bit field.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "../../include/pbf.h"
+#include "fp256.hpp"
+#include "internal.hpp"
+
+namespace pbf {
+
+struct Pass256 {
+  const U256* in;
+  U256* out;
+  const U256* rtab;    // w_R^m (Montgomery), m < R
+  const U256* twpass;  // [r][k] pass twiddles (Montgomery) or null
+  const U256* tw0;     // two-level table (Montgomery)
+  const U256* tw1;
+  U256 n_inv;          // Montgomery form
+  uint64_t n;
+  uint32_t log_n, log_ns, tw_bits, blocks_per_poly, batch;
+  uint32_t conv_in, conv_out, scale;
+};
+
+__host__ __device__ constexpr int st_logq(int logr, int s, int lq) {
+  return (logr % lq == 0) ? lq : (s == 0 ? logr % lq : lq);
+}
+__host__ __device__ constexpr int st_logl(int logr, int s, int lq) {
+  int l = 0;
+  for (int i = 0; i < s; ++i) l += st_logq(logr, i, lq);
+  return l;
+}
+__host__ __device__ constexpr int st_count(int logr, int lq) { return (logr + lq - 1) / lq; }
+__host__ __device__ constexpr int brev_c(int x, int bits) {
+  int r = 0;
+  for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1) << (bits - 1 - i);
+  return r;
+}
+
+// In-register q-point DIF DFT (natural in, bit-reversed out), unrolled by templates.
+template <int LOGQ, int H, int A>
+__device__ __forceinline__ void dif256_row(U256* v, const U256* wq) {
+  if constexpr (A < H) {
+    constexpr int Q = 1 << LOGQ;
+#pragma unroll
+    for (int blk = 0; blk < Q; blk += 2 * H) {
+      const U256 x = v[blk + A], y = v[blk + A + H];
+      v[blk + A] = Fr::add(x, y);
+      const U256 d = Fr::sub(x, y);
+      if constexpr (A == 0) v[blk + A + H] = d;
+      else v[blk + A + H] = Fr::mul(d, wq[A * (Q / (2 * H))]);
+    }
+    dif256_row<LOGQ, H, A + 1>(v, wq);
+  }
+}
+template <int LOGQ, int H>
+__device__ __forceinline__ void dif256_levels(U256* v, const U256* wq) {
+  if constexpr (H >= 1) {
+    dif256_row<LOGQ, H, 0>(v, wq);
+    dif256_levels<LOGQ, H / 2>(v, wq);
+  }
+}
+template <int LOGQ>
+__device__ __forceinline__ void dft_reg256(U256* v, const U256* wq) {
+  dif256_levels<LOGQ, (1 << LOGQ) / 2>(v, wq);
+}
+
+template <int LOGR, int W, int NT, int LQ, int S>
+__device__ __forceinline__ void stage256(U256* v, U256* lds, const U256* wq, const Pass256& a, const U256* in,
+                                         U256* out, uint64_t j0, int t) {
+  constexpr int R = 1 << LOGR;
+  constexpr int PER = (R * W) / NT;
+  constexpr int NST = st_count(LOGR, LQ);
+  constexpr int LOGQ = st_logq(LOGR, S, LQ);
+  constexpr int Q = 1 << LOGQ;
+  constexpr int L = 1 << st_logl(LOGR, S, LQ);
+  constexpr int NSUB = PER / Q;
+  constexpr int QMAX = 1 << LQ;
+  constexpr bool LAST = (S == NST - 1);
+  if constexpr (S == 0) {
+    // raw loads first (simple body: fully unrolled, v stays in registers)
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
+#pragma unroll
+      for (int c = 0; c < Q; ++c) v[u * Q + c] = in[(j0 + w) + (uint64_t)(i + c * (R / Q)) * (a.n >> LOGR)];
+    }
+    if (a.conv_in) {
+#pragma unroll
+      for (int e = 0; e < PER; ++e) v[e] = Fr::to_mont(v[e]);
+    }
+    if (a.log_ns > 0) {
+      U256 tw[PER];
+      if (a.twpass) {
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          const int sub = t + NT * (e / Q);
+          const uint64_t k = (j0 + sub % W) & ((1ull << a.log_ns) - 1);
+          const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
+          tw[e] = a.twpass[(r << a.log_ns) + k];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          const int sub = t + NT * (e / Q);
+          const uint64_t k = (j0 + sub % W) & ((1ull << a.log_ns) - 1);
+          const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
+          const uint64_t x = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
+          tw[e] = Fr::mul(a.tw0[x & ((1ull << a.tw_bits) - 1)], a.tw1[x >> a.tw_bits]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < PER; ++e) v[e] = Fr::mul(v[e], tw[e]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
+      const int k = i % L;
+#pragma unroll
+      for (int c = 0; c < Q; ++c) {
+        const int r = i + c * (R / Q);
+        U256 x = lds[r * W + w];
+        if (c != 0 && k != 0) x = Fr::mul(x, a.rtab[(R / (L * Q)) * c * k]);
+        v[u * Q + c] = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NSUB; ++u) {
+    U256 wl[Q / 2 > 0 ? Q / 2 : 1];
+#pragma unroll
+    for (int m = 0; m < Q / 2; ++m) wl[m] = wq[m * (QMAX / Q)];
+    dft_reg256<LOGQ>(v + u * Q, wl);
+  }
+  if constexpr (S > 0) __syncthreads();
+#pragma unroll
+  for (int u = 0; u < NSUB; ++u) {
+    const int sub = t + NT * u;
+    const int w = sub % W, i = sub / W;
+    const int k = i % L;
+#pragma unroll
+    for (int d = 0; d < Q; ++d) {
+      U256 y = v[u * Q + brev_c(d, LOGQ)];
+      const int r = (i / L) * L * Q + k + d * L;
+      if constexpr (!LAST) {
+        lds[r * W + w] = y;
+      } else {
+        if (a.scale) y = Fr::mul(y, a.n_inv);
+        if (a.conv_out) y = Fr::from_mont(y);
+        if (a.log_ns == 0) {
+          lds[w * (R + 1) + r] = y;
+        } else {
+          const uint64_t j = j0 + w;
+          const uint64_t msk = (1ull << a.log_ns) - 1;
+          out[((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & msk) + ((uint64_t)r << a.log_ns)] = y;
+        }
+      }
+    }
+  }
+  if constexpr (!LAST) {
+    __syncthreads();
+    stage256<LOGR, W, NT, LQ, S + 1>(v, lds, wq, a, in, out, j0, t);
+  }
+}
+
+template <int LOGR, int W, int NT, int LQ>
+__global__ void __launch_bounds__(NT) ntt256_pass_kernel(Pass256 a) {
+  constexpr int R = 1 << LOGR;
+  constexpr int E = R * W;
+  constexpr int PER = E / NT;
+  constexpr int QMAX = 1 << LQ;
+  static_assert(PER % QMAX == 0 && LOGR >= LQ, "bad shape");
+  __shared__ U256 lds[E + W];
+  const uint32_t poly = blockIdx.x / a.blocks_per_poly;
+  const uint64_t j0 = (uint64_t)(blockIdx.x % a.blocks_per_poly) * W;
+  const U256* in = a.in + (uint64_t)poly * a.n;
+  U256* out = a.out + (uint64_t)poly * a.n;
+  const int t = threadIdx.x;
+  U256 wq[QMAX / 2];
+#pragma unroll
+  for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
+  U256 v[PER];
+  stage256<LOGR, W, NT, LQ, 0>(v, lds, wq, a, in, out, j0, t);
+  if (a.log_ns == 0) {
+    __syncthreads();
+    U256* o = out + j0 * R;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int m = t + NT * u;
+      o[m] = lds[(m / R) * (R + 1) + (m % R)];
+    }
+  }
+}
+
+// Whole transform for n <= 2048 in one workgroup (bit-reversed load, radix-2 DIT).
+__global__ void __launch_bounds__(256) ntt256_small_kernel(const U256* in, U256* out, const U256* tw, uint32_t logn,
+                                                           U256 n_inv, uint32_t scale) {
+  __shared__ U256 lds[2048];
+  const uint32_t n = 1u << logn;
+  const U256* src = in + (uint64_t)blockIdx.x * n;
+  U256* dst = out + (uint64_t)blockIdx.x * n;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t r = logn ? (__brev(i) >> (32 - logn)) : 0;
+    lds[r] = Fr::to_mont(src[i]);
+  }
+  __syncthreads();
+  for (uint32_t len = 2; len <= n; len <<= 1) {
+    const uint32_t half = len >> 1;
+    for (uint32_t b = threadIdx.x; b < n / 2; b += blockDim.x) {
+      const uint32_t grp = b / half, k = b % half;
+      const uint32_t i0 = grp * len + k, i1 = i0 + half;
+      const U256 x = lds[i0], y = Fr::mul(lds[i1], tw[(uint64_t)k * (n / len)]);
+      lds[i0] = Fr::add(x, y);
+      lds[i1] = Fr::sub(x, y);
+    }
+    __syncthreads();
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    U256 y = lds[i];
+    if (scale) y = Fr::mul(y, n_inv);
+    dst[i] = Fr::from_mont(y);
+  }
+}
+
+__global__ void pointwise_mul256_kernel(const U256* a, const U256* b, U256* c, uint64_t count) {
+  // inputs canonical; mont(a)*b = a*b*R*R^-1 = a*b canonical in one product
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+    c[i] = Fr::mul(Fr::to_mont(a[i]), b[i]);
+}
+
+// ---------------------------------------------------------------- host side
+static U256 h_from64(const uint64_t* x) {
+  U256 r;
+  for (int i = 0; i < 4; ++i) { r.w[2 * i] = (uint32_t)x[i]; r.w[2 * i + 1] = (uint32_t)(x[i] >> 32); }
+  return r;
+}
+static bool h_canonical(const U256& x) { return !Fr::geq_p(x); }
+static U256 h_pow(U256 base_m, uint64_t e) {  // Montgomery in/out
+  U256 r = Fr::to_mont(Fr::one_plain());
+  while (e) {
+    if (e & 1) r = Fr::mul(r, base_m);
+    base_m = Fr::mul(base_m, base_m);
+    e >>= 1;
+  }
+  return r;
+}
+static U256 h_inv(const U256& a_m) {  // a^(r-2), Montgomery
+  // exponent r - 2 as 8 limbs, square-and-multiply from the top
+  uint32_t e[8];
+  for (int i = 0; i < 8; ++i) e[i] = Bn254FrParams::P[i];
+  e[0] -= 2;  // P[0] = 0xf0000001 >= 2
+  U256 r = Fr::to_mont(Fr::one_plain());
+  for (int i = 255; i >= 0; --i) {
+    r = Fr::mul(r, r);
+    if ((e[i / 32] >> (i % 32)) & 1) r = Fr::mul(r, a_m);
+  }
+  return r;
+}
+
+struct Plan256 {
+  uint64_t n = 0;
+  uint32_t log_n = 0;
+  int inverse = 0;
+  std::vector<int> logr;
+  uint32_t tw_bits = 0;
+  U256 n_inv{};
+  DevBuf small_tw, tw0, tw1;
+  std::vector<std::shared_ptr<DevBuf>> rtab, twpass;
+};
+
+static int up256(DevBuf& b, const std::vector<U256>& v) {
+  int rc = b.ensure(v.size() * sizeof(U256));
+  if (rc) return rc;
+  PBF_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(U256), hipMemcpyHostToDevice));
+  return 0;
+}
+
+static std::vector<U256> h_powers(const U256& w_m, uint64_t count) {
+  std::vector<U256> t(count);
+  U256 x = Fr::to_mont(Fr::one_plain());
+  for (uint64_t i = 0; i < count; ++i) { t[i] = x; x = Fr::mul(x, w_m); }
+  return t;
+}
+
+static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256* p) {
+  if (n == 0 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two");
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < n) ++log_n;
+  if (log_n > 28) return fail(PBF_EINVAL, "n exceeds the 2-adicity of BN254 Fr (2^28)");
+  U256 w = h_from64(omega);
+  if (!h_canonical(w)) return fail(PBF_EINVAL, "omega not canonical");
+  U256 wm = Fr::to_mont(w);
+  const U256 one_m = Fr::to_mont(Fr::one_plain());
+  if (n > 1 && (!Fr::eq(h_pow(wm, n), one_m) || Fr::eq(h_pow(wm, n / 2), one_m)))
+    return fail(PBF_EINVAL, "omega does not have order n");
+  p->n = n; p->log_n = log_n; p->inverse = inverse;
+  U256 nm;
+  {
+    U256 nn = Fr::one_plain();
+    nn.w[0] = (uint32_t)n; nn.w[1] = (uint32_t)(n >> 32);
+    nm = Fr::to_mont(nn);
+  }
+  p->n_inv = h_inv(nm);
+  if (inverse) wm = h_inv(wm);
+  if (n <= 2048) return up256(p->small_tw, h_powers(wm, n));
+  // passes of radix <= 2^9 (LDS tile 2048 x 32 B)
+  const int P = (log_n + 8) / 9;
+  p->logr.assign(P, log_n / P);
+  for (int i = 0; i < (int)(log_n % P); ++i) p->logr[i] += 1;
+  p->tw_bits = (log_n + 1) / 2;
+  int rc = up256(p->tw0, h_powers(wm, 1ull << p->tw_bits));
+  if (rc) return rc;
+  {
+    const U256 step = h_pow(wm, 1ull << p->tw_bits);
+    rc = up256(p->tw1, h_powers(step, n >> p->tw_bits));
+    if (rc) return rc;
+  }
+  uint64_t ns = 1;
+  for (int lr : p->logr) {
+    const uint64_t R = 1ull << lr;
+    auto rb = std::make_shared<DevBuf>();
+    if ((rc = up256(*rb, h_powers(h_pow(wm, n / R), R)))) return rc;
+    p->rtab.push_back(rb);
+    auto tb = std::make_shared<DevBuf>();
+    if (ns > 1 && R * ns <= (1ull << 20)) {
+      const uint64_t step = n / (ns * R);
+      std::vector<U256> t(R * ns);
+      for (uint64_t r = 0; r < R; ++r) {
+        const U256 wr = h_pow(wm, step * r);
+        U256 z = one_m;
+        for (uint64_t k = 0; k < ns; ++k) { t[r * ns + k] = z; z = Fr::mul(z, wr); }
+      }
+      if ((rc = up256(*tb, t))) return rc;
+    }
+    p->twpass.push_back(tb);
+    ns *= R;
+  }
+  return 0;
+}
+
+typedef void (*Pass256Fn)(Pass256);
+static int cols256(int logr) { return (2048 >> logr) > 64 ? 64 : (2048 >> logr); }
+static Pass256Fn pass256_fn(int logr) {
+  switch (logr) {  // W = min(64, 2048 / R), radix-4 register sub-DFTs, 4 elements per thread
+    case 4: return ntt256_pass_kernel<4, 64, 256, 2>;
+    case 5: return ntt256_pass_kernel<5, 64, 512, 2>;
+    case 6: return ntt256_pass_kernel<6, 32, 512, 2>;
+    case 7: return ntt256_pass_kernel<7, 16, 512, 2>;
+    case 8: return ntt256_pass_kernel<8, 8, 512, 2>;
+    case 9: return ntt256_pass_kernel<9, 4, 512, 2>;
+    default: return nullptr;
+  }
+}
+static int threads256(int logr) { return ((cols256(logr) << logr) / 4); }
+
+static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
+                  hipStream_t st) {
+  if (batch == 0) return 0;
+  if (p.n == 1) {
+    if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * sizeof(U256), hipMemcpyDeviceToDevice, st));
+    return 0;
+  }
+  if (p.logr.empty()) {
+    hipLaunchKernelGGL(ntt256_small_kernel, dim3(batch), dim3(256), 0, st, d_in, d_out,
+                       (const U256*)p.small_tw.p, p.log_n, p.n_inv, (uint32_t)p.inverse);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  const size_t P = p.logr.size();
+  const size_t bytes = batch * p.n * sizeof(U256);
+  int rc = s0.ensure(bytes);
+  if (!rc && P > 2) rc = s1.ensure(bytes);
+  if (rc) return rc;
+  uint32_t log_ns = 0;
+  for (size_t i = 0; i < P; ++i) {
+    const int lr = p.logr[i];
+    const int W = cols256(lr);
+    Pass256 a;
+    a.in = (i == 0) ? d_in : (const U256*)(((i - 1) & 1) ? s1.p : s0.p);
+    a.out = (i == P - 1) ? d_out : (U256*)((i & 1) ? s1.p : s0.p);
+    a.rtab = (const U256*)p.rtab[i]->p;
+    a.twpass = (const U256*)p.twpass[i]->p;
+    a.tw0 = (const U256*)p.tw0.p;
+    a.tw1 = (const U256*)p.tw1.p;
+    a.n_inv = p.n_inv;
+    a.n = p.n;
+    a.log_n = p.log_n;
+    a.log_ns = log_ns;
+    a.tw_bits = p.tw_bits;
+    a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
+    a.batch = (uint32_t)batch;
+    a.conv_in = (i == 0);
+    a.conv_out = (i == P - 1);
+    a.scale = (p.inverse && i == P - 1);
+    Pass256Fn fn = pass256_fn(lr);
+    if (!fn) return fail(PBF_EINVAL, "no 256-bit kernel for this radix");
+    const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
+    if (blocks > 0x7fffffffull) return fail(PBF_EINVAL, "batch too large");
+    hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(threads256(lr)), 0, st, a);
+    PBF_HIP(hipGetLastError());
+    log_ns += lr;
+  }
+  return 0;
+}
+
+static bool canonical_vec(const uint64_t* v, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (!h_canonical(h_from64(v + 4 * i))) return false;
+  return true;
+}
+
+}  // namespace pbf
+
+using namespace pbf;
+
+// per-context 256-bit plans live in a side table keyed by the context pointer
+#include <map>
+#include <mutex>
+#include <tuple>
+namespace {
+struct Key256 {
+  const void* ctx;
+  uint64_t w[4];
+  uint64_t n;
+  int inv;
+  bool operator<(const Key256& o) const {
+    return std::tie(ctx, w[0], w[1], w[2], w[3], n, inv) < std::tie(o.ctx, o.w[0], o.w[1], o.w[2], o.w[3], o.n, o.inv);
+  }
+};
+std::map<Key256, std::unique_ptr<Plan256>>& plans256() {
+  static std::map<Key256, std::unique_ptr<Plan256>> m;
+  return m;
+}
+std::mutex& plans256_mu() {
+  static std::mutex m;
+  return m;
+}
+int get_plan256(pbf_ctx* ctx, const uint64_t* omega, uint64_t n, int inverse, Plan256** out) {
+  Key256 k{ctx, {omega[0], omega[1], omega[2], omega[3]}, n, inverse ? 1 : 0};
+  std::lock_guard<std::mutex> g(plans256_mu());
+  auto it = plans256().find(k);
+  if (it != plans256().end()) { *out = it->second.get(); return 0; }
+  std::unique_ptr<Plan256> p(new Plan256());
+  PBF_HIP(hipSetDevice(ctx->device));
+  int rc = make_plan256(omega, n, inverse ? 1 : 0, p.get());
+  if (rc) return rc;
+  *out = p.get();
+  plans256()[k] = std::move(p);
+  return 0;
+}
+}  // namespace
+
+void pbf_internal_drop_plans256(const void* ctx) {
+  std::lock_guard<std::mutex> g(plans256_mu());
+  auto& m = plans256();
+  for (auto it = m.begin(); it != m.end();) it = (it->first.ctx == ctx) ? m.erase(it) : std::next(it);
+}
+
+extern "C" {
+
+// fft.rs:66-78 for the BN254 scalar field (elements 4 x u64 little-endian, canonical)
+int pbf_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* in, uint64_t* out, size_t n, int inverse) {
+  if (!ctx || !omega || (!in && n) || (!out && n)) return fail(PBF_EINVAL, "null argument");
+  Plan256* p;
+  int rc = get_plan256(ctx, omega, n, inverse, &p);
+  if (rc) return rc;
+  if (!canonical_vec(in, n)) return fail(PBF_EINVAL, "input not canonical");
+  hipStream_t s = ctx->host_stream();
+  if ((rc = ctx->io0.ensure(n * 32))) return rc;
+  PBF_HIP(hipMemcpyAsync(ctx->io0.p, in, n * 32, hipMemcpyHostToDevice, s));
+  if ((rc = run256(*p, (const U256*)ctx->io0.p, (U256*)ctx->io0.p, 1, ctx->scratch0, ctx->scratch1, s))) return rc;
+  PBF_HIP(hipMemcpyAsync(out, ctx->io0.p, n * 32, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return PBF_OK;
+}
+
+int pbf_ntt_fr256_batch_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_in, uint64_t* d_out, size_t n,
+                            size_t batch, int inverse, void* stream) {
+  if (!ctx || !omega || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  Plan256* p;
+  int rc = get_plan256(ctx, omega, n, inverse, &p);
+  if (rc) return rc;
+  return run256(*p, (const U256*)d_in, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, (hipStream_t)stream);
+}
+
+// fft.rs:109-132 mul_ntt for BN254 Fr; out has la+lb elements (4 x u64 each)
+int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, size_t la, const uint64_t* b,
+                      size_t lb, uint64_t* out) {
+  if (!ctx || !omega || !out || (!a && la) || (!b && lb)) return fail(PBF_EINVAL, "null argument");
+  const size_t n = la + lb;
+  Plan256 *fw, *iv;
+  int rc = get_plan256(ctx, omega, n, 0, &fw);
+  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv);
+  if (rc) return rc;
+  if (!canonical_vec(a, la) || !canonical_vec(b, lb)) return fail(PBF_EINVAL, "input not canonical");
+  hipStream_t s = ctx->host_stream();
+  if ((rc = ctx->io0.ensure(2 * n * 32))) return rc;
+  U256* d = (U256*)ctx->io0.p;
+  PBF_HIP(hipMemsetAsync(d, 0, 2 * n * 32, s));
+  if (la) PBF_HIP(hipMemcpyAsync(d, a, la * 32, hipMemcpyHostToDevice, s));
+  if (lb) PBF_HIP(hipMemcpyAsync(d + n, b, lb * 32, hipMemcpyHostToDevice, s));
+  if ((rc = run256(*fw, d, d, 2, ctx->scratch0, ctx->scratch1, s))) return rc;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s, d, d + n, d, (uint64_t)n);
+  PBF_HIP(hipGetLastError());
+  if ((rc = run256(*iv, d, d, 1, ctx->scratch0, ctx->scratch1, s))) return rc;
+  PBF_HIP(hipMemcpyAsync(out, d, n * 32, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return PBF_OK;
+}
+
+// device-pointer mul_ntt over `batch` pairs: d_a/d_b/d_out hold batch x n elements,
+// a and b already zero-padded to n = la + lb (the fft.rs:114-118 padding done by the caller)
+int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_a, const uint64_t* d_b,
+                          uint64_t* d_out, size_t n, size_t batch, void* stream) {
+  if (!ctx || !omega || !d_a || !d_b || !d_out) return fail(PBF_EINVAL, "null argument");
+  Plan256 *fw, *iv;
+  int rc = get_plan256(ctx, omega, n, 0, &fw);
+  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = ctx->io2.ensure(batch * n * 32))) return rc;
+  U256* fb = (U256*)ctx->io2.p;
+  if ((rc = run256(*fw, (const U256*)d_a, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
+  if ((rc = run256(*fw, (const U256*)d_b, fb, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
+  uint64_t blocks = (batch * n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s, (const U256*)d_out, fb, (U256*)d_out,
+                     (uint64_t)(batch * n));
+  PBF_HIP(hipGetLastError());
+  return run256(*iv, (const U256*)d_out, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s);
+}
+
+}  // extern "C"

@@ -46,6 +46,10 @@ SIGNATURES = [
     ("pbf_mul_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_poly_eval_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_fill_random_u64_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _sz, _vp]),
+    ("pbf_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _p64, _sz, ctypes.c_int]),
+    ("pbf_ntt_fr256_batch_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
+    ("pbf_mul_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_mul_ntt_fr256_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _vp, _sz, _sz, _vp]),
     ("pbf_ntt_shard_local_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _vp, _vp, _sz, _sz, ctypes.c_int,
                                                _vp]),
     ("pbf_ntt_shard_combine_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
@@ -159,9 +163,54 @@ class Context:
         _check(self.lib.pbf_ntt_shard_combine_dev(self.h, modulus, omega, world, rank, _vp(d_in), _vp(d_out), nl,
                                                   batch, int(inverse), _vp(stream) if stream else None))
 
+    # ---- BN254 Fr (elements as Python ints <-> 4 x u64 little-endian)
+    def ntt_fr(self, omega: int, values, inverse: bool = False) -> list:
+        a = ints_to_limbs(values)
+        out = np.empty_like(a)
+        w = ints_to_limbs([omega])
+        _check(self.lib.pbf_ntt_fr256(self.h, _ptr(w), _ptr(a), _ptr(out), len(values), int(inverse)))
+        return limbs_to_ints(out)
+
+    def mul_ntt_fr(self, omega: int, a, b) -> list:
+        la, lb = ints_to_limbs(a), ints_to_limbs(b)
+        out = np.empty((len(a) + len(b)) * 4, dtype=np.uint64)
+        w = ints_to_limbs([omega])
+        _check(self.lib.pbf_mul_ntt_fr256(self.h, _ptr(w), _ptr(la), len(a), _ptr(lb), len(b), _ptr(out)))
+        return limbs_to_ints(out)
+
+    def ntt_fr_batch_dev(self, omega: int, d_in: int, d_out: int, n: int, batch: int, inverse: bool = False,
+                         stream: int = 0) -> None:
+        w = ints_to_limbs([omega])
+        _check(self.lib.pbf_ntt_fr256_batch_dev(self.h, _ptr(w), _vp(d_in), _vp(d_out), n, batch, int(inverse),
+                                                _vp(stream) if stream else None))
+
+    def mul_ntt_fr_dev(self, omega: int, d_a: int, d_b: int, d_out: int, n: int, batch: int, stream: int = 0):
+        w = ints_to_limbs([omega])
+        _check(self.lib.pbf_mul_ntt_fr256_dev(self.h, _ptr(w), _vp(d_a), _vp(d_b), _vp(d_out), n, batch,
+                                              _vp(stream) if stream else None))
+
     def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
         _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,
                                                 _vp(stream) if stream else None))
+
+
+BN254_R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+BN254_Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+
+
+def ints_to_limbs(values) -> np.ndarray:
+    """Python ints -> flat array of 4 x u64 little-endian limbs per element."""
+    out = np.empty(len(values) * 4, dtype=np.uint64)
+    m = (1 << 64) - 1
+    for i, v in enumerate(values):
+        v = int(v)
+        out[4 * i: 4 * i + 4] = [v & m, (v >> 64) & m, (v >> 128) & m, (v >> 192) & m]
+    return out
+
+
+def limbs_to_ints(a: np.ndarray) -> list:
+    a = np.asarray(a, dtype=np.uint64).reshape(-1, 4)
+    return [int(r[0]) | (int(r[1]) << 64) | (int(r[2]) << 128) | (int(r[3]) << 192) for r in a]
 
 
 _default_ctx: Context | None = None

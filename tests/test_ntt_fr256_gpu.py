@@ -1,0 +1,95 @@
+"""GPU parity of the BN254-Fr NTT and mul_ntt (BASELINE config 3) vs the Python
+big-integer oracle (oracle/bn254.py): exact at small and medium sizes, and at the
+config-3 size (a, b of 2^22 coefficients, NTT size 2^23) through size-independent
+properties (round trip, evaluation identity c(x) = a(x) b(x) at random points)."""
+import random
+
+import numpy as np
+import pytest
+
+import bn254
+import pbf
+
+pytestmark = pytest.mark.gpu
+R = bn254.R
+
+
+@pytest.mark.parametrize("logn", [0, 1, 2, 3, 5, 8, 11])
+def test_small_vs_recursion_faithful(ctx, logn):
+    n = 1 << logn
+    w = bn254.root_of_unity(n) if n > 1 else 1
+    a = bn254.limbs_to_ints(bn254.random_limbs(n, 10 + logn))
+    got = ctx.ntt_fr(w, a)
+    assert got == (bn254.ct_fft(a, w) if n > 1 else a)
+    assert ctx.ntt_fr(w, got, inverse=True) == a
+
+
+@pytest.mark.parametrize("logn", [12, 13, 14, 15, 16, 17])
+def test_multi_pass_vs_oracle(ctx, logn):
+    n = 1 << logn
+    w = bn254.root_of_unity(n)
+    a = bn254.limbs_to_ints(bn254.random_limbs(n, 20 + logn))
+    got = ctx.ntt_fr(w, a)
+    assert got == bn254.ntt(a, w)
+    assert ctx.ntt_fr(w, got, inverse=True) == a
+
+
+def test_kat_structure_small_field_values(ctx):
+    # DFT of a delta / constant vector has a closed form (any field)
+    n = 1 << 13
+    w = bn254.root_of_unity(n)
+    delta = [0] * n
+    delta[1] = 1
+    assert ctx.ntt_fr(w, delta)[:4] == [1, w, w * w % R, pow(w, 3, R)]
+    assert ctx.ntt_fr(w, [7] * n) == [7 * n % R] + [0] * (n - 1)
+
+
+@pytest.mark.parametrize("k", [3, 6, 9, 12])
+def test_mul_ntt_vs_schoolbook(ctx, k):
+    # fft.rs:171-183 property: Poly::new(mul_ntt(a, b)) == a * b
+    n = 1 << k
+    rnd = random.Random(k)
+    a = [rnd.randrange(R) for _ in range(n // 2)]
+    b = [rnd.randrange(R) for _ in range(n // 2)]
+    c = ctx.mul_ntt_fr(bn254.root_of_unity(n), a, b)
+    if k <= 9:
+        assert bn254.normalize(c) == bn254.poly_mul(a, b)
+    else:
+        assert c == bn254.mul_ntt(a, b, bn254.root_of_unity(n))
+
+
+def test_mul_ntt_config3_size_evaluation_identity(ctx):
+    # BASELINE config 3: a, b of 2^22 coefficients -> domain 2^23
+    import torch
+
+    la = 1 << 22
+    n = 2 * la
+    w = bn254.root_of_unity(n)
+    a = bn254.random_limbs(la, 301)
+    b = bn254.random_limbs(la, 302)
+    da = torch.zeros(n * 4, dtype=torch.int64, device="cuda")
+    db = torch.zeros_like(da)
+    da[: la * 4] = torch.from_numpy(a.view(np.int64)).cuda()
+    db[: la * 4] = torch.from_numpy(b.view(np.int64)).cuda()
+    dc = torch.empty_like(da)
+    ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1,
+                       stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = bn254.limbs_to_ints(dc.cpu().numpy().view(np.uint64))
+    ai, bi = bn254.limbs_to_ints(a), bn254.limbs_to_ints(b)
+    assert c[-1] == 0  # deg(a*b) = 2^23 - 2
+    for x in (3, 123456789123456789):
+        assert bn254.poly_eval(c, x) == bn254.poly_eval(ai, x) * bn254.poly_eval(bi, x) % R
+    # forward/inverse round trip at 2^23 through the device batch entry point
+    dd = torch.empty_like(dc)
+    ctx.ntt_fr_batch_dev(w, dc.data_ptr(), dd.data_ptr(), n, 1)
+    ctx.ntt_fr_batch_dev(w, dd.data_ptr(), dd.data_ptr(), n, 1, inverse=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dd, dc)
+
+
+def test_fr_errors(ctx):
+    with pytest.raises(pbf.PbfError):
+        ctx.ntt_fr(bn254.root_of_unity(16), [1] * 8)  # omega order 16 != 8
+    with pytest.raises(pbf.PbfError):
+        ctx.ntt_fr(bn254.root_of_unity(8), [R] * 8)  # non-canonical
