@@ -112,6 +112,20 @@ int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, si
 int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_a, const uint64_t* d_b,
                           uint64_t* d_out, size_t n, size_t batch, void* stream);
 
+/* ---- BN254 G1 MSM / SRS (BASELINE config 4) -----------------------------------
+ * Points: affine, 8 x uint64_t (x then y, each 4 little-endian limbs, canonical in Fq);
+ * (0, 0) encodes the identity. Scalars: Fr canonical, 4 x uint64_t.              */
+/* SRS::eval_at_s (plonk.rs:51-58): out = sum_i scalars[i] * points[i]               */
+int pbf_msm_g1_bn254(pbf_ctx* ctx, const uint64_t* points, const uint64_t* scalars, size_t n,
+                     uint64_t* out);
+int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t* d_scalars, size_t n,
+                         uint64_t* out, void* stream);
+/* out_i = scalars_i * G (G = (1, 2)), device pointers                               */
+int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t* d_out, size_t n,
+                              void* stream);
+/* SRS::create (plonk.rs:35-48): out = [G, G*s, ..., G*s^n] (n+1 points)             */
+int pbf_srs_create_bn254(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* out);
+
 /* ---- synthetic inputs (bench / tests) ------------------------------------- */
 /* d_out[i] = splitmix64 stream of (seed, i) with rejection of values >= modulus;
  * identical to tests/golden/gen_golden.py:splitmix_field.                     */

@@ -149,3 +149,47 @@ def ints_to_limbs(values) -> np.ndarray:
     for i in range(4):
         out[:, i] = ((v >> (64 * i)) & m).astype(np.uint64)
     return out.reshape(-1)
+
+
+# ---- BN254 G1 (y^2 = x^3 + 3 over Fq, generator (1, 2)), affine with None = identity.
+# Chord/tangent formulas as in the reference's toy G1 (src/pbh/g1.rs:119-144) over Fq.
+Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+G1_GEN = (1, 2)
+
+
+def g1_add(p, q):
+    if p is None:
+        return q
+    if q is None:
+        return p
+    if p[0] == q[0]:
+        if (p[1] + q[1]) % Q == 0:
+            return None
+        m = 3 * p[0] * p[0] * pow(2 * p[1], Q - 2, Q) % Q
+    else:
+        m = (q[1] - p[1]) * pow(q[0] - p[0], Q - 2, Q) % Q
+    x = (m * m - p[0] - q[0]) % Q
+    return (x, (m * (p[0] - x) - p[1]) % Q)
+
+
+def g1_mul(p, k: int):
+    """g1.rs:146-168 double-and-add (LSB first)."""
+    r, b = None, p
+    while k:
+        if k & 1:
+            r = g1_add(r, b)
+        b = g1_add(b, b)
+        k >>= 1
+    return r
+
+
+def g1_on_curve(p) -> bool:
+    return p is None or (p[1] * p[1] - p[0] ** 3 - 3) % Q == 0
+
+
+def msm_naive(points, scalars):
+    """plonk.rs:51-58 SRS::eval_at_s: left fold of points[i] * scalars[i]."""
+    acc = None
+    for p, s in zip(points, scalars):
+        acc = g1_add(acc, g1_mul(p, s))
+    return acc

@@ -1,0 +1,157 @@
+// BN254 G1 (y^2 = x^3 + 3 over Fq, generator (1, 2) — the curve equation and
+// generator of the reference's toy G1, src/pbh/g1.rs:34-36, over the real field).
+//
+// Coordinates inside kernels: XYZZ (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2), Fq elements in
+// Montgomery form; ZZ = 0 is the identity. Formulas: EFD "xyzz" madd-2008-s,
+// add-2008-s, dbl-2008-s-1, mdbl-2008-s-1 (a = 0). Every exceptional case (identity
+// operand, P + P, P + (-P)) is handled, so results are exact group elements and the
+// canonical affine output is bit-identical to any correct implementation.
+// At the ABI an affine point is 8 x uint64_t (x, y canonical, little-endian limbs);
+// (0, 0) encodes the identity (it is not on the curve).
+#pragma once
+#include "fp256.hpp"
+
+namespace pbf {
+
+struct Affine {
+  U256 x, y;  // Montgomery inside kernels
+};
+
+struct Xyzz {
+  U256 X, Y, ZZ, ZZZ;
+};
+
+__host__ __device__ __forceinline__ U256 u256_zero() {
+  U256 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z.w[i] = 0;
+  return z;
+}
+
+struct G1 {
+  typedef Fq F;
+  __host__ __device__ __forceinline__ static U256 one_m() { return F::to_mont(F::one_plain()); }
+  __host__ __device__ __forceinline__ static Xyzz identity() {
+    Xyzz r;
+    r.X = one_m(); r.Y = one_m(); r.ZZ = u256_zero(); r.ZZZ = u256_zero();
+    return r;
+  }
+  __host__ __device__ __forceinline__ static bool is_identity(const Xyzz& p) { return F::is_zero(p.ZZ); }
+  __host__ __device__ __forceinline__ static Xyzz from_affine(const Affine& a) {
+    Xyzz r;
+    r.X = a.x; r.Y = a.y; r.ZZ = one_m(); r.ZZZ = one_m();
+    return r;
+  }
+  __host__ __device__ __forceinline__ static U256 dbl_f(const U256& a) { return F::add(a, a); }
+
+  // mdbl-2008-s-1: 2*(x, y) for an affine point (y != 0 on BN254 G1: no 2-torsion)
+  __host__ __device__ static Xyzz mdbl(const Affine& a) {
+    const U256 U = dbl_f(a.y);
+    const U256 V = F::mul(U, U);
+    const U256 W = F::mul(U, V);
+    const U256 S = F::mul(a.x, V);
+    const U256 xx = F::mul(a.x, a.x);
+    const U256 M = F::add(dbl_f(xx), xx);
+    Xyzz r;
+    r.X = F::sub(F::mul(M, M), dbl_f(S));
+    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), F::mul(W, a.y));
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+  }
+  // dbl-2008-s-1
+  __host__ __device__ static Xyzz dbl(const Xyzz& p) {
+    if (is_identity(p)) return p;
+    const U256 U = dbl_f(p.Y);
+    const U256 V = F::mul(U, U);
+    const U256 W = F::mul(U, V);
+    const U256 S = F::mul(p.X, V);
+    const U256 xx = F::mul(p.X, p.X);
+    const U256 M = F::add(dbl_f(xx), xx);
+    Xyzz r;
+    r.X = F::sub(F::mul(M, M), dbl_f(S));
+    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), F::mul(W, p.Y));
+    r.ZZ = F::mul(V, p.ZZ);
+    r.ZZZ = F::mul(W, p.ZZZ);
+    return r;
+  }
+  // madd-2008-s: p + a (a affine, not the identity)
+  __host__ __device__ static Xyzz madd(const Xyzz& p, const Affine& a) {
+    if (is_identity(p)) return from_affine(a);
+    const U256 U2 = F::mul(a.x, p.ZZ);
+    const U256 S2 = F::mul(a.y, p.ZZZ);
+    const U256 P = F::sub(U2, p.X);
+    const U256 R = F::sub(S2, p.Y);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return mdbl(a);
+      return identity();
+    }
+    const U256 PP = F::mul(P, P);
+    const U256 PPP = F::mul(P, PP);
+    const U256 Q = F::mul(p.X, PP);
+    Xyzz r;
+    r.X = F::sub(F::sub(F::mul(R, R), PPP), dbl_f(Q));
+    r.Y = F::sub(F::mul(R, F::sub(Q, r.X)), F::mul(p.Y, PPP));
+    r.ZZ = F::mul(p.ZZ, PP);
+    r.ZZZ = F::mul(p.ZZZ, PPP);
+    return r;
+  }
+  // add-2008-s: p + q
+  __host__ __device__ static Xyzz add(const Xyzz& p, const Xyzz& q) {
+    if (is_identity(p)) return q;
+    if (is_identity(q)) return p;
+    const U256 U1 = F::mul(p.X, q.ZZ);
+    const U256 U2 = F::mul(q.X, p.ZZ);
+    const U256 S1 = F::mul(p.Y, q.ZZZ);
+    const U256 S2 = F::mul(q.Y, p.ZZZ);
+    const U256 P = F::sub(U2, U1);
+    const U256 R = F::sub(S2, S1);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return dbl(p);
+      return identity();
+    }
+    const U256 PP = F::mul(P, P);
+    const U256 PPP = F::mul(P, PP);
+    const U256 Q = F::mul(U1, PP);
+    Xyzz r;
+    r.X = F::sub(F::sub(F::mul(R, R), PPP), dbl_f(Q));
+    r.Y = F::sub(F::mul(R, F::sub(Q, r.X)), F::mul(S1, PPP));
+    r.ZZ = F::mul(F::mul(p.ZZ, q.ZZ), PP);
+    r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
+    return r;
+  }
+  // k * p for a small non-negative k (double-and-add, MSB first)
+  __host__ __device__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
+    Xyzz r = identity();
+    for (int b = 31; b >= 0; --b) {
+      r = dbl(r);
+      if ((k >> b) & 1) r = add(r, p);
+    }
+    return r;
+  }
+  // a^(q-2) (Fermat), Montgomery in/out
+  __host__ __device__ static U256 inv(const U256& a) {
+    uint32_t e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = Bn254FqParams::P[i];
+    e[0] -= 2;
+    U256 r = one_m();
+    for (int i = 255; i >= 0; --i) {
+      r = F::mul(r, r);
+      if ((e[i >> 5] >> (i & 31)) & 1) r = F::mul(r, a);
+    }
+    return r;
+  }
+  // canonical affine (plain form); identity -> (0, 0)
+  __host__ __device__ static void to_affine_plain(const Xyzz& p, U256* x, U256* y) {
+    if (is_identity(p)) { *x = u256_zero(); *y = u256_zero(); return; }
+    // ZZ^3 = ZZZ^2, so 1/ZZ = ZZ^2 * (1/ZZZ)^2: one inversion
+    const U256 izzz = inv(p.ZZZ);
+    const U256 t = F::mul(p.ZZ, izzz);
+    const U256 izz = F::mul(t, t);
+    *x = F::from_mont(F::mul(p.X, izz));
+    *y = F::from_mont(F::mul(p.Y, izzz));
+  }
+};
+
+}  // namespace pbf

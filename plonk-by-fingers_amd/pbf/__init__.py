@@ -50,6 +50,10 @@ SIGNATURES = [
     ("pbf_ntt_fr256_batch_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
     ("pbf_mul_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_mul_ntt_fr256_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _vp, _sz, _sz, _vp]),
+    ("pbf_msm_g1_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
+    ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
+    ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
     ("pbf_ntt_shard_local_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _vp, _vp, _sz, _sz, ctypes.c_int,
                                                _vp]),
     ("pbf_ntt_shard_combine_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
@@ -188,6 +192,32 @@ class Context:
         w = ints_to_limbs([omega])
         _check(self.lib.pbf_mul_ntt_fr256_dev(self.h, _ptr(w), _vp(d_a), _vp(d_b), _vp(d_out), n, batch,
                                               _vp(stream) if stream else None))
+
+    # ---- BN254 G1 (points as (x, y) Python int pairs; identity = (0, 0))
+    def msm_g1(self, points, scalars) -> tuple:
+        pts = ints_to_limbs([c for pt in points for c in pt])
+        sc = ints_to_limbs(scalars)
+        out = np.zeros(8, dtype=np.uint64)
+        _check(self.lib.pbf_msm_g1_bn254(self.h, _ptr(pts), _ptr(sc), len(scalars), _ptr(out)))
+        x, y = limbs_to_ints(out)
+        return (x, y)
+
+    def msm_g1_dev(self, d_points: int, d_scalars: int, n: int, stream: int = 0) -> tuple:
+        out = np.zeros(8, dtype=np.uint64)
+        _check(self.lib.pbf_msm_g1_bn254_dev(self.h, _vp(d_points), _vp(d_scalars), n, _ptr(out),
+                                             _vp(stream) if stream else None))
+        x, y = limbs_to_ints(out)
+        return (x, y)
+
+    def g1_mul_base_dev(self, d_scalars: int, d_out: int, n: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_g1_bn254_mul_base_dev(self.h, _vp(d_scalars), _vp(d_out), n,
+                                                  _vp(stream) if stream else None))
+
+    def srs_create(self, s: int, n: int) -> list:
+        out = np.zeros((n + 1) * 8, dtype=np.uint64)
+        _check(self.lib.pbf_srs_create_bn254(self.h, _ptr(ints_to_limbs([s])), n, _ptr(out)))
+        v = limbs_to_ints(out)
+        return [(v[2 * i], v[2 * i + 1]) for i in range(n + 1)]
 
     def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
         _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,

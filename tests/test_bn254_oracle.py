@@ -38,3 +38,11 @@ def test_limb_roundtrip():
     ints = bn254.limbs_to_ints(a)
     assert all(0 <= x < bn254.R for x in ints)
     assert (bn254.ints_to_limbs(ints) == a).all()
+
+
+def test_g1_oracle_group_law():
+    g = bn254.G1_GEN
+    assert bn254.g1_on_curve(g)
+    assert bn254.g1_mul(g, bn254.R) is None  # G1 has prime order r
+    assert bn254.g1_add(bn254.g1_mul(g, 5), bn254.g1_mul(g, 7)) == bn254.g1_mul(g, 12)
+    assert bn254.g1_on_curve(bn254.g1_mul(g, 123456789))
