@@ -126,6 +126,26 @@ int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t*
 /* SRS::create (plonk.rs:35-48): out = [G, G*s, ..., G*s^n] (n+1 points)             */
 int pbf_srs_create_bn254(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* out);
 
+/* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/*.rs) -------------------
+ * 32-bit words: G1 [x, y, inf] over F101 (y^2 = x^3 + 3), G2 [a, b] (a + b*u over
+ * F101[u]/(u^2+2)), GT [a, b]. Inputs must be on the curve (else PBF_EINVAL, where the
+ * reference would panic or compute garbage).                                        */
+int pbf_pbh_g1_mul(pbf_ctx* ctx, const uint32_t* pts, const uint32_t* scalars, size_t n, uint32_t* out);
+int pbf_pbh_g2_mul(pbf_ctx* ctx, const uint32_t* pts, const uint32_t* scalars, size_t n, uint32_t* out);
+int pbf_pbh_gt_pow(pbf_ctx* ctx, const uint32_t* x, const uint32_t* e, size_t n, uint32_t* out);
+/* PBHPairing::pairing (pairing.rs:12-47), batched                                    */
+int pbf_pbh_pairing(pbf_ctx* ctx, const uint32_t* g1, const uint32_t* g2, size_t n, uint32_t* out);
+/* Plonk::prove (+ Plonk::verify when verify_u < 17) over PlonkByHandTypes
+ * (plonk.rs:120-650, pbh/mod.rs:18-33). gates: n x [q_l q_r q_o q_m q_c]; copies:
+ * 3 columns x n x [kind (0=A,1=B,2=C), 1-based index]; abc: 3 x n witness; chal:
+ * [alpha beta gamma z v]; rnd: 9 blinders; s: toxic waste; srs_n: SRS degree;
+ * omega_pows: |H|. out_pts: 9 x [x y inf] (a_s b_s c_s z_s t_lo t_mid t_hi w_z w_zw),
+ * out_f: [a_z b_z c_z s_sigma_1_z s_sigma_2_z r_z z_omega_z]; *verified = 1/0 (or -1).  */
+int pbf_pbh_prove(pbf_ctx* ctx, size_t n, const uint64_t* gates, const uint64_t* copies,
+                  const uint64_t* abc, const uint64_t* chal, const uint64_t* rnd, uint64_t s,
+                  uint64_t srs_n, uint64_t omega_pows, uint64_t verify_u, uint64_t* out_pts,
+                  uint64_t* out_f, int* verified);
+
 /* ---- synthetic inputs (bench / tests) ------------------------------------- */
 /* d_out[i] = splitmix64 stream of (seed, i) with rejection of values >= modulus;
  * identical to tests/golden/gen_golden.py:splitmix_field.                     */

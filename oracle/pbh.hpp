@@ -3,6 +3,7 @@
 // src/constraints.rs and src/plonk.rs of the reference.
 #pragma once
 #include <array>
+#include <stdexcept>
 #include <vector>
 #include "fft.hpp"
 
@@ -269,7 +270,8 @@ struct SRS {  // plonk.rs:28-59
   // plonk.rs:51-58 naive MSM: left fold from identity of g1s[i] * gf(c_i)
   G1P eval_at_s(const Poly<F17>& p) const {
     G1P acc = G1P::identity();
-    for (size_t i = 0; i < p.c.size(); ++i) acc = acc + g1s[i] * PBH::gf(p.c[i]);
+    // g1s[n] panics in the reference when the polynomial is longer than the SRS
+    for (size_t i = 0; i < p.c.size(); ++i) acc = acc + g1s.at(i) * PBH::gf(p.c[i]);
     return acc;
   }
 };

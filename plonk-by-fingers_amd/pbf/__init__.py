@@ -33,6 +33,7 @@ _u64 = ctypes.c_uint64
 _p64 = ctypes.POINTER(ctypes.c_uint64)
 _sz = ctypes.c_size_t
 _vp = ctypes.c_void_p
+_p32 = ctypes.POINTER(ctypes.c_uint32)
 
 # (name, restype, argtypes) for every entry point in include/pbf.h
 SIGNATURES = [
@@ -54,6 +55,12 @@ SIGNATURES = [
     ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
     ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
+    ("pbf_pbh_g1_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
+    ("pbf_pbh_g2_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
+    ("pbf_pbh_gt_pow", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
+    ("pbf_pbh_pairing", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
+    ("pbf_pbh_prove", ctypes.c_int, [_vp, _sz, _p64, _p64, _p64, _p64, _p64, _u64, _u64, _u64, _u64, _p64, _p64,
+                                     ctypes.POINTER(ctypes.c_int)]),
     ("pbf_ntt_shard_local_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _vp, _vp, _sz, _sz, ctypes.c_int,
                                                _vp]),
     ("pbf_ntt_shard_combine_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
@@ -218,6 +225,41 @@ class Context:
         _check(self.lib.pbf_srs_create_bn254(self.h, _ptr(ints_to_limbs([s])), n, _ptr(out)))
         v = limbs_to_ints(out)
         return [(v[2 * i], v[2 * i + 1]) for i in range(n + 1)]
+
+    # ---- plonk-by-hand types (src/pbh/*.rs), batched on the GPU
+    def _u32call(self, fn, a, b, width_out, n):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))
+        b = np.ascontiguousarray(np.asarray(b, dtype=np.uint32).reshape(-1))
+        out = np.zeros(n * width_out, dtype=np.uint32)
+        _check(fn(self.h, a.ctypes.data_as(_p32), b.ctypes.data_as(_p32), n, out.ctypes.data_as(_p32)))
+        return [tuple(int(x) for x in out[i * width_out:(i + 1) * width_out]) for i in range(n)]
+
+    def pbh_g1_mul(self, pts, scalars):
+        return self._u32call(self.lib.pbf_pbh_g1_mul, pts, scalars, 3, len(scalars))
+
+    def pbh_g2_mul(self, pts, scalars):
+        return self._u32call(self.lib.pbf_pbh_g2_mul, pts, scalars, 2, len(scalars))
+
+    def pbh_gt_pow(self, xs, es):
+        return self._u32call(self.lib.pbf_pbh_gt_pow, xs, es, 2, len(es))
+
+    def pbh_pairing(self, g1s, g2s):
+        return self._u32call(self.lib.pbf_pbh_pairing, g1s, g2s, 2, len(g2s))
+
+    def pbh_prove(self, gates, copies, abc, chal, rnd, s=2, srs_n=6, omega_pows=4, verify_u=None):
+        """Plonk::prove (+verify) over PlonkByHandTypes; same layout as oracle.pbh_prove."""
+        n = len(gates)
+        a = lambda v: np.ascontiguousarray(np.asarray(v, dtype=np.uint64).reshape(-1))  # noqa: E731
+        g, c, w = a(gates), a(copies), a(abc)
+        ch, rd = a(chal), a(rnd)
+        pts = np.zeros(27, np.uint64)
+        fs = np.zeros(7, np.uint64)
+        ver = ctypes.c_int()
+        _check(self.lib.pbf_pbh_prove(self.h, n, _ptr(g), _ptr(c), _ptr(w), _ptr(ch), _ptr(rd), s, srs_n,
+                                      omega_pows, 17 if verify_u is None else verify_u, _ptr(pts), _ptr(fs),
+                                      ctypes.byref(ver)))
+        points = [tuple(int(x) for x in pts[3 * i: 3 * i + 3]) for i in range(9)]
+        return points, [int(x) for x in fs], (None if verify_u is None else bool(ver.value))
 
     def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
         _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,
