@@ -75,6 +75,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=32, help="polynomials per step")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the config 1/3/4 side measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,6 +159,8 @@ def main() -> int:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.log_n, B),
                          "kernel": "ntt_pass_kernel (all passes of one batched NTT; 16*n bytes per transform)"},
         }
+        if world == 1 and not args.no_extra:
+            out["extra"] = other_configs(ctx, sp)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
         print(json.dumps(out), flush=True)
@@ -165,6 +168,63 @@ def main() -> int:
         dist.destroy_process_group()
     ctx.close()
     return 0
+
+
+def _time_ms(fn, reps: int) -> float:
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def other_configs(ctx, sp) -> dict:
+    """Side measurements of BASELINE configs 1, 3 and 4 (synthetic inputs resident on the
+    device; timed with host wall clock around synchronized calls)."""
+    R = pbf.BN254_R
+    res = {}
+    # config 3: BN254-Fr poly multiply via NTT, a and b of 2^22 coefficients (NTT size 2^23)
+    la = 1 << 22
+    n = 2 * la
+    w = pow(5, (R - 1) // n, R)
+    rng = np.random.default_rng(3)
+    top = np.uint64(R >> 192)
+
+    def rand_fr(count):
+        a = rng.integers(0, 1 << 64, size=(count, 4), dtype=np.uint64)
+        a[:, 3] %= top
+        return torch.from_numpy(a.reshape(-1).view(np.int64)).cuda()
+
+    da = torch.zeros(n * 4, dtype=torch.int64, device="cuda")
+    db = torch.zeros_like(da)
+    da[: la * 4] = rand_fr(la)
+    db[: la * 4] = rand_fr(la)
+    dc = torch.empty_like(da)
+    ms = _time_ms(lambda: ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1, stream=sp), 3)
+    res["config3_bn254_polymul_2p22"] = {"ms": ms, "ntt_elements_per_s": 3 * n / (ms / 1e3),
+                                         "note": "2 forward + 1 inverse NTT of 2^23 + pointwise, 256-bit Montgomery"}
+    del da, db, dc
+    # config 4: BN254 G1 MSM of 2^20 points (points = t_i * G from the batch fixed-base kernel)
+    m = 1 << 20
+    t = rand_fr(m)
+    s = rand_fr(m)
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m, stream=sp)
+    torch.cuda.synchronize()
+    ms = _time_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp), 3)
+    res["config4_bn254_msm_2p20"] = {"ms": ms, "points_per_s": m / (ms / 1e3),
+                                     "note": "Pippenger c=16, includes the 16-window host Horner"}
+    # config 1: plonk-by-hand proof + verify (pbh/mod.rs:44-124) through the GPU path
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        k = json.load(f)["plonk_by_hand"]
+    t0 = time.perf_counter()
+    _, fs, ok = ctx.pbh_prove(k["gates_qlqrqoqmqc"], k["copies_kind_idx"], k["abc"], k["challenge_alpha_beta_gamma_z_v"],
+                              k["rand"], k["s"], k["srs_n"], k["omega_pows"], verify_u=k["verify_u"])
+    res["config1_plonk_by_hand"] = {"ms": (time.perf_counter() - t0) * 1e3, "verified": ok,
+                                    "kat_fields_match": fs == k["expected_fields"]}
+    return res
 
 
 def _single_gpu(ctx, n, B, sp):

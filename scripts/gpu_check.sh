@@ -3,6 +3,7 @@
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
+cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 step() { echo "== $1"; }
 step pytest
