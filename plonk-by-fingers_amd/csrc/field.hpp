@@ -22,41 +22,47 @@ struct Goldilocks {
   static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
   static constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p = 2^32 - 1
 
-  __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs&) {
+  __host__ __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs&) {
     uint64_t s = a + b;
     // wrap (s < a) means the true sum is s + 2^64 = s + EPS (mod p); s + EPS cannot
     // wrap again because a + b - 2^64 < p - 2^32. Otherwise subtract p when s >= p.
     uint64_t t = s + EPS;
     return (s < a || s >= P) ? t : s;
   }
-  __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
+  __host__ __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
     uint64_t d = a - b;
     return (a < b) ? d - EPS : d;  // d + p (mod 2^64)
   }
-  // 128-bit product reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
-  __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {
-    uint64_t hh = hi >> 32;
-    uint64_t hl = hi & EPS;
-    uint64_t t0 = lo - hh;
-    if (lo < hh) t0 -= EPS;               // borrow: + p
-    uint64_t t1 = (hl << 32) - hl;        // hl * (2^32 - 1), < 2^64
-    uint64_t r = t0 + t1;
-    if (r < t1) r += EPS;                 // wrap: + 2^64 = + EPS (cannot wrap again)
-    return (r >= P) ? r - P : r;
+  // 128-bit value lo + hi*2^64 reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
+  __host__ __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {
+    const uint64_t hh = hi >> 32, hl = (uint32_t)hi;
+    uint64_t t0;
+    const bool br = __builtin_sub_overflow(lo, hh, &t0);
+    t0 -= br ? EPS : 0;                   // borrow: + p (cannot wrap: t0 >= 2^64 - 2^32 here)
+    uint64_t r;
+    const bool c = __builtin_add_overflow(t0, hl * EPS, &r);
+    r += c ? EPS : 0;                     // wrap: + 2^64 = + EPS (cannot wrap again)
+    return r >= P ? r - P : r;
   }
-  __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs&) {
-    return reduce128(a * b, __umul64hi(a, b));
+  // 64x64 -> 128 from four v_mad_u64_u32 (the carries ride in the 64-bit addends).
+  __host__ __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs&) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t t = (uint64_t)a0 * b1 + (p00 >> 32);
+    const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+    const uint64_t v = (uint64_t)a1 * b1 + (t >> 32);
+    return reduce128((u << 32) | (uint32_t)p00, v + (u >> 32));
   }
   // lo + t (mod p) for any lo < 2^64 and t <= (2^32-1)*EPS: one wrap/one
   // conditional subtraction suffice (see DESIGN.md "Goldilocks arithmetic").
-  __device__ __forceinline__ static uint64_t add_small(uint64_t lo, uint64_t t) {
+  __host__ __device__ __forceinline__ static uint64_t add_small(uint64_t lo, uint64_t t) {
     uint64_t s = lo + t;
     uint64_t u = s + EPS;
     return (s < t || s >= P) ? u : s;
   }
   // x * 2^S (mod p) for a compile-time 0 <= S < 96, x canonical.
   template <int S>
-  __device__ __forceinline__ static uint64_t mul_pow2(uint64_t x) {
+  __host__ __device__ __forceinline__ static uint64_t mul_pow2(uint64_t x) {
     static_assert(S >= 0 && S < 96, "shift out of range");
     if constexpr (S == 0) {
       return x;

@@ -191,18 +191,19 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
         x = DB ? buf[r * W + w] : v[u * Q + c];
         if (a.log_ns > 0) {
           const uint64_t k = (j0 + w) & ((1ull << a.log_ns) - 1);
-          const uint64_t e = (((uint64_t)r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1);
           if (a.twpass) {
             // per-pass table [r][k] (k contiguous across lanes: one coalesced load)
-            if (e) x = F::mul(x, a.twpass[((uint64_t)r << a.log_ns) + k], a.f);
-          } else if (e) {
+            // unconditional: e == 0 lanes multiply by T[r][k] = 1 (a per-lane branch would
+            // diverge inside every wave and only add exec-mask overhead)
+            x = F::mul(x, a.twpass[((uint64_t)r << a.log_ns) + k], a.f);
+          } else if (const uint64_t e = (((uint64_t)r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1)) {
             x = F::mul(x, a.twfull ? a.twfull[e] : tw_pow<F>(a, e), a.f);
           }
         }
       } else {
         x = buf[r * W + w];
         const int k = i % L;  // stage twiddle w_(L*Q)^(c*k) = w_R^((R/(L*Q))*c*k)
-        if (c != 0 && k != 0) x = F::mul(x, rt[(R / (L * Q)) * c * k], a.f);
+        if (c != 0) x = F::mul(x, rt[(R / (L * Q)) * c * k], a.f);  // k == 0 lanes: rt[0] = 1
       }
       v[u * Q + c] = x;
     }
