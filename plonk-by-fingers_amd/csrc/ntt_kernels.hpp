@@ -16,6 +16,14 @@
 
 namespace pbf {
 
+// Timing-only modes (PassArgs::dbg) are compiled in only with -DPBF_NTT_TIMING_MODES:
+// the per-element runtime checks they need split the kernels into many basic blocks.
+#ifdef PBF_NTT_TIMING_MODES
+#define PBF_DBG(a, bit) (((a).dbg & (bit)) != 0)
+#else
+#define PBF_DBG(a, bit) false
+#endif
+
 struct PassArgs {
   const uint64_t* in;    // pass input  (batch * n elements)
   uint64_t* out;         // pass output (batch * n elements)
@@ -31,10 +39,11 @@ struct PassArgs {
   uint32_t tw_bits;
   uint32_t blocks_per_poly;
   uint32_t scale;
-  uint32_t dbg;            // 0; 1 = no HBM traffic (timing), 2 = no arithmetic (timing)
+  uint32_t dbg;            // timing builds only (PBF_NTT_TIMING_MODES): 1 = no HBM traffic, 2 = no butterflies
   uint32_t cur_poly;       // set per tile inside the kernel
   uint32_t out_split_log;  // != 0: last pass stores destination-major [n/S][batch][S], S = 2^out_split_log
   uint32_t batch;
+  uint32_t xcd_kmajor;     // non-persistent grid, gridDim.x % 8 == 0: XCD-aware column-major block order
   FieldArgs f;
 };
 
@@ -154,18 +163,40 @@ __device__ __forceinline__ void tile_dma(uint64_t* buf, const PassArgs& a, const
   }
 }
 
+// Raw stage-0 inputs of one tile into registers (the same thread -> element map as stage 0).
+template <int LOGR, int W, int NT, int LQ>
+__device__ __forceinline__ void tile_load(uint64_t* v, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
+  constexpr int R = 1 << LOGR;
+  constexpr int PER = (R * W) / NT;
+  constexpr int Q = 1 << ntt_stage_logq(LOGR, 0, LQ);
+#pragma unroll
+  for (int u = 0; u < PER / Q; ++u) {
+    const int sub = t + NT * u;
+    const int w = sub % W, i = sub / W;
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+      const int r = i + c * (R / Q);
+      v[u * Q + c] = PBF_DBG(a, 1) ? (uint64_t)(t * 0x9E3779B9u + r) * 0x100000001ull
+                                 : in[(j0 + w) + (uint64_t)r * (a.n >> LOGR)];
+    }
+  }
+}
+
 struct NextTile {
   bool valid;
-  uint64_t* buf;
+  uint64_t* buf;   // mode 1: LDS destination
   const uint64_t* in;
   uint64_t j0;
+  uint64_t* regs;  // mode 2: register destination
 };
 
 // One register/LDS stage S of the in-workgroup R-point Stockham (radix Q = 2^logq).
-// Stage 0 reads the raw tile (registers v when !DB, the LDS image `buf` when DB) and
-// applies the pass twiddle; later stages read the exchange buffer and apply the stage
-// twiddle from `rt` (LDS when DB).
-template <class F, int LOGR, int W, int NT, int LQ, int E64, bool DB, int S>
+// MODE: 0 = one tile per workgroup; 1 = persistent, next tile LDS-DMA'd during this one
+// (ntt_pass_db_kernel); 2 = persistent, next tile prefetched into registers during this
+// one (ntt_pass_rp_kernel). Stage 0 reads the raw tile (registers v, or the LDS image
+// `buf` in mode 1) and applies the pass twiddle; later stages read the exchange buffer
+// and apply the stage twiddle from `rt` (an LDS copy in modes 1 and 2).
+template <class F, int LOGR, int W, int NT, int LQ, int E64, int MODE, int S>
 __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint64_t* rt, const uint64_t* wq,
                                           const PassArgs& a, uint64_t* out, uint64_t j0, int t,
                                           const NextTile& nx) {
@@ -178,39 +209,71 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
   constexpr int NSUB = PER / Q;
   constexpr bool LAST = (S == NST - 1);
   const uint64_t n = a.n;
-  // ---- gather inputs
+  // ---- gather inputs. The pass-twiddle variant is chosen once per tile (uniform
+  // branches hoisted out of the unrolled loops) so all PER twiddle loads issue
+  // back to back and are waited for once.
+  if constexpr (S == 0) {
+    if constexpr (MODE == 1) {
 #pragma unroll
-  for (int u = 0; u < NSUB; ++u) {
-    const int sub = t + NT * u;
-    const int w = sub % W, i = sub / W;
+      for (int u = 0; u < NSUB; ++u) {
+        const int sub = t + NT * u;
+        const int w = sub % W, i = sub / W;
 #pragma unroll
-    for (int c = 0; c < Q; ++c) {
-      const int r = i + c * (R / Q);
-      uint64_t x;
-      if constexpr (S == 0) {
-        x = DB ? buf[r * W + w] : v[u * Q + c];
-        if (a.log_ns > 0) {
-          const uint64_t k = (j0 + w) & ((1ull << a.log_ns) - 1);
-          if (a.twpass) {
-            // per-pass table [r][k] (k contiguous across lanes: one coalesced load)
-            // unconditional: e == 0 lanes multiply by T[r][k] = 1 (a per-lane branch would
-            // diverge inside every wave and only add exec-mask overhead)
-            x = F::mul(x, a.twpass[((uint64_t)r << a.log_ns) + k], a.f);
-          } else if (const uint64_t e = (((uint64_t)r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1)) {
-            x = F::mul(x, a.twfull ? a.twfull[e] : tw_pow<F>(a, e), a.f);
+        for (int c = 0; c < Q; ++c) v[u * Q + c] = buf[(i + c * (R / Q)) * W + w];
+      }
+    }
+    if (a.log_ns > 0) {
+      const uint64_t kmask = (1ull << a.log_ns) - 1;
+      if (a.twpass) {
+        // per-pass table [r][k] (k contiguous across lanes: coalesced loads); lanes with
+        // r*k == 0 multiply by T = 1 (a per-lane branch would only diverge)
+        uint64_t tw[PER];
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u) {
+          const int sub = t + NT * u;
+          const int w = sub % W, i = sub / W;
+          const uint64_t k = (j0 + w) & kmask;
+#pragma unroll
+          for (int c = 0; c < Q; ++c) tw[u * Q + c] = a.twpass[((uint64_t)(i + c * (R / Q)) << a.log_ns) + k];
+        }
+#pragma unroll
+        for (int m = 0; m < PER; ++m) v[m] = F::mul(v[m], tw[m], a.f);
+      } else {
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u) {
+          const int sub = t + NT * u;
+          const int w = sub % W, i = sub / W;
+          const uint64_t k = (j0 + w) & kmask;
+#pragma unroll
+          for (int c = 0; c < Q; ++c) {
+            const uint64_t r = i + c * (R / Q);
+            const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1);
+            if (e) v[u * Q + c] = F::mul(v[u * Q + c], a.twfull ? a.twfull[e] : tw_pow<F>(a, e), a.f);
           }
         }
-      } else {
-        x = buf[r * W + w];
-        const int k = i % L;  // stage twiddle w_(L*Q)^(c*k) = w_R^((R/(L*Q))*c*k)
-        if (c != 0) x = F::mul(x, rt[(R / (L * Q)) * c * k], a.f);  // k == 0 lanes: rt[0] = 1
       }
-      v[u * Q + c] = x;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
+      const int k = i % L;  // stage twiddle w_(L*Q)^(c*k) = w_R^((R/(L*Q))*c*k)
+#pragma unroll
+      for (int c = 0; c < Q; ++c) {
+        const uint64_t x = buf[(i + c * (R / Q)) * W + w];
+        v[u * Q + c] = (c != 0) ? F::mul(x, rt[(R / (L * Q)) * c * k], a.f) : x;  // k == 0: rt[0] = 1
+      }
     }
   }
-  if constexpr (DB && S == 0) {
+  if constexpr (MODE == 1 && S == 0) {
     // this tile's pass-twiddle loads are consumed: start the next tile's LDS-DMA now
     if (nx.valid) tile_dma<LOGR, W, NT>(nx.buf, a, nx.in, nx.j0, t);
+  }
+  if constexpr (MODE == 2 && S == 0) {
+    // same point for the register prefetch: its loads stay in flight through the later
+    // stages (LDS twiddles, raw barriers: nothing waits on vmcnt until the next tile)
+    if (nx.valid) tile_load<LOGR, W, NT, LQ>(nx.regs, a, nx.in, nx.j0, t);
   }
   // ---- radix-Q DFTs in registers (wq[m] = w_QMAX^m; w_Q = w_QMAX^(QMAX/Q))
   constexpr int QMAX = 1 << LQ;
@@ -221,46 +284,74 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
 #pragma unroll
       for (int m = 0; m < Q / 2; ++m) wloc[m] = wq[m * (QMAX / Q)];
     }
-    if (!(a.dbg & 2)) dft_reg<F, LOGQ, sub_root_exp(E64, LOGQ)>(v + u * Q, wloc, a.f);
+    if (!PBF_DBG(a, 2)) dft_reg<F, LOGQ, sub_root_exp(E64, LOGQ)>(v + u * Q, wloc, a.f);
   }
-  if constexpr (S > 0 || DB) tile_barrier<DB>();  // all reads of the exchange buffer are done
-  // ---- scatter outputs
+  if constexpr (S > 0 || MODE == 1) tile_barrier<(MODE != 0)>();  // all reads of the exchange buffer are done
+  // ---- scatter outputs (uniform output-mode branches hoisted out of the unrolled loops)
+  if constexpr (!LAST) {
 #pragma unroll
-  for (int u = 0; u < NSUB; ++u) {
-    const int sub = t + NT * u;
-    const int w = sub % W, i = sub / W;
-    const int k = i % L;
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
 #pragma unroll
-    for (int d = 0; d < Q; ++d) {
-      uint64_t y = v[u * Q + bitrev_c(d, LOGQ)];
-      const int r = (i / L) * L * Q + k + d * L;  // Stockham output slot
-      if constexpr (!LAST) {
-        buf[r * W + w] = y;
-      } else {
-        if (a.scale) y = F::mul(y, a.n_inv, a.f);
-        if (a.log_ns == 0) {
-          buf[w * (R + 1) + r] = y;  // transposed image, stored linearly by the caller
-        } else {
-          const uint64_t j = j0 + w;
-          const uint64_t ns_mask = (1ull << a.log_ns) - 1;
-          const uint64_t kk = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) + ((uint64_t)r << a.log_ns);
-          if (a.dbg & 1) {
-            if (y == 0x123456789ull) out[kk] = y;  // keeps the arithmetic live, never true in practice
-          } else if (a.out_split_log == 0) {
-            out[kk] = y;
-          } else {
-            // multi-GPU send layout: block kk/S goes to rank kk/S, polynomials contiguous per rank
-            const uint64_t poly = a.cur_poly;
-            const uint64_t sl = a.out_split_log;
-            a.out[((((kk >> sl) * a.batch) + poly) << sl) + (kk & ((1ull << sl) - 1))] = y;
+      for (int d = 0; d < Q; ++d)
+        buf[((i / L) * L * Q + (i % L) + d * L) * W + w] = v[u * Q + bitrev_c(d, LOGQ)];  // Stockham slot
+    }
+  } else {
+    if (a.scale) {
+#pragma unroll
+      for (int m = 0; m < PER; ++m) v[m] = F::mul(v[m], a.n_inv, a.f);
+    }
+    if (a.log_ns == 0) {
+      // transposed image, stored linearly by the caller
+#pragma unroll
+      for (int u = 0; u < NSUB; ++u) {
+        const int sub = t + NT * u;
+        const int w = sub % W, i = sub / W;
+#pragma unroll
+        for (int d = 0; d < Q; ++d)
+          buf[w * (R + 1) + (i / L) * L * Q + (i % L) + d * L] = v[u * Q + bitrev_c(d, LOGQ)];
+      }
+    } else {
+      const uint64_t ns_mask = (1ull << a.log_ns) - 1;
+      const uint32_t sl = a.out_split_log;
+      // output index of element d of sub-DFT u: kbase(u) + (slot << log_ns)
+      auto kk_of = [&](int u, int d) -> uint64_t {
+        const int sub = t + NT * u;
+        const int w = sub % W, i = sub / W;
+        const uint64_t j = j0 + w;
+        return ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask) +
+               ((uint64_t)((i / L) * L * Q + (i % L) + d * L) << a.log_ns);
+      };
+      if (PBF_DBG(a, 1)) {
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+          for (int d = 0; d < Q; ++d) {
+            const uint64_t y = v[u * Q + bitrev_c(d, LOGQ)];
+            if (y == 0x123456789ull) out[kk_of(u, d)] = y;  // keeps the arithmetic live
           }
-        }
+      } else if (sl == 0) {
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+          for (int d = 0; d < Q; ++d) out[kk_of(u, d)] = v[u * Q + bitrev_c(d, LOGQ)];
+      } else {
+        // multi-GPU send layout: block kk/S goes to rank kk/S, polynomials contiguous per rank
+        const uint64_t smask = (1ull << sl) - 1;
+#pragma unroll
+        for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+          for (int d = 0; d < Q; ++d) {
+            const uint64_t kk = kk_of(u, d);
+            a.out[((((kk >> sl) * a.batch) + a.cur_poly) << sl) + (kk & smask)] = v[u * Q + bitrev_c(d, LOGQ)];
+          }
       }
     }
   }
   if constexpr (!LAST) {
-    tile_barrier<DB>();
-    ntt_stage<F, LOGR, W, NT, LQ, E64, DB, S + 1>(v, buf, rt, wq, a, out, j0, t, nx);
+    tile_barrier<(MODE != 0)>();
+    ntt_stage<F, LOGR, W, NT, LQ, E64, MODE, S + 1>(v, buf, rt, wq, a, out, j0, t, nx);
   }
 }
 
@@ -276,34 +367,25 @@ __device__ __forceinline__ void store_transposed(const uint64_t* buf, uint64_t* 
   for (int u = 0; u < PER; ++u) {
     const int m = t + NT * u;
     const uint64_t y = buf[(m / R) * (R + 1) + (m % R)];
-    if (!(a.dbg & 1) || y == 0x123456789ull) o[m] = y;
-  }
-}
-
-// Raw stage-0 inputs of one tile into registers (the same thread -> element map as stage 0).
-template <int LOGR, int W, int NT, int LQ>
-__device__ __forceinline__ void tile_load(uint64_t* v, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
-  constexpr int R = 1 << LOGR;
-  constexpr int PER = (R * W) / NT;
-  constexpr int Q = 1 << ntt_stage_logq(LOGR, 0, LQ);
-#pragma unroll
-  for (int u = 0; u < PER / Q; ++u) {
-    const int sub = t + NT * u;
-    const int w = sub % W, i = sub / W;
-#pragma unroll
-    for (int c = 0; c < Q; ++c) {
-      const int r = i + c * (R / Q);
-      v[u * Q + c] = (a.dbg & 1) ? (uint64_t)(t * 0x9E3779B9u + r) * 0x100000001ull
-                                 : in[(j0 + w) + (uint64_t)r * (a.n >> LOGR)];
-    }
+    if (!PBF_DBG(a, 1) || y == 0x123456789ull) o[m] = y;
   }
 }
 
 // One Stockham pass over HBM, one tile per workgroup (tiles too large to double-buffer).
 // NT threads, W columns of R = 2^LOGR points, register sub-DFTs of radix up to 2^LQ;
 // E64 >= 0 selects shift twiddles for a standard Goldilocks root (w_64 = 2^E64).
+// Waves per SIMD the pass kernels are register-budgeted for: as many as the LDS tile
+// lets reside (R*W*8 bytes per workgroup of NT threads, 160 KiB per CU), at most 8.
+__host__ __device__ constexpr int ntt_waves_per_eu(int e, int nt) {
+  int per_cu = 163840 / (8 * e + 2048);
+  if (per_cu < 1) per_cu = 1;
+  int w = per_cu * (nt / 64) / 4;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
 template <class F, int LOGR, int W, int NT, int LQ, int E64>
-__global__ void __launch_bounds__(NT) ntt_pass_kernel(PassArgs a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ntt_waves_per_eu(W << LOGR, NT))))
+ntt_pass_kernel(PassArgs a) {
   constexpr int R = 1 << LOGR;
   constexpr int E = R * W;
   constexpr int PER = E / NT;
@@ -314,8 +396,20 @@ __global__ void __launch_bounds__(NT) ntt_pass_kernel(PassArgs a) {
   // +W pad keeps the transposed [w][r] image of the first pass bank-conflict free
   __shared__ uint64_t lds[E + W];
 
-  const uint32_t poly = blockIdx.x / a.blocks_per_poly;
-  const uint64_t j0 = (uint64_t)(blockIdx.x % a.blocks_per_poly) * W;
+  // Block order: with a pass-twiddle table, blocks of one XCD (blockIdx b, b+8, ... share
+  // an L2) take a contiguous range of column blocks, all polynomials of a column block
+  // back to back, so each slice of T[r][k] is fetched into that L2 once per pass instead
+  // of once per polynomial (PMC: 387 -> ~260 MiB fetched per pass at 2^20 x 32).
+  uint32_t poly, kb;
+  if (a.xcd_kmajor) {
+    const uint32_t v = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    kb = v / a.batch;
+    poly = v % a.batch;
+  } else {
+    poly = blockIdx.x / a.blocks_per_poly;
+    kb = blockIdx.x % a.blocks_per_poly;
+  }
+  const uint64_t j0 = (uint64_t)kb * W;
   const uint64_t* in = a.in + (uint64_t)poly * a.n;
   uint64_t* out = a.out + (uint64_t)poly * a.n;
   const int t = threadIdx.x;
@@ -329,8 +423,8 @@ __global__ void __launch_bounds__(NT) ntt_pass_kernel(PassArgs a) {
   }
   uint64_t v[PER];
   tile_load<LOGR, W, NT, LQ>(v, a, in, j0, t);
-  const NextTile none{false, nullptr, nullptr, 0};
-  ntt_stage<F, LOGR, W, NT, LQ, E64, false, 0>(v, lds, a.rtab, wq, b, out, j0, t, none);
+  const NextTile none{false, nullptr, nullptr, 0, nullptr};
+  ntt_stage<F, LOGR, W, NT, LQ, E64, 0, 0>(v, lds, a.rtab, wq, b, out, j0, t, none);
   if (a.log_ns == 0) store_transposed<LOGR, W, NT, false>(lds, out, j0, t, a);
 }
 
@@ -380,12 +474,62 @@ __global__ void __launch_bounds__(NT) ntt_pass_db_kernel(PassArgs a) {
     nx.j0 = (uint64_t)(nb % a.blocks_per_poly) * W;
     uint64_t* buf = lds + cur * BUF;
     uint64_t v[PER];
-    ntt_stage<F, LOGR, W, NT, LQ, E64, true, 0>(v, buf, rt, wq, b, out, j0, t, nx);
+    ntt_stage<F, LOGR, W, NT, LQ, E64, 1, 0>(v, buf, rt, wq, b, out, j0, t, nx);
     if (a.log_ns == 0) store_transposed<LOGR, W, NT, true>(buf, out, j0, t, a);
     // retire the next tile's LDS-DMA (issued before this tile's PER output stores)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     tile_barrier<true>();
     cur ^= 1;
+  }
+}
+
+// Persistent pass with a register prefetch (mode 2): while a tile's stages 1.. run, the
+// next tile's inputs load into registers, so one workgroup overlaps its own HBM reads
+// with arithmetic and keeps a single LDS tile (two workgroups per CU at R*W = 8192).
+// Stage twiddles are copied to LDS so no global load waits behind the prefetch.
+template <class F, int LOGR, int W, int NT, int LQ, int E64>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ntt_waves_per_eu(W << LOGR, NT))))
+ntt_pass_rp_kernel(PassArgs a) {
+  constexpr int R = 1 << LOGR;
+  constexpr int E = R * W;
+  constexpr int PER = E / NT;
+  constexpr int QMAX = 1 << LQ;
+  static_assert(LOGR >= LQ && PER >= QMAX && PER % QMAX == 0, "bad tile shape");
+  static_assert(E + W + R <= 20480, "LDS budget");
+  __shared__ uint64_t lds[E + W + R];
+  uint64_t* rt = lds + E + W;
+  const int t = threadIdx.x;
+  const uint32_t total = a.blocks_per_poly * a.batch;
+  uint32_t blk = blockIdx.x;
+  if (blk >= total) return;
+  for (int i = t; i < R; i += NT) rt[i] = a.rtab[i];
+  uint64_t wq[QMAX / 2];
+  if constexpr (E64 < 0) {
+#pragma unroll
+    for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
+  }
+  uint64_t nxt[PER];
+  tile_load<LOGR, W, NT, LQ>(nxt, a, a.in + (uint64_t)(blk / a.blocks_per_poly) * a.n,
+                             (uint64_t)(blk % a.blocks_per_poly) * W, t);
+  for (; blk < total; blk += gridDim.x) {
+    const uint32_t poly = blk / a.blocks_per_poly;
+    const uint64_t j0 = (uint64_t)(blk % a.blocks_per_poly) * W;
+    uint64_t* out = a.out + (uint64_t)poly * a.n;
+    PassArgs b = a;
+    b.cur_poly = poly;
+    uint64_t v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = nxt[i];
+    const uint32_t nb = blk + gridDim.x;
+    NextTile nx;
+    nx.valid = nb < total;
+    nx.buf = nullptr;
+    nx.in = a.in + (uint64_t)(nb / a.blocks_per_poly) * a.n;
+    nx.j0 = (uint64_t)(nb % a.blocks_per_poly) * W;
+    nx.regs = nxt;
+    ntt_stage<F, LOGR, W, NT, LQ, E64, 2, 0>(v, lds, rt, wq, b, out, j0, t, nx);
+    if (a.log_ns == 0) store_transposed<LOGR, W, NT, true>(lds, out, j0, t, a);
+    tile_barrier<true>();  // the next tile rewrites the exchange buffer
   }
 }
 

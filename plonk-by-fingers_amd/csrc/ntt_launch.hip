@@ -176,30 +176,34 @@ static int cols_for(int logr) {
 // Kernel configuration of one pass: W columns, register radix 2^LQ, double-buffered
 // persistent (DB) or one tile per workgroup.
 struct PassCfg {
-  int w, lq, db;
+  int w, lq, db, nt;  // nt != 0: threads per workgroup other than R*W/2^lq
 };
 
 static PassCfg pass_cfg(int logr) {
   // default: one tile per workgroup (measured faster than the LDS-DMA
   // double-buffered kernel, whose two tiles halve occupancy: DESIGN.md "NTT")
-  PassCfg def = PassCfg{cols_for(logr), 4, 0};
+  PassCfg def = PassCfg{cols_for(logr), 4, 0, 0};
   const char* env = getenv("PBF_NTT_CFG");  // "W,LQ,DB" e.g. "16,4,0" (benchmarking override)
   if (env && *env) {
-    int v[3] = {def.w, def.lq, def.db}, i = 0;
-    for (const char* c = env; *c && i < 3;) {
+    int v[4] = {def.w, def.lq, def.db, 0}, i = 0;
+    for (const char* c = env; *c && i < 4;) {
       v[i++] = atoi(c);
       while (*c && *c != ',') ++c;
       if (*c == ',') ++c;
     }
-    return PassCfg{v[0], v[1], v[2]};
+    return PassCfg{v[0], v[1], v[2], v[3]};
   }
   return def;
 }
 
 #define PBF_PASS(F, LR, W, LQ, E)                                                              \
-  if (logr == LR && c.w == W && c.lq == LQ && !c.db) return ntt_pass_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+  if (logr == LR && c.w == W && c.lq == LQ && !c.db && !c.nt) return ntt_pass_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
 #define PBF_PASS_DB(F, LR, W, LQ, E)                                                           \
-  if (logr == LR && c.w == W && c.lq == LQ && c.db) return ntt_pass_db_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+  if (logr == LR && c.w == W && c.lq == LQ && c.db == 1) return ntt_pass_db_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+#define PBF_PASS_NT(F, LR, W, LQ, NTH, E)                                                      \
+  if (logr == LR && c.w == W && c.lq == LQ && !c.db && c.nt == NTH) return ntt_pass_kernel<F, LR, W, NTH, LQ, E>;
+#define PBF_PASS_RP(F, LR, W, LQ, E)                                                           \
+  if (logr == LR && c.w == W && c.lq == LQ && c.db == 2) return ntt_pass_rp_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
 
 template <class F, int E>
 static PassFn pass_fn_e(int logr, PassCfg c) {
@@ -208,9 +212,15 @@ static PassFn pass_fn_e(int logr, PassCfg c) {
   PBF_PASS_DB(F, 8, 32, 4, E)
   PBF_PASS_DB(F, 9, 16, 4, E)
   PBF_PASS_DB(F, 10, 8, 4, E)
+  PBF_PASS_RP(F, 10, 8, 4, E)
+  PBF_PASS_RP(F, 10, 16, 4, E)
   PBF_PASS(F, 10, 16, 4, E)
   PBF_PASS(F, 10, 8, 4, E)
+  PBF_PASS_NT(F, 10, 8, 4, 256, E)
+  PBF_PASS_NT(F, 10, 16, 4, 512, E)
   PBF_PASS(F, 10, 8, 3, E)
+  PBF_PASS(F, 10, 8, 5, E)
+  PBF_PASS(F, 10, 16, 5, E)
   PBF_PASS(F, 10, 4, 4, E)
   PBF_PASS(F, 10, 4, 3, E)
   PBF_PASS(F, 11, 8, 4, E)
@@ -405,10 +415,11 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     a.dbg = getenv("PBF_NTT_DBG") ? (uint32_t)atoi(getenv("PBF_NTT_DBG")) : 0;
     a.batch = (uint32_t)batch;
     a.f = p.fa;
-    const int nt = (W << lr) >> cfg.lq;
+    const int nt = cfg.nt ? cfg.nt : (W << lr) >> cfg.lq;
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
     if (blocks > 0x7fffffffull) return fail(1, "batch too large");
-    const uint32_t grid = cfg.db ? persistent_grid(fn, nt, blocks) : (uint32_t)blocks;
+    const uint32_t grid = cfg.db ? persistent_grid(fn, nt, blocks) : (uint32_t)blocks;  // modes 1, 2: persistent
+    a.xcd_kmajor = (!cfg.db && log_ns > 0 && batch > 1 && grid % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(nt), 0, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;
