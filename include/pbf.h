@@ -126,7 +126,7 @@ int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t*
 /* SRS::create (plonk.rs:35-48): out = [G, G*s, ..., G*s^n] (n+1 points)             */
 int pbf_srs_create_bn254(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* out);
 
-/* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/*.rs) -------------------
+/* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/{g1,g2,gt,pairing}.rs) -------------------
  * 32-bit words: G1 [x, y, inf] over F101 (y^2 = x^3 + 3), G2 [a, b] (a + b*u over
  * F101[u]/(u^2+2)), GT [a, b]. Inputs must be on the curve (else PBF_EINVAL, where the
  * reference would panic or compute garbage).                                        */

@@ -69,6 +69,8 @@ struct NttPlan {
   uint32_t tw_bits = 0;
   DevBuf tw0, tw1, small_tw;
   std::vector<std::shared_ptr<DevBuf>> rtab;  // per pass
+  bool gl = false;         // passes run on ntt_gl_pass_kernel (standard Goldilocks roots)
+  std::vector<std::shared_ptr<DevBuf>> tc;    // per pass: stage-C tables of ntt_gl_pass_kernel
 };
 
 // Build a plan (validates omega's order and n^-1). Returns PBF status.

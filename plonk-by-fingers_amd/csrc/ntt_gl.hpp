@@ -1,0 +1,288 @@
+// Goldilocks pass kernel for standard roots (gfx950) — the hot path of src/fft.rs
+// CooleyTurkey (fft.rs:55-106) at BASELINE configs 2 and 5.
+//
+// Same Stockham-over-HBM pass structure as ntt_pass_kernel (ntt_kernels.hpp): pass input
+// x[j + r*(n/R)], pre-twiddle w^((n/(Ns*R))*r*(j mod Ns)), an R-point DFT along r,
+// output y[(j/Ns)*Ns*R + (j mod Ns) + k*Ns]. What differs is how the R-point DFT is
+// split, chosen so that every general (table) multiplication that can be a shift is one:
+//
+//   R = 4 * 16 * C  (C = R/64),   r = 16C*s1 + C*s2 + r2,   k = q1 + 4*q2 + 64*k2
+//   stage A  4-point DFT over s1                          -> Z[q1][s2][r2]
+//   stage B  Z *= w_64^(s2*q1)  (a power of two: shift)   16-point DFT over s2
+//                                                          -> Y[k1 = q1 + 4 q2][r2]
+//   stage C  Y *= w_R^(r2*k1)   (table, general multiply)  C-point DFT over r2 -> X[k1 + 64 k2]
+//
+// For a standard root w (w_64 = 2^39, inverse 2^153) every root of order <= 64 is a
+// power of two, so the 4-, 16- and C-point register DFTs and the stage-B twiddle are
+// shift-reductions; only stage C's pre-twiddle (and the pass twiddle) multiply by
+// table entries: one general multiplication per element per pass, the minimum for
+// DFT blocks of <= 64 points (2^20 = 2 passes -> 3 general multiplications per
+// element including the one pass twiddle; ntt_pass_kernel's 4|16|16 split needs 5).
+//
+// Stage B runs one q1 per wave (4 values, 2 waves each), so its twiddle exponents are
+// compile-time constants under a wave-uniform switch. LDS layouts (elements of 8 B):
+//   Z: ((q1*16 + s2)*C + r2)*W + w           (A writes and B reads 64 contiguous)
+//   Y: r2*(65*W) + k1*W + w                  (B writes rows r2 padded by W: 2-pass
+//                                             64-bit accesses; C reads contiguous)
+// Tile: TILE = R x W elements (W = TILE/R columns: W*8 B contiguous runs in HBM), TILE/16
+// threads, 16 elements per thread in every stage.
+#pragma once
+#include "ntt_kernels.hpp"
+
+namespace pbf {
+
+struct GlPassArgs {
+  const uint64_t* in;
+  uint64_t* out;
+  const uint64_t* twpass;  // per-pass [r][k] table w^((n/(Ns*R))*r*k), or null (two-level)
+  const uint64_t* tw0;     // two-level table of w (low part)
+  const uint64_t* tw1;     //                     (high part)
+  const uint64_t* tc;      // stage-C table [r2][k1] = w_R^(r2*k1) (times n^-1 when scaled)
+  uint64_t n;
+  uint32_t log_n;
+  uint32_t log_ns;
+  uint32_t tw_bits;
+  uint32_t blocks_per_poly;
+  uint32_t batch;
+  uint32_t scaled;         // tc carries n^-1: multiply every element, k1 = 0 / r2 = 0 too
+  uint32_t out_split_log;  // != 0: store destination-major [n/S][batch][S] (multi-GPU send layout)
+  uint32_t xcd_kmajor;     // XCD-aware column-major block order (pass-twiddle table reuse in L2)
+};
+
+// x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1.
+template <int K>
+__device__ __forceinline__ uint64_t gl_pow2(uint64_t x) {
+  constexpr int S = ((K % 192) + 192) % 192;
+  if constexpr (S == 0) {
+    return x;
+  } else if constexpr (S < 96) {
+    return Goldilocks::mul_pow2<S>(x);
+  } else {
+    const FieldArgs f{};
+    return Goldilocks::sub(0, Goldilocks::mul_pow2<S - 96>(x), f);
+  }
+}
+
+// Stage-B twiddle: v[s2] *= w_64^(s2*Q1) = 2^(E64*s2*Q1).
+template <int E64, int Q1, int S2 = 1>
+__device__ __forceinline__ void gl_stage_b_twiddle(uint64_t* v) {
+  if constexpr (S2 < 16) {
+    v[S2] = gl_pow2<(E64 * S2 * Q1) % 192>(v[S2]);
+    gl_stage_b_twiddle<E64, Q1, S2 + 1>(v);
+  }
+}
+
+template <int LOGR, int TILE>
+struct GlShape {
+  static constexpr int R = 1 << LOGR;
+  static constexpr int LOGC = LOGR - 6;
+  static constexpr int C = 1 << LOGC;
+  static constexpr int W = TILE / R;
+  static constexpr int NT = TILE / 16;             // 16 elements per thread
+  static constexpr int WPQ = NT / 256;              // waves per stage-B q1 value
+  static constexpr int YP = 65 * W;                 // Y row pitch (elements)
+  static constexpr int LDS = (C * YP > TILE) ? C * YP : TILE;
+  static constexpr int NSUB_C = (64 * W) / NT;      // stage-C sub-DFTs per thread
+  // Y column swizzle: the first pass's stage C reads 8 k1 x 8 w per wave; w ^ ysw(k1)
+  // spreads them over the banks (2 passes per 512-B wave access, the minimum)
+  __host__ __device__ static constexpr int ysw(int k1) {
+    return W == 8 ? 0 : (W == 16 ? ((k1 >> 1) & 1) * 8 : (k1 & 3) * 8);
+  }
+};
+
+// Tile id -> (polynomial, column block). With xcd_kmajor the tiles of one XCD (block ids
+// congruent mod 8) take a contiguous range
+// of column blocks, all polynomials of a block back to back, so each slice of the
+// pass-twiddle table is fetched into that XCD's L2 once per pass, not once per polynomial.
+__device__ __forceinline__ void gl_tile_coords(const GlPassArgs& a, uint32_t tile, uint32_t tiles, uint32_t* poly,
+                                               uint32_t* kb) {
+  if (a.xcd_kmajor) {
+    const uint32_t v = (tile & 7) * (tiles >> 3) + (tile >> 3);
+    *kb = v / a.batch;
+    *poly = v % a.batch;
+  } else {
+    *poly = tile / a.blocks_per_poly;
+    *kb = tile % a.blocks_per_poly;
+  }
+}
+
+// One tile per workgroup (a persistent variant that LDS-DMA'd the next tile during stage
+// C measured 0.52 vs 0.47 ms at 2^20 x 32: the loop's address bookkeeping cost more VALU
+// than the overlap gained; two resident workgroups per CU already overlap each other).
+template <int LOGR, int E64, bool FIRST, int TILE>
+__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_gl_pass_kernel(GlPassArgs a) {
+  using Sh = GlShape<LOGR, TILE>;
+  constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
+  static_assert(LOGR >= 6 && LOGR <= 10, "radix 2^6 .. 2^10");
+  static_assert(Sh::LDS * 8 <= 80 * 1024, "two workgroups per CU");
+  static_assert(Sh::W >= 8 && Sh::WPQ >= 1, "tile shape");
+  __shared__ uint64_t lds[Sh::LDS];
+  const FieldArgs f{};
+  using G = Goldilocks;
+  const int t = threadIdx.x;
+  const uint32_t tiles = a.blocks_per_poly * a.batch;
+  {
+    const uint32_t tile = blockIdx.x;
+    uint32_t poly, kb;
+    gl_tile_coords(a, tile, tiles, &poly, &kb);
+    const uint64_t j0 = (uint64_t)kb * W;
+    const uint64_t* in = a.in + (uint64_t)poly * a.n;
+    const uint64_t stride = a.n >> LOGR;
+
+    // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
+    uint64_t v[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = t + NT * u;
+      const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
+#pragma unroll
+      for (int s1 = 0; s1 < 4; ++s1) v[u * 4 + s1] = in[(j0 + w) + (uint64_t)(16 * C * s1 + C * s2 + r2) * stride];
+    }
+    if constexpr (!FIRST) {
+      const uint64_t kmask = (1ull << a.log_ns) - 1;
+      // in groups of 8 elements (loads of a group issue back to back; bounded live registers)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint64_t tw[8];
+#pragma unroll
+        for (int uu = 0; uu < 2; ++uu) {
+          const int u = 2 * h + uu;
+          const int idx = t + NT * u;
+          const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
+          const uint64_t k = (j0 + w) & kmask;
+#pragma unroll
+          for (int s1 = 0; s1 < 4; ++s1) {
+            const uint64_t r = (uint64_t)(16 * C * s1 + C * s2 + r2);
+            if (a.twpass) {
+              tw[uu * 4 + s1] = a.twpass[(r << a.log_ns) + k];
+            } else {
+              const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
+              tw[uu * 4 + s1] = G::mul(a.tw0[e & ((1ull << a.tw_bits) - 1)], a.tw1[e >> a.tw_bits], f);
+            }
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[8 * h + m] = G::mul(v[8 * h + m], tw[m], f);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = t + NT * u;  // = s2*(C*W) + (r2*W + w)
+      const int s2 = idx / (C * W), rw = idx % (C * W);
+#pragma unroll
+      for (int q1 = 0; q1 < 4; ++q1) lds[(q1 * 16 + s2) * (C * W) + rw] = v[u * 4 + bitrev_c(q1, 2)];
+    }
+    __syncthreads();
+
+    // ---------------- stage B: one q1 per wave; shift twiddles; 16-point DFT over s2
+    {
+      const int wave = t >> 6;
+      const int q1 = wave / Sh::WPQ;
+      const int rw = (wave % Sh::WPQ) * 64 + (t & 63);  // r2*W + w
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
+      switch (__builtin_amdgcn_readfirstlane(q1)) {
+        case 1: gl_stage_b_twiddle<E64, 1>(v); break;
+        case 2: gl_stage_b_twiddle<E64, 2>(v); break;
+        case 3: gl_stage_b_twiddle<E64, 3>(v); break;
+        default: break;
+      }
+      dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
+      __syncthreads();
+      const int r2 = rw / W, w = rw % W;
+#pragma unroll
+      for (int q2 = 0; q2 < 16; ++q2) {
+        const int k1 = q1 + 4 * q2;
+        lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))] = v[bitrev_c(q2, 4)];
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage C: table twiddle w_R^(r2*k1); C-point DFT over r2
+    // sub-DFT (k1, w) of thread t: FIRST pass 8 k1 x 8 w per wave (64-B runs of k in the
+    // output rows out[j*R + k]); later passes w fastest (W-element runs of j)
+    auto c_map = [&](int u, int* k1, int* w) {
+      const int idx = t + NT * u;
+      if constexpr (FIRST) {
+        *k1 = (idx & 7) + 8 * ((idx >> 3) / W);
+        *w = (idx >> 3) % W;
+      } else {
+        *k1 = idx / W;
+        *w = idx % W;
+      }
+    };
+    uint64_t x[Sh::NSUB_C * C];
+#pragma unroll
+    for (int u = 0; u < Sh::NSUB_C; ++u) {
+      int k1, w;
+      c_map(u, &k1, &w);
+#pragma unroll
+      for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
+    }
+    uint64_t tw[Sh::NSUB_C * C];
+    const int r2lo = a.scaled ? 0 : 1;  // scaled table carries n^-1: every element multiplies
+#pragma unroll
+    for (int u = 0; u < Sh::NSUB_C; ++u) {
+      int k1, w;
+      c_map(u, &k1, &w);
+#pragma unroll
+      for (int r2 = 0; r2 < C; ++r2) tw[u * C + r2] = (r2 >= r2lo) ? a.tc[r2 * 64 + k1] : 1;
+    }
+    if (a.scaled) {
+#pragma unroll
+      for (int m = 0; m < Sh::NSUB_C * C; ++m) x[m] = G::mul(x[m], tw[m], f);
+    } else {
+      // r2 = 0 rows multiply by 1 and are skipped; k1 = 0 lanes multiply by 1 (a per-lane
+      // branch would only diverge)
+#pragma unroll
+      for (int u = 0; u < Sh::NSUB_C; ++u)
+#pragma unroll
+        for (int r2 = 1; r2 < C; ++r2) x[u * C + r2] = G::mul(x[u * C + r2], tw[u * C + r2], f);
+    }
+    if constexpr (C > 1) {
+#pragma unroll
+      for (int u = 0; u < Sh::NSUB_C; ++u) dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f);
+    }
+
+    // ---------------- store
+    if constexpr (FIRST) {
+      uint64_t* o = a.out + (uint64_t)poly * a.n;
+#pragma unroll
+      for (int u = 0; u < Sh::NSUB_C; ++u) {
+        int k1, w;
+        c_map(u, &k1, &w);
+        const uint64_t base = (j0 + w) << LOGR;
+#pragma unroll
+        for (int k2 = 0; k2 < C; ++k2) o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
+      }
+    } else {
+      const uint64_t ns_mask = (1ull << a.log_ns) - 1;
+      uint64_t* out = a.out + (uint64_t)poly * a.n;
+      const uint32_t sl = a.out_split_log;
+#pragma unroll
+      for (int u = 0; u < Sh::NSUB_C; ++u) {
+        int k1, w;
+        c_map(u, &k1, &w);
+        const uint64_t j = j0 + w;
+        const uint64_t base = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask);
+        if (sl == 0) {
+#pragma unroll
+          for (int k2 = 0; k2 < C; ++k2)
+            out[base + ((uint64_t)(k1 + 64 * k2) << a.log_ns)] = x[u * C + bitrev_c(k2, LOGC)];
+        } else {
+          const uint64_t smask = (1ull << sl) - 1;
+#pragma unroll
+          for (int k2 = 0; k2 < C; ++k2) {
+            const uint64_t kk = base + ((uint64_t)(k1 + 64 * k2) << a.log_ns);
+            a.out[((((kk >> sl) * a.batch) + poly) << sl) + (kk & smask)] = x[u * C + bitrev_c(k2, LOGC)];
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace pbf

@@ -2,7 +2,7 @@
 #include <cstdlib>
 #include <cstring>
 #include "internal.hpp"
-#include "ntt_kernels.hpp"
+#include "ntt_gl.hpp"
 
 namespace pbf {
 
@@ -159,6 +159,27 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
     if (rc) return rc;
     p->rtab.push_back(b);
   }
+  // ntt_gl_pass_kernel (standard Goldilocks roots, radices 2^6..2^10): stage-C tables
+  // tc[r2][k1] = w_R^(r2*k1), r2 < R/64, k1 < 64; the last pass of an inverse carries n^-1
+  p->gl = p->e64 >= 0 && !getenv("PBF_NTT_LEGACY");
+  for (int lr : p->logr) p->gl = p->gl && lr >= 6 && lr <= 10;
+  if (p->gl) {
+    for (size_t i = 0; i < p->logr.size(); ++i) {
+      const uint64_t R = 1ull << p->logr[i], C = R / 64;
+      const uint64_t wr = hpow(w, n / R, m);
+      const bool scaled = p->inverse && i + 1 == p->logr.size();
+      std::vector<uint64_t> tc(C * 64);
+      for (uint64_t r2 = 0; r2 < C; ++r2)
+        for (uint64_t k1 = 0; k1 < 64; ++k1) {
+          const uint64_t z = hpow(wr, r2 * k1, m);
+          tc[r2 * 64 + k1] = scaled ? hmul(z, p->n_inv, m) : z;
+        }
+      auto b = std::make_shared<DevBuf>();
+      rc = upload(*b, tc);
+      if (rc) return rc;
+      p->tc.push_back(b);
+    }
+  }
   return 0;
 }
 
@@ -166,8 +187,6 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
 typedef void (*PassFn)(PassArgs);
 
 static int cols_for(int logr) {
-  const char* env = getenv("PBF_NTT_WIDE");  // A/B: widest tile (W*R = 16384) for small radices
-  if (env && logr <= 9) return 16384 >> logr > 64 ? 64 : 16384 >> logr;
   // radix 2^10: 8 columns (64-KiB tile, two workgroups per CU overlap each other's HBM
   // and arithmetic phases; measured 0.548 vs 0.585 ms for 16 columns at 2^20 x 32)
   return logr < 10 ? 16 : (logr == 10 ? 8 : (logr == 11 ? 8 : 4));
@@ -207,27 +226,11 @@ static PassCfg pass_cfg(int logr) {
 
 template <class F, int E>
 static PassFn pass_fn_e(int logr, PassCfg c) {
-  PBF_PASS_DB(F, 6, 64, 4, E)
-  PBF_PASS_DB(F, 7, 64, 4, E)
-  PBF_PASS_DB(F, 8, 32, 4, E)
-  PBF_PASS_DB(F, 9, 16, 4, E)
-  PBF_PASS_DB(F, 10, 8, 4, E)
-  PBF_PASS_RP(F, 10, 8, 4, E)
-  PBF_PASS_RP(F, 10, 16, 4, E)
-  PBF_PASS(F, 10, 16, 4, E)
+  PBF_PASS_DB(F, 10, 8, 4, E)  // A/B only (PBF_NTT_CFG=8,4,1): measured slower, DESIGN.md "NTT"
+  PBF_PASS_RP(F, 10, 8, 4, E)  // A/B only (PBF_NTT_CFG=8,4,2)
   PBF_PASS(F, 10, 8, 4, E)
-  PBF_PASS_NT(F, 10, 8, 4, 256, E)
-  PBF_PASS_NT(F, 10, 16, 4, 512, E)
-  PBF_PASS(F, 10, 8, 3, E)
-  PBF_PASS(F, 10, 8, 5, E)
-  PBF_PASS(F, 10, 16, 5, E)
-  PBF_PASS(F, 10, 4, 4, E)
-  PBF_PASS(F, 10, 4, 3, E)
   PBF_PASS(F, 11, 8, 4, E)
   PBF_PASS(F, 12, 4, 4, E)
-  PBF_PASS(F, 8, 64, 4, E)
-  PBF_PASS(F, 9, 32, 4, E)
-  // single-tile fallbacks for every radix (used when a DB shape is not instantiated)
   PBF_PASS(F, 6, 16, 4, E)
   PBF_PASS(F, 7, 16, 4, E)
   PBF_PASS(F, 8, 16, 4, E)
@@ -362,6 +365,70 @@ static uint32_t persistent_grid(PassFn fn, int nt, uint64_t tiles) {
   return (uint32_t)(tiles < slots ? tiles : slots);
 }
 
+typedef void (*GlPassFn)(GlPassArgs);
+
+template <int E, int T>
+static GlPassFn gl_fn_t(int logr, bool first) {
+  switch (logr) {
+    case 6: return first ? ntt_gl_pass_kernel<6, E, true, T> : ntt_gl_pass_kernel<6, E, false, T>;
+    case 7: return first ? ntt_gl_pass_kernel<7, E, true, T> : ntt_gl_pass_kernel<7, E, false, T>;
+    case 8: return first ? ntt_gl_pass_kernel<8, E, true, T> : ntt_gl_pass_kernel<8, E, false, T>;
+    case 9: return first ? ntt_gl_pass_kernel<9, E, true, T> : ntt_gl_pass_kernel<9, E, false, T>;
+    default: return nullptr;
+  }
+}
+
+// Tile of R x W elements per workgroup: 4096 (four workgroups per CU) or 8192 (two);
+// radix 2^10 always 8192 (W >= 8: 64-B runs in HBM).
+static int gl_tile(int logr) {
+  if (logr >= 10) return 8192;
+  const char* env = getenv("PBF_NTT_TILE");  // A/B override
+  return (env && atoi(env) == 8192) ? 8192 : 4096;
+}
+
+template <int E>
+static GlPassFn gl_fn_e(int logr, bool first, int tile) {
+  if (logr == 10) return first ? ntt_gl_pass_kernel<10, E, true, 8192> : ntt_gl_pass_kernel<10, E, false, 8192>;
+  return tile == 8192 ? gl_fn_t<E, 8192>(logr, first) : gl_fn_t<E, 4096>(logr, first);
+}
+
+// Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
+static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log) {
+  const size_t P = p.logr.size();
+  uint32_t log_ns = 0;
+  for (size_t i = 0; i < P; ++i) {
+    const int lr = p.logr[i];
+    const int tile = gl_tile(lr);
+    GlPassFn fn = p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile) : gl_fn_e<153>(lr, log_ns == 0, tile);
+    if (!fn) return fail(1, "no Goldilocks pass kernel for this radix");
+    const uint64_t W = (uint64_t)tile >> lr;
+    if ((p.n >> lr) % W) return fail(1, "transform too small for the pass tile");
+    GlPassArgs a;
+    a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p);
+    a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p);
+    a.twpass = (const uint64_t*)p.twpass[i]->p;
+    a.tw0 = (const uint64_t*)p.tw0.p;
+    a.tw1 = (const uint64_t*)p.tw1.p;
+    a.tc = (const uint64_t*)p.tc[i]->p;
+    a.n = p.n;
+    a.log_n = p.log_n;
+    a.log_ns = log_ns;
+    a.tw_bits = p.tw_bits;
+    a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
+    a.batch = (uint32_t)batch;
+    a.scaled = (p.inverse && i == P - 1) ? 1 : 0;
+    a.out_split_log = (i == P - 1) ? split_log : 0;
+    const uint64_t tiles = (uint64_t)a.blocks_per_poly * batch;
+    if (tiles > 0x7fffffffull) return fail(1, "batch too large");
+    a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
+    hipLaunchKernelGGL(fn, dim3((uint32_t)tiles), dim3(tile / 16), 0, stream, a);
+    PBF_HIP(hipGetLastError());
+    log_ns += lr;
+  }
+  return 0;
+}
+
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log) {
   if (batch == 0) return 0;
@@ -385,6 +452,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   if (!rc && P > 2) rc = s1.ensure(bytes);
   if (rc) return rc;
   uint32_t log_ns = 0;
+  if (p.gl) return run_gl_passes(p, d_in, d_out, batch, s0, s1, stream, split_log);
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
     PassCfg cfg = pass_cfg(lr);
