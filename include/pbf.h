@@ -126,6 +126,26 @@ int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t*
 /* SRS::create (plonk.rs:35-48): out = [G, G*s, ..., G*s^n] (n+1 points)             */
 int pbf_srs_create_bn254(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* out);
 
+/* ---- BN254 pairing (BASELINE config 4 "pairing check") ------------------------
+ * The BN254 instance of Pairing::pairing (src/ec.rs:87-93; the reference's own is the
+ * toy reduced Tate pairing, src/pbh/pairing.rs:12-47) as Plonk::verify uses it
+ * (src/plonk.rs:646-647): optimal ate, e(P, Q) = f_{6u+2,Q}(P)...^((q^12-1)/r).
+ * G1: 8 x uint64_t affine (as above). G2: 16 x uint64_t affine on the twist
+ * y^2 = x^3 + 3/(9+u) over Fq2 = Fq[u]/(u^2+1): x.c0, x.c1, y.c0, y.c1 (4 limbs each),
+ * all zero = identity. GT: 48 x uint64_t = 12 Fq in the tower order of
+ * Fq12 = Fq6[w]/(w^2-v), Fq6 = Fq2[v]/(v^3-(9+u)): c0.a0, c0.a1, c0.a2, c1.a0, c1.a1,
+ * c1.a2 (each Fq2 as c0, c1). Inputs must be subgroup points (not checked; coordinates
+ * are checked canonical, else PBF_EINVAL).                                             */
+int pbf_pairing_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out);
+int pbf_pairing_bn254_dev(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_g2, size_t n, uint64_t* d_out,
+                          void* stream);
+/* *ok = (prod_i e(g1_i, g2_i) == 1): n Miller loops, one shared final exponentiation.
+ * The KZG opening check of Plonk::verify (plonk.rs:646-650) is n = 2:
+ * e(W, [s]G2) * e(-(C - y G + z W), G2) == 1.                                          */
+int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, int* ok);
+/* out_i = scalars_i * pts_i on the twist (G2P::mul, src/pbh/g2.rs:82-101): SRS [s]G2  */
+int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars, size_t n, uint64_t* out);
+
 /* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/{g1,g2,gt,pairing}.rs) -------------------
  * 32-bit words: G1 [x, y, inf] over F101 (y^2 = x^3 + 3), G2 [a, b] (a + b*u over
  * F101[u]/(u^2+2)), GT [a, b]. Inputs must be on the curve (else PBF_EINVAL, where the

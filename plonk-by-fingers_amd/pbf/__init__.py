@@ -55,6 +55,10 @@ SIGNATURES = [
     ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
     ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
+    ("pbf_pairing_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
+    ("pbf_pairing_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    ("pbf_pairing_check_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, ctypes.POINTER(ctypes.c_int)]),
+    ("pbf_g2_bn254_mul", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
     ("pbf_pbh_g1_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_g2_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_gt_pow", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
@@ -234,6 +238,39 @@ class Context:
         _check(fn(self.h, a.ctypes.data_as(_p32), b.ctypes.data_as(_p32), n, out.ctypes.data_as(_p32)))
         return [tuple(int(x) for x in out[i * width_out:(i + 1) * width_out]) for i in range(n)]
 
+    # ---- BN254 pairing (config 4 pairing check; pairing.hip)
+    def pairing_bn254(self, g1s, g2s) -> np.ndarray:
+        """[(x, y)] G1 affine and [((x0, x1), (y0, y1))] G2 affine (None = identity) ->
+        n x 12 Fq ints (tower order c0.a0.re, c0.a0.im, ..., c1.a2.im)."""
+        n = len(g1s)
+        a = _g1_limbs(g1s)
+        b = _g2_limbs(g2s)
+        out = np.zeros(n * 48, dtype=np.uint64)
+        _check(self.lib.pbf_pairing_bn254(self.h, _ptr(a), _ptr(b), n, _ptr(out)))
+        return [limbs_to_ints(out[48 * i: 48 * (i + 1)]) for i in range(n)]
+
+    def pairing_bn254_dev(self, d_g1: int, d_g2: int, n: int, d_out: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_pairing_bn254_dev(self.h, d_g1, d_g2, n, d_out, stream))
+
+    def pairing_check_bn254(self, g1s, g2s) -> bool:
+        a = _g1_limbs(g1s)
+        b = _g2_limbs(g2s)
+        ok = ctypes.c_int(-1)
+        _check(self.lib.pbf_pairing_check_bn254(self.h, _ptr(a), _ptr(b), len(g1s), ctypes.byref(ok)))
+        return ok.value == 1
+
+    def g2_bn254_mul(self, pts, scalars) -> list:
+        n = len(pts)
+        a = _g2_limbs(pts)
+        s = ints_to_limbs([int(x) for x in scalars])
+        out = np.zeros(n * 16, dtype=np.uint64)
+        _check(self.lib.pbf_g2_bn254_mul(self.h, _ptr(a), _ptr(s), n, _ptr(out)))
+        res = []
+        for i in range(n):
+            v = limbs_to_ints(out[16 * i: 16 * (i + 1)])
+            res.append(None if not any(v) else ((v[0], v[1]), (v[2], v[3])))
+        return res
+
     def pbh_g1_mul(self, pts, scalars):
         return self._u32call(self.lib.pbf_pbh_g1_mul, pts, scalars, 3, len(scalars))
 
@@ -268,6 +305,14 @@ class Context:
 
 BN254_R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 BN254_Q = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+
+
+def _g1_limbs(pts) -> np.ndarray:
+    return ints_to_limbs([c for p in pts for c in ((0, 0) if p is None else p)])
+
+
+def _g2_limbs(pts) -> np.ndarray:
+    return ints_to_limbs([c for p in pts for c in ((0, 0, 0, 0) if p is None else (p[0][0], p[0][1], p[1][0], p[1][1]))])
 
 
 def ints_to_limbs(values) -> np.ndarray:
