@@ -146,6 +146,39 @@ int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2
 /* out_i = scalars_i * pts_i on the twist (G2P::mul, src/pbh/g2.rs:82-101): SRS [s]G2  */
 int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars, size_t n, uint64_t* out);
 
+/* ---- Generalised PLONK prover / verifier over BN254 (BASELINE config 5) ---------
+ * Plonk::prove / Plonk::verify (src/plonk.rs:191-650) for n = 2^k >= 8 gates with
+ * HF = GF = Fr, G1/G2 of BN254 and the pairing above; t(x) split into three parts of
+ * n+2 coefficients (plonk.rs:376-378 generalised). Field elements canonical 4 x u64.
+ *   q:      5 x n x 4   (columns q_l, q_r, q_o, q_m, q_c)
+ *   copies: 3 x n x 2   (columns c_a, c_b, c_c; per wire (kind 0=A 1=B 2=C, 1-based index))
+ *   abc:    3 x n x 4   (witness columns a, b, c)
+ *   chal:   5 x 4       (alpha, beta, gamma, z, v)      rnd: 9 x 4 (b1..b9)
+ *   k1k2:   2 x 4       (PlonkTypes::K1, K2: cosets k1 H, k2 H, plonk.rs:133-139)
+ *   srs:    srs_m x 8   affine G1 [G, sG, s^2 G, ...] (SRS::create); prove needs
+ *           srs_m >= 2n+2 in mode 0, >= n+3 in mode 1; verify >= n. g2: [G2, [s]G2].
+ *   out_pts 9 x 8: a_s b_s c_s z_s t_lo_s t_mid_s t_hi_s w_z_s w_zw_s
+ *   out_f   7 x 4: a_z b_z c_z s_sigma_1_z s_sigma_2_z r_z z_omega_z   (Proof, plonk.rs:61-95)
+ * mode 0 = the reference's formulas (r_3(x) of plonk.rs:414-416; verifier step 7 of
+ * plonk.rs:575-581), mode 1 = the paper linearisation the verifier checks (SURVEY §0.7:
+ * with mode 0 an honest proof verifies only when alpha = 1, as in the reference).
+ * Errors: PBF_EINVAL for an unsatisfied circuit (constraints.rs:198), a zero permutation
+ * denominator (plonk.rs:297), a non-divisible quotient (plonk.rs:370), short SRS.       */
+int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies, const uint64_t* abc,
+                          const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* srs,
+                          size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f);
+int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                              const uint64_t* d_abc, const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2,
+                              const uint64_t* d_srs, size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f,
+                              void* stream);
+int pbf_plonk_verify_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies, const uint64_t* srs,
+                           size_t srs_m, const uint64_t* g2, const uint64_t* proof_pts, const uint64_t* proof_f,
+                           const uint64_t* chal, const uint64_t* u, const uint64_t* k1k2, int mode, int* ok);
+int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                               const uint64_t* d_srs, size_t srs_m, const uint64_t* g2, const uint64_t* proof_pts,
+                               const uint64_t* proof_f, const uint64_t* chal, const uint64_t* u, const uint64_t* k1k2,
+                               int mode, int* ok, void* stream);
+
 /* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/{g1,g2,gt,pairing}.rs) -------------------
  * 32-bit words: G1 [x, y, inf] over F101 (y^2 = x^3 + 3), G2 [a, b] (a + b*u over
  * F101[u]/(u^2+2)), GT [a, b]. Inputs must be on the curve (else PBF_EINVAL, where the

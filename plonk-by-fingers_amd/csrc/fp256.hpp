@@ -152,6 +152,19 @@ struct Fp256 {
   }
 };
 
+// 4 x uint64_t little-endian (the ABI layout) <-> 8 x uint32_t limbs
+__host__ __device__ inline U256 u256_from_u64(const uint64_t* l) {
+  U256 r;
+  for (int i = 0; i < 4; ++i) {
+    r.w[2 * i] = (uint32_t)l[i];
+    r.w[2 * i + 1] = (uint32_t)(l[i] >> 32);
+  }
+  return r;
+}
+__host__ __device__ inline void u256_to_u64(const U256& a, uint64_t* l) {
+  for (int i = 0; i < 4; ++i) l[i] = (uint64_t)a.w[2 * i] | ((uint64_t)a.w[2 * i + 1] << 32);
+}
+
 typedef Fp256<Bn254FrParams> Fr;
 typedef Fp256<Bn254FqParams> Fq;
 

@@ -114,4 +114,11 @@ struct pbf_ctx {
   static hipStream_t pick(void* s) { return (hipStream_t)s; }
   hipStream_t host_stream() const { return user_stream ? user_stream : stream; }
   int plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, pbf::NttPlan** out);
+  // named scratch buffers of the larger pipelines (prover), freed with the context
+  std::map<std::string, std::unique_ptr<pbf::DevBuf>> named;
+  pbf::DevBuf& buf(const std::string& name) {
+    auto& b = named[name];
+    if (!b) b.reset(new pbf::DevBuf());
+    return *b;
+  }
 };

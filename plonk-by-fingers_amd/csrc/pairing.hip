@@ -55,18 +55,6 @@ static const uint64_t K_HARD[12] = {0xe81bb482ccdf42b1ull, 0x5abf5cc4f49c36d4ull
                                     0x6c0eb522d5b12278ull, 0x331ec15183177fafull, 0x01baaa710b0759adull};
 static const uint64_t K_ATE_LO = 0x9d797039be763ba8ull;  // 6u+2 = 2^64 + K_ATE_LO
 
-__host__ __device__ inline U256 u256_from_u64(const uint64_t* l) {
-  U256 r;
-  for (int i = 0; i < 4; ++i) {
-    r.w[2 * i] = (uint32_t)l[i];
-    r.w[2 * i + 1] = (uint32_t)(l[i] >> 32);
-  }
-  return r;
-}
-__host__ __device__ inline void u256_to_u64(const U256& a, uint64_t* l) {
-  for (int i = 0; i < 4; ++i) l[i] = (uint64_t)a.w[2 * i] | ((uint64_t)a.w[2 * i + 1] << 32);
-}
-
 // ---------------------------------------------------------------- tower arithmetic
 struct Fq2 {
   U256 c0, c1;

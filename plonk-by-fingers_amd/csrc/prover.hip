@@ -1,0 +1,1031 @@
+// Generalised PLONK prover over BN254 on gfx950 — BASELINE config 5 and the §8(f) rows:
+// Plonk::prove (src/plonk.rs:191-466) for any power-of-two number of gates n, with every
+// O(n^2)/O(n^3) step of the reference replaced by an equivalent O(n log n) one:
+//
+//   interpolate_at_h (Vandermonde inverse, plonk.rs:177-179)   -> batched INTT
+//   round-2 accumulator (per-row s_sigma.eval, plonk.rs:278-299) -> sigma labels +
+//        batch inversion + prefix product (the values s_sigma_k(w^j) ARE sigma_k[j])
+//   t(x) = (t1 + t2 - t3 + t4) / Z_H (Poly mul/div, plonk.rs:339-370) -> 13 coset NTTs of
+//        size 4n, one pointwise quotient kernel (Z_H(x) = x^n - 1 takes 4 values on the
+//        coset), one coset INTT; the division's `rem == 0` assert becomes "coefficients
+//        3n+6 .. 4n-1 of t are zero" (also the 3-way split's precondition, plonk.rs:376-378
+//        generalised to n+2 coefficients per part)
+//   evaluations at z (Poly::eval, plonk.rs:393-399)              -> chunked Horner + reduction
+//   W_z, W_zw (Poly::div by x - z, plonk.rs:430-442)             -> pointwise on the coset
+//        (the numerators vanish at z exactly) + coset INTT
+//   SRS::eval_at_s commitments (plonk.rs:51-58)                 -> Pippenger MSM (msm.hip)
+//
+// Every output is the unique mathematical value the reference's formulas define (the
+// same polynomials, evaluations and group elements), so results are bit-identical to a
+// literal restatement (oracle/plonk_bn254.py). mode 0 keeps the reference's r_3(x)
+// (plonk.rs:414-416: z(x) * s_sigma_3(x) * ..., product computed on the coset); mode 1
+// uses the linearisation its verifier checks.
+//
+// Field elements at rest in HBM: canonical Fr, 4 x u64 little-endian (the ABI layout);
+// kernels convert to Montgomery on load and back on store.
+#include <cstring>
+#include <vector>
+#include "../../include/pbf.h"
+#include "ec_bn254.hpp"
+#include "internal.hpp"
+
+namespace pbf {
+
+typedef uint64_t fr4[4];
+
+__device__ __forceinline__ U256 ldr(const uint64_t* p) { return Fr::to_mont(u256_from_u64(p)); }
+__device__ __forceinline__ void str(uint64_t* p, const U256& m) { u256_to_u64(Fr::from_mont(m), p); }
+__host__ __device__ __forceinline__ U256 fr_one_m() { return Fr::to_mont(Fr::one_plain()); }
+
+__device__ U256 fr_pow(U256 a, uint64_t e) {
+  U256 r = fr_one_m();
+  while (e) {
+    if (e & 1) r = Fr::mul(r, a);
+    a = Fr::mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+// a^(r-2): Fermat inverse (a != 0)
+__device__ U256 fr_inv(const U256& a) {
+  U256 r = fr_one_m();
+  for (int i = 255; i >= 0; --i) {
+    r = Fr::mul(r, r);
+    uint32_t e = Bn254FrParams::P[i / 32] - (i < 32 ? 2u : 0u);
+    if ((e >> (i % 32)) & 1) r = Fr::mul(r, a);
+  }
+  return r;
+}
+
+constexpr int PV_CHUNK = 64;  // elements per thread in the chunked kernels
+
+static uint32_t blocks_for(uint64_t threads) {
+  uint64_t b = (threads + 255) / 256;
+  return (uint32_t)(b ? b : 1);
+}
+
+// out[i] = i < len ? in[i] * base^(i + off) : 0, i < count (coset scaling, zero padding;
+// base = 1 plain copy). Chunks of PV_CHUNK consecutive elements per thread.
+__global__ void k_scale_pow(const uint64_t* in, uint64_t len, uint64_t* out, uint64_t count, U256 base, uint64_t off) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * PV_CHUNK;
+  if (i0 >= count) return;
+  U256 x = fr_pow(base, i0 + off);
+  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < count; ++i) {
+    if (i < len) str(out + 4 * i, Fr::mul(ldr(in + 4 * i), x));
+    else for (int k = 0; k < 4; ++k) out[4 * i + k] = 0;
+    x = Fr::mul(x, base);
+  }
+}
+
+// out[i] = start * base^i
+__global__ void k_powers(uint64_t* out, uint64_t count, U256 base, U256 start) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * PV_CHUNK;
+  if (i0 >= count) return;
+  U256 x = Fr::mul(start, fr_pow(base, i0));
+  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < count; ++i) {
+    str(out + 4 * i, x);
+    x = Fr::mul(x, base);
+  }
+}
+
+// copy_constraints_to_roots (plonk.rs:181-189): sigma[col][i] = {w^j, k1 w^j, k2 w^j}[kind]
+__global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n, U256 k1, U256 k2, uint64_t* sigma,
+                        int* bad) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= 3 * n) return;
+  const uint64_t kind = copies[2 * id], idx = copies[2 * id + 1];
+  if (kind > 2 || idx < 1 || idx > n) {
+    *bad = 1;
+    for (int k = 0; k < 4; ++k) sigma[4 * id + k] = 0;
+    return;
+  }
+  U256 h = ldr(hpow + 4 * (idx - 1));
+  if (kind == 1) h = Fr::mul(h, k1);
+  if (kind == 2) h = Fr::mul(h, k2);
+  str(sigma + 4 * id, h);
+}
+
+// Constrains::satisfies (constraints.rs:198-230, with its q_l * b term): gates and copies
+__global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64_t* copies, uint64_t n, int* bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U256 ql = ldr(q + 4 * i), qo = ldr(q + 4 * (2 * n + i)), qm = ldr(q + 4 * (3 * n + i)),
+             qc = ldr(q + 4 * (4 * n + i));
+  const U256 a = ldr(abc + 4 * i), b = ldr(abc + 4 * (n + i)), c = ldr(abc + 4 * (2 * n + i));
+  U256 r = Fr::add(Fr::mul(ql, a), Fr::mul(ql, b));
+  r = Fr::add(r, Fr::mul(qo, c));
+  r = Fr::add(r, Fr::mul(Fr::mul(qm, a), b));
+  r = Fr::add(r, qc);
+  if (!Fr::is_zero(r)) *bad = 1;
+  for (int col = 0; col < 3; ++col) {
+    const uint64_t kind = copies[2 * (col * n + i)], idx = copies[2 * (col * n + i) + 1];
+    if (kind > 2 || idx < 1 || idx > n) { *bad = 1; continue; }
+    const uint64_t* v = abc + 4 * (kind * n + idx - 1);
+    const uint64_t* w = abc + 4 * (col * n + i);
+    if (v[0] != w[0] || v[1] != w[1] || v[2] != w[2] || v[3] != w[3]) *bad = 1;
+  }
+}
+
+// round 2 terms (plonk.rs:282-297) for row j < n-1: num_j = dend, den_j = dsor
+__global__ void k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n, U256 beta,
+                             U256 gamma, U256 k1, U256 k2, uint64_t* num, uint64_t* den) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j + 1 >= n) return;
+  const U256 a = ldr(abc + 4 * j), b = ldr(abc + 4 * (n + j)), c = ldr(abc + 4 * (2 * n + j));
+  const U256 w = ldr(hpow + 4 * j);
+  const U256 bw = Fr::mul(beta, w);
+  U256 d1 = Fr::add(Fr::add(a, bw), gamma);
+  U256 d2 = Fr::add(Fr::add(b, Fr::mul(bw, k1)), gamma);
+  U256 d3 = Fr::add(Fr::add(c, Fr::mul(bw, k2)), gamma);
+  str(num + 4 * j, Fr::mul(Fr::mul(d1, d2), d3));
+  U256 e1 = Fr::add(Fr::add(a, Fr::mul(beta, ldr(sigma + 4 * j))), gamma);
+  U256 e2 = Fr::add(Fr::add(b, Fr::mul(beta, ldr(sigma + 4 * (n + j)))), gamma);
+  U256 e3 = Fr::add(Fr::add(c, Fr::mul(beta, ldr(sigma + 4 * (2 * n + j)))), gamma);
+  str(den + 4 * j, Fr::mul(Fr::mul(e1, e2), e3));
+}
+
+// out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
+// chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297)
+constexpr int INV_CHUNK = 32;
+__global__ void k_div_batch(const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * INV_CHUNK;
+  if (i0 >= count) return;
+  const int m = (int)((count - i0) < INV_CHUNK ? (count - i0) : INV_CHUNK);
+  U256 pre[INV_CHUNK];
+  U256 acc = fr_one_m();
+  for (int k = 0; k < m; ++k) {
+    const U256 d = ldr(den + 4 * (i0 + k));
+    if (Fr::is_zero(d)) { *bad = 1; return; }
+    pre[k] = acc;
+    acc = Fr::mul(acc, d);
+  }
+  U256 inv = fr_inv(acc);  // 1 / prod
+  for (int k = m - 1; k >= 0; --k) {
+    const U256 d = ldr(den + 4 * (i0 + k));
+    const U256 dinv = Fr::mul(inv, pre[k]);  // 1 / d_k
+    inv = Fr::mul(inv, d);
+    str(out + 4 * (i0 + k), num ? Fr::mul(ldr(num + 4 * (i0 + k)), dinv) : dinv);
+  }
+}
+
+// ---- exclusive prefix product: out[0] = 1, out[i] = prod_{j<i} in[j]  (i < count)
+constexpr int SCAN_T = 256, SCAN_PER = 8, SCAN_BLK = SCAN_T * SCAN_PER;
+
+__device__ void block_scan_mul(U256* sh, int t) {  // inclusive Hillis-Steele over SCAN_T
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    U256 v = sh[t];
+    if (t >= off) v = Fr::mul(sh[t - off], v);
+    __syncthreads();
+    sh[t] = v;
+    __syncthreads();
+  }
+}
+
+// phase 1: block-local inclusive products (in place into out), block totals
+__global__ void __launch_bounds__(SCAN_T) k_scan1(const uint64_t* in, uint64_t* out, uint64_t count, uint64_t* totals) {
+  __shared__ U256 sh[SCAN_T];
+  const int t = threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * SCAN_BLK + (uint64_t)t * SCAN_PER;
+  U256 v[SCAN_PER];
+  U256 acc = fr_one_m();
+  for (int k = 0; k < SCAN_PER; ++k) {
+    const uint64_t i = base + k;
+    const U256 x = i < count ? ldr(in + 4 * i) : fr_one_m();
+    acc = Fr::mul(acc, x);
+    v[k] = acc;
+  }
+  sh[t] = acc;
+  __syncthreads();
+  block_scan_mul(sh, t);
+  const U256 pre = t ? sh[t - 1] : fr_one_m();
+  for (int k = 0; k < SCAN_PER; ++k) {
+    const uint64_t i = base + k;
+    if (i < count) str(out + 4 * i, Fr::mul(pre, v[k]));
+  }
+  if (t == SCAN_T - 1) str(totals + 4 * blockIdx.x, sh[t]);
+}
+
+// phase 2: exclusive scan of the block totals in one block (any number of totals)
+__global__ void __launch_bounds__(SCAN_T) k_scan2(uint64_t* totals, uint64_t nb) {
+  __shared__ U256 sh[SCAN_T];
+  const int t = threadIdx.x;
+  const uint64_t per = (nb + SCAN_T - 1) / SCAN_T;
+  const uint64_t b0 = (uint64_t)t * per;
+  U256 acc = fr_one_m();
+  for (uint64_t k = 0; k < per; ++k)
+    if (b0 + k < nb) acc = Fr::mul(acc, ldr(totals + 4 * (b0 + k)));
+  sh[t] = acc;
+  __syncthreads();
+  block_scan_mul(sh, t);
+  U256 run = t ? sh[t - 1] : fr_one_m();  // exclusive prefix of this thread's range
+  for (uint64_t k = 0; k < per; ++k) {
+    if (b0 + k >= nb) break;
+    const U256 x = ldr(totals + 4 * (b0 + k));
+    str(totals + 4 * (b0 + k), run);
+    run = Fr::mul(run, x);
+  }
+}
+
+// phase 3: out[i] = (inclusive product up to i-1) = block exclusive prefix * local
+// inclusive[i-1]; reads the phase-1 inclusive values from incl, writes exclusive into out
+__global__ void k_scan3(const uint64_t* incl, uint64_t* out, uint64_t count, const uint64_t* totals) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  if (i == 0) { str(out, fr_one_m()); return; }
+  const uint64_t j = i - 1;
+  const uint64_t blk = j / SCAN_BLK;
+  str(out + 4 * i, Fr::mul(ldr(totals + 4 * blk), ldr(incl + 4 * j)));
+}
+
+// coeff[idx] += delta (blinding: (b_lo + b_hi x [+ b x^2]) * (x^n - 1), plonk.rs:250-252, 304)
+struct Blind {
+  uint64_t idx[6];
+  U256 delta[6];
+  int count;
+};
+__global__ void k_blind(uint64_t* coeff, Blind b) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int k = 0; k < b.count; ++k) str(coeff + 4 * b.idx[k], Fr::add(ldr(coeff + 4 * b.idx[k]), b.delta[k]));
+}
+
+// out[i] = sum_k c_k * in_k[i] (+ c0 at i = 0); in_k shorter than i contributes 0
+struct LinComb {
+  const uint64_t* in[10];
+  uint64_t len[10];
+  U256 c[10];
+  int k;
+  U256 c0;
+};
+__global__ void k_lincomb(LinComb L, uint64_t* out, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  U256 acc = i == 0 ? L.c0 : u256_zero();
+  for (int k = 0; k < L.k; ++k)
+    if (i < L.len[k]) acc = Fr::add(acc, Fr::mul(L.c[k], ldr(L.in[k] + 4 * i)));
+  str(out + 4 * i, acc);
+}
+
+__global__ void k_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t count) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) str(out + 4 * i, Fr::mul(ldr(a + 4 * i), ldr(b + 4 * i)));
+}
+
+// t(x_i) for x_i = g w_N^i on the coset (N = 4n): the numerator of plonk.rs:358-368
+// divided by Z_H(x_i) = g^n w_4^(i mod 4) - 1 (inverses zh_inv[0..3] from the host)
+struct QuotArgs {
+  const uint64_t *a, *b, *c, *z, *ql, *qr, *qo, *qm, *qc, *s1, *s2, *s3, *l1;
+  uint64_t N;
+  U256 alpha, beta, gamma, k1, k2, alpha2, g, wN;
+  U256 zh_inv[4];
+};
+__global__ void k_quotient(QuotArgs q, uint64_t* out) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * PV_CHUNK;
+  if (i0 >= q.N) return;
+  U256 x = Fr::mul(q.g, fr_pow(q.wN, i0));
+  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < q.N; ++i, x = Fr::mul(x, q.wN)) {
+    const uint64_t o = 4 * i;
+    const U256 a = ldr(q.a + o), b = ldr(q.b + o), c = ldr(q.c + o), z = ldr(q.z + o);
+    const U256 zw = ldr(q.z + 4 * ((i + 4) % q.N));  // z(w x_i): w = w_N^4
+    // t1: a b q_m + a q_l + b q_r + c q_o + q_c
+    U256 t1 = Fr::mul(Fr::mul(a, b), ldr(q.qm + o));
+    t1 = Fr::add(t1, Fr::mul(a, ldr(q.ql + o)));
+    t1 = Fr::add(t1, Fr::mul(b, ldr(q.qr + o)));
+    t1 = Fr::add(t1, Fr::mul(c, ldr(q.qo + o)));
+    t1 = Fr::add(t1, ldr(q.qc + o));
+    // t2: alpha (a + beta x + gamma)(b + beta k1 x + gamma)(c + beta k2 x + gamma) z
+    const U256 bx = Fr::mul(q.beta, x);
+    U256 t2 = Fr::mul(q.alpha, Fr::add(Fr::add(a, bx), q.gamma));
+    t2 = Fr::mul(t2, Fr::add(Fr::add(b, Fr::mul(bx, q.k1)), q.gamma));
+    t2 = Fr::mul(t2, Fr::add(Fr::add(c, Fr::mul(bx, q.k2)), q.gamma));
+    t2 = Fr::mul(t2, z);
+    // t3: alpha (a + beta s1 + gamma)(b + beta s2 + gamma)(c + beta s3 + gamma) z(w x)
+    U256 t3 = Fr::mul(q.alpha, Fr::add(Fr::add(a, Fr::mul(q.beta, ldr(q.s1 + o))), q.gamma));
+    t3 = Fr::mul(t3, Fr::add(Fr::add(b, Fr::mul(q.beta, ldr(q.s2 + o))), q.gamma));
+    t3 = Fr::mul(t3, Fr::add(Fr::add(c, Fr::mul(q.beta, ldr(q.s3 + o))), q.gamma));
+    t3 = Fr::mul(t3, zw);
+    // t4: alpha^2 (z - 1) L1
+    const U256 t4 = Fr::mul(Fr::mul(q.alpha2, Fr::sub(z, fr_one_m())), ldr(q.l1 + o));
+    const U256 num = Fr::add(Fr::sub(Fr::add(t1, t2), t3), t4);
+    str(out + o, Fr::mul(num, q.zh_inv[i & 3]));
+  }
+}
+
+// out[i] = (P(x_i) - y) / (x_i - z) on the coset, inv_xz[i] = 1/(x_i - z) precomputed
+__global__ void k_coset_minus(uint64_t* out, uint64_t N, U256 g, U256 wN, U256 zpt) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * PV_CHUNK;
+  if (i0 >= N) return;
+  U256 x = Fr::mul(g, fr_pow(wN, i0));
+  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < N; ++i, x = Fr::mul(x, wN)) str(out + 4 * i, Fr::sub(x, zpt));
+}
+__global__ void k_sub_mul(const uint64_t* p, U256 y, const uint64_t* inv, uint64_t* out, uint64_t N) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) str(out + 4 * i, Fr::mul(Fr::sub(ldr(p + 4 * i), y), ldr(inv + 4 * i)));
+}
+
+// any nonzero element in [from, to) sets *bad
+__global__ void k_nonzero(const uint64_t* a, uint64_t from, uint64_t to, int* bad) {
+  const uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < to && (a[4 * i] | a[4 * i + 1] | a[4 * i + 2] | a[4 * i + 3])) *bad = 1;
+}
+
+// batched Horner: partial[p][chunk] = x^(chunk start) * sum of the chunk's terms
+constexpr int EV_T = 256, EV_PER = 64;
+struct EvalArgs {
+  const uint64_t* poly[12];
+  uint64_t len[12];
+  U256 x[12];
+  uint64_t chunks;  // per polynomial
+};
+__global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* partial) {
+  __shared__ U256 sh[EV_T];
+  const uint64_t p = blockIdx.x / e.chunks, ch = blockIdx.x % e.chunks;
+  const int t = threadIdx.x;
+  const uint64_t start = (ch * EV_T + t) * EV_PER;
+  const U256 x = e.x[p];
+  U256 acc = u256_zero();
+  if (start < e.len[p]) {
+    uint64_t end = start + EV_PER;
+    if (end > e.len[p]) end = e.len[p];
+    for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul(acc, x), ldr(e.poly[p] + 4 * j));
+    acc = Fr::mul(acc, fr_pow(x, start));
+  }
+  sh[t] = acc;
+  __syncthreads();
+  for (int s = EV_T / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] = Fr::add(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  if (t == 0) str(partial + 4 * blockIdx.x, sh[0]);
+}
+__global__ void k_eval_final(const uint64_t* partial, uint64_t chunks, uint64_t np, uint64_t* out) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  U256 acc = u256_zero();
+  for (uint64_t i = 0; i < chunks; ++i) acc = Fr::add(acc, ldr(partial + 4 * (p * chunks + i)));
+  str(out + 4 * p, acc);
+}
+
+// ---------------------------------------------------------------- host helpers
+static U256 hm(const uint64_t* p) { return Fr::to_mont(u256_from_u64(p)); }
+static U256 hm64(uint64_t v) {
+  U256 r = u256_zero();
+  r.w[0] = (uint32_t)v;
+  r.w[1] = (uint32_t)(v >> 32);
+  return Fr::to_mont(r);
+}
+static U256 hpowm(U256 a, const U256& e_plain) {  // exponent given as plain U256
+  U256 r = fr_one_m();
+  for (int i = 255; i >= 0; --i) {
+    r = Fr::mul(r, r);
+    if ((e_plain.w[i / 32] >> (i % 32)) & 1) r = Fr::mul(r, a);
+  }
+  return r;
+}
+static U256 hpow64(U256 a, uint64_t e) {
+  U256 r = fr_one_m();
+  while (e) {
+    if (e & 1) r = Fr::mul(r, a);
+    a = Fr::mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+static U256 hinvm(const U256& a) {
+  U256 e;
+  for (int i = 0; i < 8; ++i) e.w[i] = Bn254FrParams::P[i];
+  e.w[0] -= 2;
+  return hpowm(a, e);
+}
+static void hout(uint64_t* p, const U256& m) { u256_to_u64(Fr::from_mont(m), p); }
+static bool heq1(const U256& m) { return Fr::eq(m, fr_one_m()); }
+// primitive 2^k-th root of unity of Fr: 5^((r-1)/2^k)
+static U256 hroot(uint32_t log_n) {
+  U256 e;  // (r-1) >> log_n
+  for (int i = 0; i < 8; ++i) e.w[i] = Bn254FrParams::P[i];
+  e.w[0] -= 1;
+  for (uint32_t s = 0; s < log_n; ++s) {
+    for (int i = 0; i < 8; ++i) e.w[i] = (e.w[i] >> 1) | (i < 7 ? (e.w[i + 1] << 31) : 0);
+  }
+  return hpowm(hm64(5), e);
+}
+
+struct ProverBufs {
+  DevBuf &hpow, &sigma, &coef, &acc, &tmp0, &tmp1, &tmp2, &coset, &t, &work, &flag, &evals, &partial;
+  explicit ProverBufs(pbf_ctx* c)
+      : hpow(c->buf("pv.hpow")), sigma(c->buf("pv.sigma")), coef(c->buf("pv.coef")), acc(c->buf("pv.acc")),
+        tmp0(c->buf("pv.tmp0")), tmp1(c->buf("pv.tmp1")), tmp2(c->buf("pv.tmp2")), coset(c->buf("pv.coset")),
+        t(c->buf("pv.t")), work(c->buf("pv.work")), flag(c->buf("pv.flag")), evals(c->buf("pv.evals")),
+        partial(c->buf("pv.partial")) {}
+};
+
+}  // namespace pbf
+
+using namespace pbf;
+
+namespace {
+
+struct Prover {
+  pbf_ctx* ctx;
+  hipStream_t s;
+  uint64_t n, N;
+  uint32_t log_n;
+  U256 omega, omegaN, omegaN_inv, g, g_inv;
+  uint64_t w_plain[4], wN_plain[4];
+  int* d_bad;
+
+  int check_bad(const char* what) {
+    int bad = 0;
+    PBF_HIP(hipMemcpyAsync(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    if (bad) return fail(PBF_EINVAL, what);
+    return 0;
+  }
+  int ntt(const uint64_t* w, uint64_t* in, uint64_t* out, uint64_t size, uint64_t batch, int inverse) {
+    return pbf_ntt_fr256_batch_dev(ctx, w, in, out, size, batch, inverse, s);
+  }
+  // coset NTT of `len` coefficients into N evaluations at g w_N^i
+  int coset_ntt(const uint64_t* coeff, uint64_t len, uint64_t* out) {
+    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, coeff, len, out, N,
+                       g, (uint64_t)0);
+    PBF_HIP(hipGetLastError());
+    return ntt(wN_plain, out, out, N, 1, 0);
+  }
+  // coefficients of the degree < N polynomial with evaluations `ev` on the coset
+  int coset_intt(uint64_t* ev, uint64_t* out) {
+    int rc = ntt(wN_plain, ev, ev, N, 1, 1);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, ev, N, out, N,
+                       g_inv, (uint64_t)0);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  int commit(const uint64_t* d_srs, const uint64_t* coeff, uint64_t len, uint64_t* out) {
+    return pbf_msm_g1_bn254_dev(ctx, d_srs, coeff, len, out, s);
+  }
+};
+
+}  // namespace
+
+extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                                         const uint64_t* d_abc, const uint64_t* chal, const uint64_t* rnd,
+                                         const uint64_t* k1k2, const uint64_t* d_srs, size_t srs_m, int mode,
+                                         uint64_t* out_pts, uint64_t* out_f, void* stream) {
+  if (!ctx || !d_q || !d_copies || !d_abc || !chal || !rnd || !k1k2 || !d_srs || !out_pts || !out_f)
+    return fail(PBF_EINVAL, "null argument");
+  if (n < 8 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two >= 8");
+  if (mode != 0 && mode != 1) return fail(PBF_EINVAL, "mode must be 0 (reference r_3) or 1 (paper)");
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < n) ++log_n;
+  if (log_n + 2 > 28) return fail(PBF_EINVAL, "4n exceeds the 2-adicity of Fr");
+  const uint64_t need_srs = mode == 0 ? 2 * n + 2 : n + 3;  // longest committed polynomial
+  if (srs_m < need_srs) return fail(PBF_EINVAL, "SRS too short for this n and mode");
+  for (int i = 0; i < 5; ++i)
+    if (Fr::geq_p(u256_from_u64(chal + 4 * i))) return fail(PBF_EINVAL, "challenge not canonical");
+  for (int i = 0; i < 9; ++i)
+    if (Fr::geq_p(u256_from_u64(rnd + 4 * i))) return fail(PBF_EINVAL, "blinder not canonical");
+
+  Prover P;
+  P.ctx = ctx;
+  P.s = (hipStream_t)stream;
+  P.n = n;
+  P.N = 4 * n;
+  P.log_n = log_n;
+  P.omega = hroot(log_n);
+  P.omegaN = hroot(log_n + 2);
+  P.g = hm64(5);  // coset shift: a quadratic non-residue, outside every 2^k subgroup
+  P.g_inv = hinvm(P.g);
+  hout(P.w_plain, P.omega);
+  hout(P.wN_plain, P.omegaN);
+  const hipStream_t s = P.s;
+  const uint64_t N = P.N;
+  const U256 one = fr_one_m();
+  const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
+  // Plonk::new asserts (plonk.rs:133-138): k1, k2 not in H, k2 not in k1 H
+  if (heq1(hpow64(k1, n)) || heq1(hpow64(k2, n)) || heq1(hpow64(Fr::mul(k2, hinvm(k1)), n)) || Fr::is_zero(k1) ||
+      Fr::is_zero(k2))
+    return fail(PBF_EINVAL, "k1/k2 do not give disjoint cosets of H");
+  const U256 alpha = hm(chal), beta = hm(chal + 4), gamma = hm(chal + 8), zc = hm(chal + 12), v = hm(chal + 16);
+  U256 bl[9];
+  for (int i = 0; i < 9; ++i) bl[i] = hm(rnd + 4 * i);
+
+  ProverBufs B(ctx);  // context-owned scratch (one ctx per host thread, pbf.h)
+  const uint64_t E = 32;           // bytes per element
+  int rc;
+  if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure(3 * n * E)) || (rc = B.coef.ensure(11 * (n + 8) * E)) ||
+      (rc = B.acc.ensure((n + 8) * E)) || (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure(n * E)) ||
+      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure(13 * N * E)) ||
+      (rc = B.t.ensure(N * E)) || (rc = B.work.ensure(3 * N * E)) || (rc = B.flag.ensure(64)) ||
+      (rc = B.evals.ensure(16 * E)))
+    return rc;
+  P.d_bad = (int*)B.flag.p;
+  PBF_HIP(hipMemsetAsync(P.d_bad, 0, sizeof(int), s));
+  uint64_t* hpow = (uint64_t*)B.hpow.p;
+  uint64_t* sigma = (uint64_t*)B.sigma.p;
+  const uint64_t CS = n + 8;  // coefficient slot (room for blinding terms up to x^(n+2))
+  uint64_t* coef = (uint64_t*)B.coef.p;
+  auto C = [&](int k) { return coef + 4 * CS * k; };
+  // slots: 0 a, 1 b, 2 c, 3 q_l, 4 q_r, 5 q_o, 6 q_m, 7 q_c, 8 s1, 9 s2, 10 s3
+  uint64_t* coset = (uint64_t*)B.coset.p;
+  auto CE = [&](int k) { return coset + 4 * N * k; };
+  // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1
+  uint64_t* work = (uint64_t*)B.work.p;
+  uint64_t* W0 = work;
+  uint64_t* W1 = work + 4 * N;
+  uint64_t* W2 = work + 8 * N;
+
+  // ---- satisfies (constraints.rs:198-230)
+  hipLaunchKernelGGL(k_satisfies, dim3(blocks_for(n)), dim3(256), 0, s, d_q, d_abc, d_copies, (uint64_t)n, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
+
+  // ---- h = w^i, sigma labels (plonk.rs:124, 181-189, 222-224)
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
+                     P.omega, one);
+  hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, (uint64_t)n,
+                     k1, k2, sigma, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
+  PBF_HIP(hipMemsetAsync(coef, 0, 11 * CS * E, s));
+  for (int k = 0; k < 3; ++k)
+    PBF_HIP(hipMemcpyAsync(C(k), d_abc + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+  for (int k = 0; k < 5; ++k)
+    PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+  for (int k = 0; k < 3; ++k)
+    PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+  for (int k = 0; k < 11; ++k)
+    if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
+  // ---- round 1: a(x) = (b2 + b1 x)(x^n - 1) + f_a(x), likewise b, c (plonk.rs:250-252)
+  for (int k = 0; k < 3; ++k) {
+    const U256 lo = bl[2 * k + 1], hi = bl[2 * k];  // (b2, b1), (b4, b3), (b6, b5)
+    Blind b;
+    b.count = 4;
+    b.idx[0] = 0; b.delta[0] = Fr::sub(u256_zero(), lo);
+    b.idx[1] = 1; b.delta[1] = Fr::sub(u256_zero(), hi);
+    b.idx[2] = n; b.delta[2] = lo;
+    b.idx[3] = n + 1; b.delta[3] = hi;
+    hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, C(k), b);
+  }
+  PBF_HIP(hipGetLastError());
+  uint64_t pts[9][8];
+  for (int k = 0; k < 3; ++k)
+    if ((rc = P.commit(d_srs, C(k), n + 2, pts[k]))) return rc;
+
+  // ---- round 2: accumulator (plonk.rs:278-313)
+  uint64_t* acc = (uint64_t*)B.acc.p;
+  uint64_t* num = (uint64_t*)B.tmp0.p;
+  uint64_t* den = (uint64_t*)B.tmp1.p;
+  PBF_HIP(hipMemsetAsync(acc, 0, CS * E, s));
+  hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(n)), dim3(256), 0, s, d_abc, (const uint64_t*)sigma,
+                     (const uint64_t*)hpow, (uint64_t)n, beta, gamma, k1, k2, num, den);
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((n - 1 + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)num, (const uint64_t*)den, num, (uint64_t)(n - 1), P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("zero permutation denominator (plonk.rs:297 unwrap)"))) return rc;
+  {
+    const uint64_t nb = (n - 1 + SCAN_BLK - 1) / SCAN_BLK;
+    uint64_t* totals = (uint64_t*)B.tmp2.p;
+    hipLaunchKernelGGL(k_scan1, dim3((uint32_t)nb), dim3(SCAN_T), 0, s, (const uint64_t*)num, den, (uint64_t)(n - 1),
+                       totals);
+    hipLaunchKernelGGL(k_scan2, dim3(1), dim3(SCAN_T), 0, s, totals, nb);
+    hipLaunchKernelGGL(k_scan3, dim3(blocks_for(n)), dim3(256), 0, s, (const uint64_t*)den, acc, (uint64_t)n,
+                       (const uint64_t*)totals);
+    PBF_HIP(hipGetLastError());
+  }
+  if ((rc = P.ntt(P.w_plain, acc, acc, n, 1, 1))) return rc;  // acc_x
+  {
+    Blind b;  // z(x) = (b9 + b8 x + b7 x^2)(x^n - 1) + acc(x)   (plonk.rs:309)
+    b.count = 6;
+    const U256 c0 = bl[8], c1 = bl[7], c2 = bl[6];
+    b.idx[0] = 0; b.delta[0] = Fr::sub(u256_zero(), c0);
+    b.idx[1] = 1; b.delta[1] = Fr::sub(u256_zero(), c1);
+    b.idx[2] = 2; b.delta[2] = Fr::sub(u256_zero(), c2);
+    b.idx[3] = n; b.delta[3] = c0;
+    b.idx[4] = n + 1; b.delta[4] = c1;
+    b.idx[5] = n + 2; b.delta[5] = c2;
+    hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, acc, b);
+    PBF_HIP(hipGetLastError());
+  }
+  uint64_t* zx = acc;  // length n+3
+  if ((rc = P.commit(d_srs, zx, n + 3, pts[3]))) return rc;
+
+  // ---- round 3: quotient on the coset g H_4n (plonk.rs:326-382)
+  const int cmap[13] = {0, 1, 2, -1, 3, 4, 5, 6, 7, 8, 9, 10, -2};  // coef slot per coset slot
+  // l_1(x) = interpolate([1, 0, ..., 0]) = n^-1 (1 + x + ... + x^(n-1)) (plonk.rs:328-332)
+  const U256 ninv = hinvm(hm64(n));
+  {
+    uint64_t* l1 = (uint64_t*)B.tmp0.p;
+    hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, (uint64_t)n,
+                       one, ninv);
+    PBF_HIP(hipGetLastError());
+  }
+  for (int k = 0; k < 13; ++k) {
+    const uint64_t* src;
+    uint64_t len;
+    if (cmap[k] == -1) { src = zx; len = n + 3; }
+    else if (cmap[k] == -2) { src = (const uint64_t*)B.tmp0.p; len = n; }
+    else { src = C(cmap[k]); len = cmap[k] < 3 ? n + 2 : n; }
+    if ((rc = P.coset_ntt(src, len, CE(k)))) return rc;
+  }
+  QuotArgs qa;
+  qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
+  qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);
+  qa.N = N;
+  qa.alpha = alpha; qa.beta = beta; qa.gamma = gamma; qa.k1 = k1; qa.k2 = k2;
+  qa.alpha2 = Fr::mul(alpha, alpha);
+  qa.g = P.g; qa.wN = P.omegaN;
+  {
+    // Z_H(g w_N^i) = g^n w_4^(i mod 4) - 1
+    const U256 gn = hpow64(P.g, n), w4 = hpow64(P.omegaN, n);
+    U256 x = gn;
+    for (int j = 0; j < 4; ++j) {
+      const U256 d = Fr::sub(x, one);
+      if (Fr::is_zero(d)) return fail(PBF_EINVAL, "coset meets H");
+      qa.zh_inv[j] = hinvm(d);
+      x = Fr::mul(x, w4);
+    }
+  }
+  uint64_t* tq = (uint64_t*)B.t.p;
+  hipLaunchKernelGGL(k_quotient, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, qa, W0);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.coset_intt(W0, tq))) return rc;
+  const uint64_t m = n + 2;  // coefficients per t part
+  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - 3 * m)), dim3(256), 0, s, (const uint64_t*)tq, 3 * m, N, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)")))
+    return rc;
+  if ((rc = P.commit(d_srs, tq, m, pts[4]))) return rc;            // t_lo
+  if ((rc = P.commit(d_srs, tq + 4 * m, m, pts[5]))) return rc;    // t_mid
+  if ((rc = P.commit(d_srs, tq + 8 * m, m, pts[6]))) return rc;    // t_hi
+
+  // ---- round 4: evaluations at z (plonk.rs:393-399), linearisation r(x) (:401-422)
+  const U256 zw = Fr::mul(zc, P.omega);
+  auto eval = [&](int np, const uint64_t* const* polys, const uint64_t* lens, const U256* xs, U256* res) -> int {
+    EvalArgs e;
+    uint64_t maxlen = 0;
+    for (int i = 0; i < np; ++i) {
+      e.poly[i] = polys[i]; e.len[i] = lens[i]; e.x[i] = xs[i];
+      if (lens[i] > maxlen) maxlen = lens[i];
+    }
+    e.chunks = (maxlen + EV_T * EV_PER - 1) / (EV_T * EV_PER);
+    int rc2 = B.partial.ensure(np * e.chunks * 32);
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(k_eval_partial, dim3((uint32_t)(np * e.chunks)), dim3(EV_T), 0, s, e, (uint64_t*)B.partial.p);
+    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, s, (const uint64_t*)B.partial.p, e.chunks, (uint64_t)np,
+                       (uint64_t*)B.evals.p);
+    PBF_HIP(hipGetLastError());
+    std::vector<uint64_t> h(4 * np);
+    PBF_HIP(hipMemcpyAsync(h.data(), B.evals.p, 4 * np * 8, hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < np; ++i) res[i] = hm(h.data() + 4 * i);
+    return 0;
+  };
+  U256 ev[8];
+  {
+    const uint64_t* polys[8] = {C(0), C(1), C(2), C(8), C(9), tq, zx, (const uint64_t*)B.tmp0.p};
+    const uint64_t lens[8] = {n + 2, n + 2, n + 2, n, n, 3 * m, n + 3, n};
+    const U256 xs[8] = {zc, zc, zc, zc, zc, zc, zw, zc};
+    if ((rc = eval(8, polys, lens, xs, ev))) return rc;
+  }
+  const U256 a_z = ev[0], b_z = ev[1], c_z = ev[2], s1_z = ev[3], s2_z = ev[4], t_z = ev[5], zw_z = ev[6];
+  const U256 l1_z = ev[7];
+  (void)t_z;
+  // r(x) = q_m a_z b_z + q_l a_z + q_r b_z + q_o c_z + q_c + K2 z(x) + r_3(x) + L1(z) alpha^2 z(x)
+  const U256 K2 = Fr::mul(Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, zc)), gamma),
+                                          Fr::add(Fr::add(b_z, Fr::mul(Fr::mul(beta, k1), zc)), gamma)),
+                                  Fr::add(Fr::add(c_z, Fr::mul(Fr::mul(beta, k2), zc)), gamma)),
+                          alpha);
+  const U256 K3 = Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, s1_z)), gamma),
+                                  Fr::add(Fr::add(b_z, Fr::mul(beta, s2_z)), gamma)),
+                          alpha);
+  const U256 K4 = Fr::mul(l1_z, qa.alpha2);
+  const uint64_t rlen = mode == 0 ? 2 * n + 2 : n + 3;
+  uint64_t* rx = W1;  // r(x) coefficients (length rlen, N slot)
+  {
+    LinComb L;
+    L.k = 7;
+    L.in[0] = C(6); L.len[0] = n; L.c[0] = Fr::mul(a_z, b_z);
+    L.in[1] = C(3); L.len[1] = n; L.c[1] = a_z;
+    L.in[2] = C(4); L.len[2] = n; L.c[2] = b_z;
+    L.in[3] = C(5); L.len[3] = n; L.c[3] = c_z;
+    L.in[4] = C(7); L.len[4] = n; L.c[4] = one;
+    L.in[5] = zx; L.len[5] = n + 3; L.c[5] = Fr::add(K2, K4);
+    if (mode == 1) {  // paper: - beta z_w(z) K3 s_sigma_3(x)
+      L.in[6] = C(10); L.len[6] = n; L.c[6] = Fr::sub(u256_zero(), Fr::mul(Fr::mul(beta, zw_z), K3));
+    } else {
+      L.k = 6;
+    }
+    L.c0 = u256_zero();
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L, rx, N);
+    PBF_HIP(hipGetLastError());
+    if (mode == 0) {
+      // r_3(x) = z(x) s_sigma_3(x) (beta z_w(z)) K3 (plonk.rs:414-416): the product on the coset
+      hipLaunchKernelGGL(k_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)CE(3), (const uint64_t*)CE(11),
+                         W2, N);
+      PBF_HIP(hipGetLastError());
+      if ((rc = P.coset_intt(W2, W0))) return rc;
+      LinComb L2;
+      L2.k = 2;
+      L2.in[0] = rx; L2.len[0] = N; L2.c[0] = one;
+      L2.in[1] = W0; L2.len[1] = N; L2.c[1] = Fr::mul(Fr::mul(beta, zw_z), K3);
+      L2.c0 = u256_zero();
+      hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L2, W2, N);
+      PBF_HIP(hipGetLastError());
+      PBF_HIP(hipMemcpyAsync(rx, W2, N * E, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  U256 r_z;
+  {
+    const uint64_t* polys[1] = {rx};
+    const uint64_t lens[1] = {rlen};
+    const U256 xs[1] = {zc};
+    if ((rc = eval(1, polys, lens, xs, &r_z))) return rc;
+  }
+
+  // ---- round 5: W_z = [t_lo + z^(n+2) t_mid + z^(2n+4) t_hi - t_z + v (r - r_z) + v^2 (a - a_z)
+  //      + v^3 (b - b_z) + v^4 (c - c_z) + v^5 (s1 - s1_z) + v^6 (s2 - s2_z)] / (x - z)   (:430-439)
+  U256 vp[7];
+  vp[0] = one;
+  for (int i = 1; i < 7; ++i) vp[i] = Fr::mul(vp[i - 1], v);
+  {
+    LinComb L;  // numerator coefficients into W2 (constant term folded: vanishes at z)
+    L.k = 10;
+    const U256 zn2 = hpow64(zc, n + 2), z2n4 = hpow64(zc, 2 * n + 4);
+    L.in[0] = tq; L.len[0] = m; L.c[0] = one;
+    L.in[1] = tq + 4 * m; L.len[1] = m; L.c[1] = zn2;
+    L.in[2] = tq + 8 * m; L.len[2] = m; L.c[2] = z2n4;
+    L.in[3] = rx; L.len[3] = rlen; L.c[3] = vp[1];
+    L.in[4] = C(0); L.len[4] = n + 2; L.c[4] = vp[2];
+    L.in[5] = C(1); L.len[5] = n + 2; L.c[5] = vp[3];
+    L.in[6] = C(2); L.len[6] = n + 2; L.c[6] = vp[4];
+    L.in[7] = C(8); L.len[7] = n; L.c[7] = vp[5];
+    L.in[8] = C(9); L.len[8] = n; L.c[8] = vp[6];
+    L.k = 9;
+    U256 cst = Fr::add(t_z, Fr::mul(vp[1], r_z));
+    cst = Fr::add(cst, Fr::mul(vp[2], a_z));
+    cst = Fr::add(cst, Fr::mul(vp[3], b_z));
+    cst = Fr::add(cst, Fr::mul(vp[4], c_z));
+    cst = Fr::add(cst, Fr::mul(vp[5], s1_z));
+    cst = Fr::add(cst, Fr::mul(vp[6], s2_z));
+    L.c0 = Fr::sub(u256_zero(), cst);
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L, W2, N);
+    PBF_HIP(hipGetLastError());
+  }
+  // division by (x - z) on the coset: W(x_i) = P(x_i) / (x_i - z)
+  uint64_t* inv = W0;
+  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, N, P.g, P.omegaN,
+                     zc);
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((N + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, N, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("z lies on the evaluation coset"))) return rc;
+  if ((rc = P.coset_ntt(W2, N, W1))) return rc;  // numerator evaluations (rx no longer needed)
+  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)W1, u256_zero(),
+                     (const uint64_t*)inv, W2, N);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.coset_intt(W2, W1))) return rc;  // W_z coefficients
+  const uint64_t wlen = rlen - 1 > m ? rlen - 1 : m;
+  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - wlen)), dim3(256), 0, s, (const uint64_t*)W1, wlen, N, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("W_z division left a remainder (plonk.rs:438)"))) return rc;
+  if ((rc = P.commit(d_srs, W1, wlen, pts[7]))) return rc;
+  // W_zw = (z(x) - z_w(z)) / (x - z w)   (plonk.rs:441-442), z's coset evaluations reused
+  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, N, P.g, P.omegaN,
+                     zw);
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((N + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, N, P.d_bad);
+  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)CE(3), zw_z,
+                     (const uint64_t*)inv, W2, N);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("z w lies on the evaluation coset"))) return rc;
+  if ((rc = P.coset_intt(W2, W1))) return rc;
+  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - (n + 2))), dim3(256), 0, s, (const uint64_t*)W1, n + 2, N, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.check_bad("W_zw division left a remainder (plonk.rs:442)"))) return rc;
+  if ((rc = P.commit(d_srs, W1, n + 2, pts[8]))) return rc;
+
+  for (int i = 0; i < 9; ++i) memcpy(out_pts + 8 * i, pts[i], 64);
+  const U256 fo[7] = {a_z, b_z, c_z, s1_z, s2_z, r_z, zw_z};
+  for (int i = 0; i < 7; ++i) hout(out_f + 4 * i, fo[i]);
+  return 0;
+}
+
+// host-pointer wrapper: uploads q / copies / abc / SRS, proves, returns (pts, fields)
+extern "C" int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies,
+                                     const uint64_t* abc, const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2,
+                                     const uint64_t* srs, size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f) {
+  if (!ctx || !q || !copies || !abc || !srs) return fail(PBF_EINVAL, "null argument");
+  hipStream_t s = ctx->host_stream();
+  DevBuf &dq = ctx->buf("pv.q"), &dc = ctx->buf("pv.copies"), &dabc = ctx->buf("pv.abc"), &dsrs = ctx->buf("pv.srs");
+  int rc;
+  if ((rc = dq.ensure(5 * n * 32)) || (rc = dc.ensure(3 * n * 16)) || (rc = dabc.ensure(3 * n * 32)) ||
+      (rc = dsrs.ensure(srs_m * 64)))
+    return rc;
+  PBF_HIP(hipMemcpyAsync(dq.p, q, 5 * n * 32, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(dc.p, copies, 3 * n * 16, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(dabc.p, abc, 3 * n * 32, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(dsrs.p, srs, srs_m * 64, hipMemcpyHostToDevice, s));
+  rc = pbf_plonk_prove_bn254_dev(ctx, n, (const uint64_t*)dq.p, (const uint64_t*)dc.p, (const uint64_t*)dabc.p, chal,
+                                 rnd, k1k2, (const uint64_t*)dsrs.p, srs_m, mode, out_pts, out_f, s);
+  if (rc) return rc;
+  PBF_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// ---------------------------------------------------------------- Plonk::verify
+namespace {
+
+// y^2 == x^3 + 3 over Fq for an affine canonical point (identity (0,0) accepted: G1P::in_curve)
+bool h_on_curve(const uint64_t* p) {
+  bool zero = true;
+  for (int i = 0; i < 8; ++i) zero = zero && p[i] == 0;
+  if (zero) return true;
+  const U256 x = u256_from_u64(p), y = u256_from_u64(p + 4);
+  if (Fq::geq_p(x) || Fq::geq_p(y)) return false;
+  const U256 xm = Fq::to_mont(x), ym = Fq::to_mont(y);
+  U256 three = u256_zero();
+  three.w[0] = 3;
+  const U256 rhs = Fq::add(Fq::mul(Fq::mul(xm, xm), xm), Fq::to_mont(three));
+  return Fq::eq(Fq::mul(ym, ym), rhs);
+}
+
+void h_neg_g1(const uint64_t* p, uint64_t* out) {
+  for (int i = 0; i < 8; ++i) out[i] = p[i];
+  const U256 y = u256_from_u64(p + 4);
+  if (Fq::is_zero(y)) return;
+  U256 q;
+  for (int i = 0; i < 8; ++i) q.w[i] = Bn254FqParams::P[i];
+  // q - y (y < q)
+  uint64_t borrow = 0;
+  U256 d;
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t t = (uint64_t)q.w[i] - y.w[i] - borrow;
+    d.w[i] = (uint32_t)t;
+    borrow = (t >> 63) & 1;
+  }
+  u256_to_u64(d, out + 4);
+}
+
+}  // namespace
+
+// Plonk::verify (src/plonk.rs:468-650). srs: >= n affine G1 points (g1s, device), g2: [g2_1, g2_s]
+// (2 x 16 u64, host); proof as pbf_plonk_prove_bn254 returns it; u the verifier's random
+// scalar (rand[0], plonk.rs:519). mode 0 keeps step 7's t_z (plonk.rs:575-581, no alpha on
+// the permutation term), mode 1 the paper's. *ok = 1 iff e(E1, [s]G2) == e(E2, G2).
+extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                                          const uint64_t* d_srs, size_t srs_m, const uint64_t* g2,
+                                          const uint64_t* proof_pts, const uint64_t* proof_f, const uint64_t* chal,
+                                          const uint64_t* u_in, const uint64_t* k1k2, int mode, int* ok, void* stream) {
+  if (!ctx || !d_q || !d_copies || !d_srs || !g2 || !proof_pts || !proof_f || !chal || !u_in || !k1k2 || !ok)
+    return fail(PBF_EINVAL, "null argument");
+  *ok = 0;
+  if (n < 8 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two >= 8");
+  if (srs_m < n) return fail(PBF_EINVAL, "SRS too short");
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < n) ++log_n;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t E = 32;
+  int rc;
+  // Step 1-2: proof points on the curve, proof fields canonical (plonk.rs:523-547)
+  for (int i = 0; i < 9; ++i)
+    if (!h_on_curve(proof_pts + 8 * i)) return 0;
+  for (int i = 0; i < 7; ++i)
+    if (Fr::geq_p(u256_from_u64(proof_f + 4 * i))) return 0;
+  // preprocessing (plonk.rs:507-517): commitments of q_m q_l q_r q_o q_c, s_sigma_1..3
+  DevBuf &hp = ctx->buf("vf.hpow"), &sg = ctx->buf("vf.sigma"), &cf = ctx->buf("vf.coef"), &fl = ctx->buf("vf.flag");
+  if ((rc = hp.ensure(n * E)) || (rc = sg.ensure(3 * n * E)) || (rc = cf.ensure(8 * n * E)) || (rc = fl.ensure(64)))
+    return rc;
+  const U256 omega = hroot(log_n), one = fr_one_m();
+  uint64_t w_plain[4];
+  hout(w_plain, omega);
+  const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
+  PBF_HIP(hipMemsetAsync(fl.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
+                     (uint64_t)n, omega, one);
+  hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hp.p, (uint64_t)n,
+                     k1, k2, (uint64_t*)sg.p, (int*)fl.p);
+  PBF_HIP(hipGetLastError());
+  uint64_t* c = (uint64_t*)cf.p;
+  // slots: 0 q_m 1 q_l 2 q_r 3 q_o 4 q_c 5 s1 6 s2 7 s3  (q columns: q_l q_r q_o q_m q_c)
+  const int qcol[5] = {3, 0, 1, 2, 4};
+  for (int k = 0; k < 5; ++k)
+    PBF_HIP(hipMemcpyAsync(c + 4 * n * k, d_q + 4 * n * qcol[k], n * E, hipMemcpyDeviceToDevice, s));
+  PBF_HIP(hipMemcpyAsync(c + 4 * n * 5, sg.p, 3 * n * E, hipMemcpyDeviceToDevice, s));
+  if ((rc = pbf_ntt_fr256_batch_dev(ctx, w_plain, c, c, n, 8, 1, s))) return rc;
+  uint64_t pre[8][8];
+  for (int k = 0; k < 8; ++k)
+    if ((rc = pbf_msm_g1_bn254_dev(ctx, d_srs, c + 4 * n * k, n, pre[k], s))) return rc;
+  int bad = 0;
+  PBF_HIP(hipMemcpyAsync(&bad, fl.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  if (bad) return fail(PBF_EINVAL, "bad copy constraint label");
+
+  const U256 alpha = hm(chal), beta = hm(chal + 4), gamma = hm(chal + 8), zc = hm(chal + 12), v = hm(chal + 16);
+  const U256 u = hm(u_in);
+  const U256 a_z = hm(proof_f), b_z = hm(proof_f + 4), c_z = hm(proof_f + 8), s1_z = hm(proof_f + 12),
+             s2_z = hm(proof_f + 16), r_z = hm(proof_f + 20), zw_z = hm(proof_f + 24);
+  // Step 4-5: Z_H(z) = z^n - 1, L_1(z) = n^-1 sum_{i<n} z^i (the interpolated Lagrange poly)
+  const U256 zn = hpow64(zc, n);
+  const U256 z_h_z = Fr::sub(zn, one);
+  U256 l1 = u256_zero(), zp = one;
+  for (uint64_t i = 0; i < n && i < 64; ++i) { l1 = Fr::add(l1, zp); zp = Fr::mul(zp, zc); }
+  if (n > 64) {  // geometric sum (z^n - 1)/(z - 1) for z != 1
+    const U256 zm1 = Fr::sub(zc, one);
+    l1 = Fr::is_zero(zm1) ? hm64(n) : Fr::mul(z_h_z, hinvm(zm1));
+  }
+  l1 = Fr::mul(l1, hinvm(hm64(n)));
+  if (Fr::is_zero(z_h_z)) return 0;  // the reference's .unwrap() would panic (plonk.rs:581)
+  // Step 7: t_z
+  const U256 alpha2 = Fr::mul(alpha, alpha);
+  U256 perm = Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, s1_z)), gamma),
+                              Fr::add(Fr::add(b_z, Fr::mul(beta, s2_z)), gamma)),
+                      Fr::mul(Fr::add(c_z, gamma), zw_z));
+  if (mode == 1) perm = Fr::mul(perm, alpha);
+  const U256 t_z = Fr::mul(Fr::sub(Fr::sub(r_z, perm), Fr::mul(l1, alpha2)), hinvm(z_h_z));
+  // Steps 8-10 as one linear combination of points (bases / scalars)
+  U256 vp[7];
+  vp[0] = one;
+  for (int i = 1; i < 7; ++i) vp[i] = Fr::mul(vp[i - 1], v);
+  const U256 d2 = Fr::add(Fr::add(Fr::mul(Fr::mul(Fr::mul(Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, zc)), gamma),
+      Fr::add(Fr::add(b_z, Fr::mul(Fr::mul(beta, k1), zc)), gamma)), Fr::add(Fr::add(c_z, Fr::mul(Fr::mul(beta, k2), zc)), gamma)),
+      alpha), v), one), Fr::mul(Fr::mul(l1, alpha2), v)), u);
+  const U256 d3 = Fr::mul(Fr::mul(Fr::mul(Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, s1_z)), gamma),
+      Fr::add(Fr::add(b_z, Fr::mul(beta, s2_z)), gamma)), alpha), v), beta), zw_z);
+  U256 ecoef = Fr::add(t_z, Fr::mul(v, r_z));
+  ecoef = Fr::add(ecoef, Fr::mul(vp[2], a_z));
+  ecoef = Fr::add(ecoef, Fr::mul(vp[3], b_z));
+  ecoef = Fr::add(ecoef, Fr::mul(vp[4], c_z));
+  ecoef = Fr::add(ecoef, Fr::mul(vp[5], s1_z));
+  ecoef = Fr::add(ecoef, Fr::mul(vp[6], s2_z));
+  ecoef = Fr::add(ecoef, Fr::mul(u, zw_z));
+  const U256 omega_m = omega;
+  // bases: proof a b c z t_lo t_mid t_hi w_z w_zw | q_m q_l q_r q_o q_c s1 s2 s3 | G
+  std::vector<uint64_t> bases(18 * 8), sc(18 * 4);
+  for (int i = 0; i < 9; ++i) memcpy(&bases[8 * i], proof_pts + 8 * i, 64);
+  for (int k = 0; k < 8; ++k) memcpy(&bases[8 * (9 + k)], pre[k], 64);
+  std::vector<uint64_t> g0(8);
+  PBF_HIP(hipMemcpyAsync(g0.data(), d_srs, 64, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  memcpy(&bases[8 * 17], g0.data(), 64);
+  U256 scal[18];
+  scal[0] = vp[2];                                       // a_s
+  scal[1] = vp[3];                                       // b_s
+  scal[2] = vp[4];                                       // c_s
+  scal[3] = d2;                                          // z_s
+  scal[4] = one;                                         // t_lo
+  scal[5] = hpow64(zc, n + 2);                           // t_mid
+  scal[6] = hpow64(zc, 2 * n + 4);                       // t_hi
+  scal[7] = zc;                                          // w_z * z
+  scal[8] = Fr::mul(Fr::mul(u, zc), omega_m);            // w_zw * u z w
+  scal[9] = Fr::mul(Fr::mul(a_z, b_z), v);               // q_m
+  scal[10] = Fr::mul(a_z, v);                            // q_l
+  scal[11] = Fr::mul(b_z, v);                            // q_r
+  scal[12] = Fr::mul(c_z, v);                            // q_o
+  scal[13] = v;                                          // q_c
+  scal[14] = vp[5];                                      // s1
+  scal[15] = vp[6];                                      // s2
+  scal[16] = Fr::sub(u256_zero(), d3);                   // - s3 d3
+  scal[17] = Fr::sub(u256_zero(), ecoef);                // - E
+  for (int i = 0; i < 18; ++i) hout(&sc[4 * i], scal[i]);
+  DevBuf &db = ctx->buf("vf.bases"), &ds = ctx->buf("vf.scalars");
+  if ((rc = db.ensure(18 * 64)) || (rc = ds.ensure(18 * 32))) return rc;
+  PBF_HIP(hipMemcpyAsync(db.p, bases.data(), 18 * 64, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(ds.p, sc.data(), 18 * 32, hipMemcpyHostToDevice, s));
+  uint64_t e2[8], e1[8];
+  if ((rc = pbf_msm_g1_bn254_dev(ctx, (const uint64_t*)db.p, (const uint64_t*)ds.p, 18, e2, s))) return rc;
+  // E1 = w_z + u w_zw
+  U256 one_u[2] = {one, u};
+  std::vector<uint64_t> sc1(8);
+  hout(&sc1[0], one_u[0]);
+  hout(&sc1[4], one_u[1]);
+  PBF_HIP(hipMemcpyAsync(db.p, proof_pts + 8 * 7, 2 * 64, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(ds.p, sc1.data(), 2 * 32, hipMemcpyHostToDevice, s));
+  if ((rc = pbf_msm_g1_bn254_dev(ctx, (const uint64_t*)db.p, (const uint64_t*)ds.p, 2, e1, s))) return rc;
+  // e(E1, [s]G2) == e(E2, G2)  <=>  e(E1, [s]G2) e(-E2, G2) == 1  (plonk.rs:646-650)
+  uint64_t g1s[16], g2s[32];
+  memcpy(g1s, e1, 64);
+  h_neg_g1(e2, g1s + 8);
+  memcpy(g2s, g2 + 16, 128);  // [s]G2
+  memcpy(g2s + 16, g2, 128);  // G2
+  return pbf_pairing_check_bn254(ctx, g1s, g2s, 2, ok);
+}
+
+extern "C" int pbf_plonk_verify_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies,
+                                      const uint64_t* srs, size_t srs_m, const uint64_t* g2, const uint64_t* proof_pts,
+                                      const uint64_t* proof_f, const uint64_t* chal, const uint64_t* u,
+                                      const uint64_t* k1k2, int mode, int* ok) {
+  if (!ctx || !q || !copies || !srs) return fail(PBF_EINVAL, "null argument");
+  hipStream_t s = ctx->host_stream();
+  DevBuf &dq = ctx->buf("vf.q"), &dc = ctx->buf("vf.copies"), &dsrs = ctx->buf("vf.srs");
+  int rc;
+  if ((rc = dq.ensure(5 * n * 32)) || (rc = dc.ensure(3 * n * 16)) || (rc = dsrs.ensure(srs_m * 64))) return rc;
+  PBF_HIP(hipMemcpyAsync(dq.p, q, 5 * n * 32, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(dc.p, copies, 3 * n * 16, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(dsrs.p, srs, srs_m * 64, hipMemcpyHostToDevice, s));
+  return pbf_plonk_verify_bn254_dev(ctx, n, (const uint64_t*)dq.p, (const uint64_t*)dc.p, (const uint64_t*)dsrs.p,
+                                    srs_m, g2, proof_pts, proof_f, chal, u, k1k2, mode, ok, s);
+}

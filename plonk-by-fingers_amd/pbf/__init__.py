@@ -59,6 +59,14 @@ SIGNATURES = [
     ("pbf_pairing_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     ("pbf_pairing_check_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, ctypes.POINTER(ctypes.c_int)]),
     ("pbf_g2_bn254_mul", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
+    ("pbf_plonk_prove_bn254", ctypes.c_int, [_vp, _sz, _p64, _p64, _p64, _p64, _p64, _p64, _p64, _sz, ctypes.c_int,
+                                             _p64, _p64]),
+    ("pbf_plonk_prove_bn254_dev", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _p64, _p64, _p64, _vp, _sz, ctypes.c_int,
+                                                 _p64, _p64, _vp]),
+    ("pbf_plonk_verify_bn254", ctypes.c_int, [_vp, _sz, _p64, _p64, _p64, _sz, _p64, _p64, _p64, _p64, _p64, _p64,
+                                              ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    ("pbf_plonk_verify_bn254_dev", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _sz, _p64, _p64, _p64, _p64, _p64, _p64,
+                                                  ctypes.c_int, ctypes.POINTER(ctypes.c_int), _vp]),
     ("pbf_pbh_g1_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_g2_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_gt_pow", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
@@ -229,6 +237,46 @@ class Context:
         _check(self.lib.pbf_srs_create_bn254(self.h, _ptr(ints_to_limbs([s])), n, _ptr(out)))
         v = limbs_to_ints(out)
         return [(v[2 * i], v[2 * i + 1]) for i in range(n + 1)]
+
+    # ---- generalised PLONK over BN254 (config 5; prover.hip)
+    def plonk_prove_bn254(self, q, copies, abc, chal, rnd, srs, k1k2=(2, 3), mode=0):
+        """q: 5 columns (q_l, q_r, q_o, q_m, q_c) of n ints; copies: 3 columns of (kind, 1-based
+        idx); abc: 3 columns; chal: (alpha, beta, gamma, z, v); rnd: b1..b9; srs: affine points.
+        Returns (9 points, 7 field ints) as Proof (plonk.rs:61-95)."""
+        n = len(abc[0])
+        qa = ints_to_limbs([x for col in q for x in col])
+        ca = np.array([v for col in copies for (k, i) in col for v in (k, i)], dtype=np.uint64)
+        aa = ints_to_limbs([x for col in abc for x in col])
+        sa = _g1_limbs(srs)
+        pts = np.zeros(72, dtype=np.uint64)
+        fs = np.zeros(28, dtype=np.uint64)
+        _check(self.lib.pbf_plonk_prove_bn254(self.h, n, _ptr(qa), _ptr(ca), _ptr(aa), _ptr(ints_to_limbs(chal)),
+                                              _ptr(ints_to_limbs(rnd)), _ptr(ints_to_limbs(k1k2)), _ptr(sa), len(srs),
+                                              mode, _ptr(pts), _ptr(fs)))
+        pv = limbs_to_ints(pts)
+        return [None if pv[2 * i] == 0 and pv[2 * i + 1] == 0 else (pv[2 * i], pv[2 * i + 1]) for i in range(9)], \
+            limbs_to_ints(fs)
+
+    def plonk_verify_bn254(self, q, copies, srs, g2s, pts, fields, chal, u, k1k2=(2, 3), mode=0) -> bool:
+        n = len(q[0])
+        qa = ints_to_limbs([x for col in q for x in col])
+        ca = np.array([v for col in copies for (k, i) in col for v in (k, i)], dtype=np.uint64)
+        sa = _g1_limbs(srs)
+        ok = ctypes.c_int(-1)
+        _check(self.lib.pbf_plonk_verify_bn254(self.h, n, _ptr(qa), _ptr(ca), _ptr(sa), len(srs), _ptr(_g2_limbs(g2s)),
+                                               _ptr(_g1_limbs(pts)), _ptr(ints_to_limbs(fields)),
+                                               _ptr(ints_to_limbs(chal)), _ptr(ints_to_limbs([u])),
+                                               _ptr(ints_to_limbs(k1k2)), mode, ctypes.byref(ok)))
+        return ok.value == 1
+
+    def plonk_prove_bn254_dev(self, n, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m, k1k2=(2, 3), mode=0,
+                              stream: int = 0):
+        pts = np.zeros(72, dtype=np.uint64)
+        fs = np.zeros(28, dtype=np.uint64)
+        _check(self.lib.pbf_plonk_prove_bn254_dev(self.h, n, d_q, d_copies, d_abc, _ptr(ints_to_limbs(chal)),
+                                                  _ptr(ints_to_limbs(rnd)), _ptr(ints_to_limbs(k1k2)), d_srs, srs_m,
+                                                  mode, _ptr(pts), _ptr(fs), stream))
+        return pts, fs
 
     # ---- plonk-by-hand types (src/pbh/*.rs), batched on the GPU
     def _u32call(self, fn, a, b, width_out, n):
