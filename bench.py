@@ -235,6 +235,12 @@ def other_configs(ctx, sp) -> dict:
     dout = torch.empty(npair * 48, dtype=torch.int64, device="cuda")
     ms = _time_ms(lambda: ctx.pairing_bn254_dev(d1.data_ptr(), d2.data_ptr(), npair, dout.data_ptr(), stream=sp), 2)
     res["config4_pairings_batch"] = {"ms": ms, "pairings_per_s": npair / (ms / 1e3), "batch": npair}
+    # config 5: generalised PLONK prove (+ verify) of the synthetic mul circuit, 2^20 gates on
+    # one GPU (scripts/bench_prover.py; 2^24 gates: profiles/r01/session2/prover_2p22_2p24.log)
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import bench_prover  # noqa: E402
+
+    res["config5_prove_2p20"] = bench_prover.run(ctx, 20, reps=2)
     # config 1: plonk-by-hand proof + verify (pbh/mod.rs:44-124) through the GPU path
     with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
         k = json.load(f)["plonk_by_hand"]

@@ -179,6 +179,13 @@ int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, cons
                                const uint64_t* proof_f, const uint64_t* chal, const uint64_t* u, const uint64_t* k1k2,
                                int mode, int* ok, void* stream);
 
+/* synthetic config-5 circuit on the device (bench / tests): every gate a*b = c, a, b
+ * uniform (splitmix64 of seed), every 4th gate's c copied into the next gate's a       */
+int pbf_plonk_synth_circuit_bn254_dev(pbf_ctx* ctx, size_t n, uint64_t seed, uint64_t* d_q, uint64_t* d_copies,
+                                      uint64_t* d_abc, void* stream);
+/* SRS::create with the output left on the device (n+1 points)                          */
+int pbf_srs_create_bn254_dev(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* d_out, void* stream);
+
 /* ---- Plonk-by-hand types (BASELINE config 1; src/pbh/{g1,g2,gt,pairing}.rs) -------------------
  * 32-bit words: G1 [x, y, inf] over F101 (y^2 = x^3 + 3), G2 [a, b] (a + b*u over
  * F101[u]/(u^2+2)), GT [a, b]. Inputs must be on the curve (else PBF_EINVAL, where the

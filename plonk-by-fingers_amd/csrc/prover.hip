@@ -23,7 +23,9 @@
 //
 // Field elements at rest in HBM: canonical Fr, 4 x u64 little-endian (the ABI layout);
 // kernels convert to Montgomery on load and back on store.
+#include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <vector>
 #include "../../include/pbf.h"
 #include "ec_bn254.hpp"
@@ -437,6 +439,18 @@ struct Prover {
   U256 omega, omegaN, omegaN_inv, g, g_inv;
   uint64_t w_plain[4], wN_plain[4];
   int* d_bad;
+  bool timing = false;
+  double t_last = 0;
+  // PBF_PROVER_TIMING=1: per-round wall times on stderr (stream synchronised at each mark)
+  void mark(const char* what) {
+    if (!timing) return;
+    (void)hipStreamSynchronize(s);
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double t = ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+    if (t_last > 0) fprintf(stderr, "[pbf prover] %-28s %9.3f ms\n", what, t - t_last);
+    t_last = t;
+  }
 
   int check_bad(const char* what) {
     int bad = 0;
@@ -492,6 +506,8 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   Prover P;
   P.ctx = ctx;
   P.s = (hipStream_t)stream;
+  P.timing = getenv("PBF_PROVER_TIMING") != nullptr;
+  P.mark("start");
   P.n = n;
   P.N = 4 * n;
   P.log_n = log_n;
@@ -542,6 +558,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   hipLaunchKernelGGL(k_satisfies, dim3(blocks_for(n)), dim3(256), 0, s, d_q, d_abc, d_copies, (uint64_t)n, P.d_bad);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
+  P.mark("satisfies");
 
   // ---- h = w^i, sigma labels (plonk.rs:124, 181-189, 222-224)
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
@@ -559,6 +576,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
   for (int k = 0; k < 11; ++k)
     if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
+  P.mark("interpolate (11 INTT)");
   // ---- round 1: a(x) = (b2 + b1 x)(x^n - 1) + f_a(x), likewise b, c (plonk.rs:250-252)
   for (int k = 0; k < 3; ++k) {
     const U256 lo = bl[2 * k + 1], hi = bl[2 * k];  // (b2, b1), (b4, b3), (b6, b5)
@@ -574,6 +592,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   uint64_t pts[9][8];
   for (int k = 0; k < 3; ++k)
     if ((rc = P.commit(d_srs, C(k), n + 2, pts[k]))) return rc;
+  P.mark("round 1 commits (3 MSM)");
 
   // ---- round 2: accumulator (plonk.rs:278-313)
   uint64_t* acc = (uint64_t*)B.acc.p;
@@ -611,7 +630,9 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     PBF_HIP(hipGetLastError());
   }
   uint64_t* zx = acc;  // length n+3
+  P.mark("round 2 accumulator");
   if ((rc = P.commit(d_srs, zx, n + 3, pts[3]))) return rc;
+  P.mark("round 2 commit (MSM)");
 
   // ---- round 3: quotient on the coset g H_4n (plonk.rs:326-382)
   const int cmap[13] = {0, 1, 2, -1, 3, 4, 5, 6, 7, 8, 9, 10, -2};  // coef slot per coset slot
@@ -631,6 +652,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     else { src = C(cmap[k]); len = cmap[k] < 3 ? n + 2 : n; }
     if ((rc = P.coset_ntt(src, len, CE(k)))) return rc;
   }
+  P.mark("round 3 coset NTTs (13)");
   QuotArgs qa;
   qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
   qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);
@@ -659,8 +681,10 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   if ((rc = P.check_bad("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)")))
     return rc;
   if ((rc = P.commit(d_srs, tq, m, pts[4]))) return rc;            // t_lo
+  P.mark("round 3 quotient + INTT");
   if ((rc = P.commit(d_srs, tq + 4 * m, m, pts[5]))) return rc;    // t_mid
   if ((rc = P.commit(d_srs, tq + 8 * m, m, pts[6]))) return rc;    // t_hi
+  P.mark("round 3 commits (3 MSM)");
 
   // ---- round 4: evaluations at z (plonk.rs:393-399), linearisation r(x) (:401-422)
   const U256 zw = Fr::mul(zc, P.omega);
@@ -745,6 +769,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     const U256 xs[1] = {zc};
     if ((rc = eval(1, polys, lens, xs, &r_z))) return rc;
   }
+  P.mark("round 4 evals + r(x)");
 
   // ---- round 5: W_z = [t_lo + z^(n+2) t_mid + z^(2n+4) t_hi - t_z + v (r - r_z) + v^2 (a - a_z)
   //      + v^3 (b - b_z) + v^4 (c - c_z) + v^5 (s1 - s1_z) + v^6 (s2 - s2_z)] / (x - z)   (:430-439)
@@ -807,6 +832,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("W_zw division left a remainder (plonk.rs:442)"))) return rc;
   if ((rc = P.commit(d_srs, W1, n + 2, pts[8]))) return rc;
+  P.mark("round 5 openings + 2 MSM");
 
   for (int i = 0; i < 9; ++i) memcpy(out_pts + 8 * i, pts[i], 64);
   const U256 fo[7] = {a_z, b_z, c_z, s1_z, s2_z, r_z, zw_z};
@@ -1028,4 +1054,86 @@ extern "C" int pbf_plonk_verify_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q,
   PBF_HIP(hipMemcpyAsync(dsrs.p, srs, srs_m * 64, hipMemcpyHostToDevice, s));
   return pbf_plonk_verify_bn254_dev(ctx, n, (const uint64_t*)dq.p, (const uint64_t*)dc.p, (const uint64_t*)dsrs.p,
                                     srs_m, g2, proof_pts, proof_f, chal, u, k1k2, mode, ok, s);
+}
+
+// ---------------------------------------------------------------- synthetic config-5 inputs
+namespace pbf {
+__device__ __forceinline__ uint64_t sm64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// uniform canonical Fr from (seed, stream index): 4 splitmix64 words, top limb masked to
+// 254 bits, re-mixed until < r
+__device__ U256 rand_fr(uint64_t seed, uint64_t i) {
+  const uint64_t G = 0x9E3779B97F4A7C15ull;
+  uint64_t ctr = seed + (i + 1) * G * 4;
+  for (;;) {
+    uint64_t l[4];
+    for (int k = 0; k < 4; ++k) l[k] = sm64(ctr += G);
+    l[3] &= (1ull << 62) - 1;
+    const U256 v = u256_from_u64(l);
+    if (!Fr::geq_p(v)) return v;
+  }
+}
+// BASELINE config 5 circuit: every gate a*b = c (q_m = 1, q_o = -1, q_l = q_r = q_c = 0),
+// a, b uniform; every 4th gate's c feeds the next gate's a (a real copy constraint)
+__global__ void k_synth_circuit(uint64_t n, uint64_t seed, uint64_t* q, uint64_t* copies, uint64_t* abc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  U256 mone;
+  for (int k = 0; k < 8; ++k) mone.w[k] = Bn254FrParams::P[k];
+  mone.w[0] -= 1;  // r - 1
+  const U256 z = u256_zero();
+  U256 one = z;
+  one.w[0] = 1;
+  u256_to_u64(z, q + 4 * i);
+  u256_to_u64(z, q + 4 * (n + i));
+  u256_to_u64(mone, q + 4 * (2 * n + i));
+  u256_to_u64(one, q + 4 * (3 * n + i));
+  u256_to_u64(z, q + 4 * (4 * n + i));
+  U256 b = rand_fr(seed ^ 0xB0B0ull, i);
+  U256 a;
+  if (i % 4 == 1) {  // a_i = c_{i-1} = a_{i-1} b_{i-1}
+    a = Fr::from_mont(Fr::mul(Fr::to_mont(rand_fr(seed, i - 1)), Fr::to_mont(rand_fr(seed ^ 0xB0B0ull, i - 1))));
+  } else {
+    a = rand_fr(seed, i);
+  }
+  const U256 c = Fr::from_mont(Fr::mul(Fr::to_mont(a), Fr::to_mont(b)));
+  u256_to_u64(a, abc + 4 * i);
+  u256_to_u64(b, abc + 4 * (n + i));
+  u256_to_u64(c, abc + 4 * (2 * n + i));
+  // copies (kind, 1-based index): identity, with a_{i} <-> c_{i-1} swapped for i % 4 == 1
+  uint64_t* ca = copies + 2 * i;
+  uint64_t* cb = copies + 2 * (n + i);
+  uint64_t* cc = copies + 2 * (2 * n + i);
+  ca[0] = 0; ca[1] = i + 1;
+  cb[0] = 1; cb[1] = i + 1;
+  cc[0] = 2; cc[1] = i + 1;
+  if (i % 4 == 1) { ca[0] = 2; ca[1] = i; }            // a_i is a copy of c_{i-1}
+  if (i % 4 == 0 && i + 1 < n) { cc[0] = 0; cc[1] = i + 2; }  // c_i is a copy of a_{i+1}
+}
+}  // namespace pbf
+
+extern "C" int pbf_plonk_synth_circuit_bn254_dev(pbf_ctx* ctx, size_t n, uint64_t seed, uint64_t* d_q,
+                                                 uint64_t* d_copies, uint64_t* d_abc, void* stream) {
+  if (!ctx || !d_q || !d_copies || !d_abc) return fail(PBF_EINVAL, "null argument");
+  hipLaunchKernelGGL(k_synth_circuit, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, (uint64_t)n, seed, d_q,
+                     d_copies, d_abc);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+// SRS::create on the device: d_out = [G, sG, ..., s^n G] (n+1 affine points)
+extern "C" int pbf_srs_create_bn254_dev(pbf_ctx* ctx, const uint64_t* s, size_t n, uint64_t* d_out, void* stream) {
+  if (!ctx || !s || !d_out) return fail(PBF_EINVAL, "null argument");
+  if (Fr::geq_p(u256_from_u64(s))) return fail(PBF_EINVAL, "s not canonical");
+  hipStream_t st = (hipStream_t)stream;
+  DevBuf& pw = ctx->buf("srs.pows");
+  int rc = pw.ensure((n + 1) * 32);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + 1 + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, st, (uint64_t*)pw.p,
+                     (uint64_t)(n + 1), hm(s), fr_one_m());
+  PBF_HIP(hipGetLastError());
+  return pbf_g1_bn254_mul_base_dev(ctx, (const uint64_t*)pw.p, d_out, n + 1, stream);
 }

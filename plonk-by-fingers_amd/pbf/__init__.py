@@ -67,6 +67,8 @@ SIGNATURES = [
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("pbf_plonk_verify_bn254_dev", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _sz, _p64, _p64, _p64, _p64, _p64, _p64,
                                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int), _vp]),
+    ("pbf_plonk_synth_circuit_bn254_dev", ctypes.c_int, [_vp, _sz, _u64, _vp, _vp, _vp, _vp]),
+    ("pbf_srs_create_bn254_dev", ctypes.c_int, [_vp, _p64, _sz, _vp, _vp]),
     ("pbf_pbh_g1_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_g2_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
     ("pbf_pbh_gt_pow", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
@@ -268,6 +270,12 @@ class Context:
                                                _ptr(ints_to_limbs(chal)), _ptr(ints_to_limbs([u])),
                                                _ptr(ints_to_limbs(k1k2)), mode, ctypes.byref(ok)))
         return ok.value == 1
+
+    def plonk_synth_circuit_dev(self, n, seed, d_q, d_copies, d_abc, stream: int = 0) -> None:
+        _check(self.lib.pbf_plonk_synth_circuit_bn254_dev(self.h, n, seed, d_q, d_copies, d_abc, stream))
+
+    def srs_create_dev(self, s: int, n: int, d_out: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_srs_create_bn254_dev(self.h, _ptr(ints_to_limbs([s])), n, d_out, stream))
 
     def plonk_prove_bn254_dev(self, n, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m, k1k2=(2, 3), mode=0,
                               stream: int = 0):

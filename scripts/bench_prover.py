@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Config-5 prover timing: synthetic 2^k-gate mul circuit generated on the device, SRS on the
+device, prove (mode 1 = paper linearisation) timed after a warm-up, then one verify.
+Usage: bench_prover.py LOG_N [LOG_N ...]  -> one JSON line per size."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "plonk-by-fingers_amd"))
+import torch  # noqa: E402
+
+import pbf  # noqa: E402
+
+G2 = ((10857046999023057135944570762232829481370756359578518086990519993285655852781,
+       11559732032986387107991004021392285783925812861821192530917403151452391805634),
+      (8495653923123431417604973247489272438418190587263600148770280649306958101930,
+       4082367875863433681332203403145435568316851327593401208105741076214120093531))
+
+
+def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True) -> dict:
+    n = 1 << log_n
+    sp = torch.cuda.current_stream().cuda_stream
+    dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
+    dc = torch.empty(3 * n * 2, dtype=torch.int64, device="cuda")
+    dabc = torch.empty(3 * n * 4, dtype=torch.int64, device="cuda")
+    ctx.plonk_synth_circuit_dev(n, 0x5EED0005, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), stream=sp)
+    srs_m = (n + 3) if mode == 1 else (2 * n + 2)
+    s = 0x5EED0005C0FFEE
+    dsrs = torch.empty(srs_m * 8, dtype=torch.int64, device="cuda")
+    t0 = time.perf_counter()
+    ctx.srs_create_dev(s, srs_m - 1, dsrs.data_ptr(), stream=sp)
+    torch.cuda.synchronize()
+    t_srs = time.perf_counter() - t0
+    chal = [0x1111 * (i + 3) for i in range(5)]
+    rnd = [0x2222 * (i + 5) for i in range(9)]
+    ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(), srs_m,
+                              mode=mode, stream=sp)  # warm-up (plans, buffers)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pts, fs = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd,
+                                            dsrs.data_ptr(), srs_m, mode=mode, stream=sp)
+    torch.cuda.synchronize()
+    t_prove = (time.perf_counter() - t0) / reps
+    out = {"log_n": log_n, "gates": n, "mode": mode, "prove_ms": t_prove * 1e3, "proofs_per_s": 1 / t_prove,
+           "srs_create_ms": t_srs * 1e3}
+    if verify:
+        import ctypes
+
+        import numpy as np
+
+        g2 = ctx.g2_bn254_mul([G2], [s])[0]
+        g2l = pbf._g2_limbs([G2, g2])
+        ok = ctypes.c_int(-1)
+        t0 = time.perf_counter()
+        pbf._check(ctx.lib.pbf_plonk_verify_bn254_dev(ctx.h, n, dq.data_ptr(), dc.data_ptr(), dsrs.data_ptr(), srs_m,
+                                                      pbf._ptr(g2l), pbf._ptr(pts), pbf._ptr(fs),
+                                                      pbf._ptr(pbf.ints_to_limbs(chal)),
+                                                      pbf._ptr(pbf.ints_to_limbs([12345])),
+                                                      pbf._ptr(pbf.ints_to_limbs([2, 3])), mode, ctypes.byref(ok), sp))
+        out["verify_ms"] = (time.perf_counter() - t0) * 1e3
+        out["verified"] = ok.value == 1
+        del np
+    return out
+
+
+if __name__ == "__main__":
+    ctx = pbf.Context(0)
+    for a in sys.argv[1:]:
+        print(json.dumps(run(ctx, int(a))), flush=True)
