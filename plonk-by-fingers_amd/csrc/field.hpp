@@ -83,6 +83,21 @@ struct Goldilocks {
   }
 };
 
+// x * 2^-K (mod p) for a compile-time 1 <= K <= 32, x canonical: with m = -x mod 2^K,
+// x + m*p is divisible by 2^K (p = 1 mod 2^32), and (x + m*p) / 2^K
+//   = ((x + m) >> K) + (m << (32-K)) * (2^32 - 1)      (x + m < 2^64 for canonical x)
+// -- two shifts, one v_mad_u64_u32 and one add_small, against ~25 instructions for the
+// equivalent x * 2^(96-K) * (-1) through mul_pow2 (DESIGN.md "Goldilocks arithmetic").
+template <int K>
+__host__ __device__ __forceinline__ uint64_t gl_div_pow2(uint64_t x) {
+  static_assert(K >= 1 && K <= 32, "division by 2^1 .. 2^32");
+  const uint32_t mask = K == 32 ? 0xFFFFFFFFu : ((1u << (K & 31)) - 1u);
+  const uint32_t m = (0u - (uint32_t)x) & mask;
+  const uint64_t q = (x + m) >> K;
+  const uint32_t mp = K == 32 ? m : (m << ((32 - K) & 31));
+  return Goldilocks::add_small(q, (uint64_t)mp * Goldilocks::EPS);
+}
+
 struct Mod32 {
   __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs& f) {
     uint64_t s = a + b;  // < 2^33

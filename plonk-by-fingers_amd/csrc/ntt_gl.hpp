@@ -29,6 +29,15 @@
 #pragma once
 #include "ntt_kernels.hpp"
 
+// Timing experiment only (make nomath): -DPBF_GL_NOMATH drops every twiddle multiply and
+// register DFT of ntt_gl_pass_kernel, leaving its loads, LDS exchanges, barriers and
+// stores: the data-movement floor of the kernel. Never the product build.
+#ifdef PBF_GL_NOMATH
+#define PBF_GL_MATH(x) do { } while (0)
+#else
+#define PBF_GL_MATH(x) x
+#endif
+
 namespace pbf {
 
 struct GlPassArgs {
@@ -49,17 +58,24 @@ struct GlPassArgs {
   uint32_t xcd_kmajor;     // XCD-aware column-major block order (pass-twiddle table reuse in L2)
 };
 
-// x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1.
+// x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1. Exponents in
+// (160, 192) are divisions by 2^(192-K) (no sign); a remaining sign costs one subtraction.
 template <int K>
 __device__ __forceinline__ uint64_t gl_pow2(uint64_t x) {
-  constexpr int S = ((K % 192) + 192) % 192;
-  if constexpr (S == 0) {
+  constexpr int RAW = ((K % 192) + 192) % 192;
+  if constexpr (RAW == 0) {
     return x;
-  } else if constexpr (S < 96) {
-    return Goldilocks::mul_pow2<S>(x);
+  } else if constexpr (RAW > 160) {
+    return gl_div_pow2<192 - RAW>(x);
   } else {
-    const FieldArgs f{};
-    return Goldilocks::sub(0, Goldilocks::mul_pow2<S - 96>(x), f);
+    using T = ShiftKind<RAW>;
+    const uint64_t y = apply_shift<Goldilocks, T>(x);
+    if constexpr (T::NEG) {
+      const FieldArgs f{};
+      return Goldilocks::sub(0, y, f);
+    } else {
+      return y;
+    }
   }
 }
 
@@ -83,10 +99,12 @@ struct GlShape {
   static constexpr int YP = 65 * W;                 // Y row pitch (elements)
   static constexpr int LDS = (C * YP > TILE) ? C * YP : TILE;
   static constexpr int NSUB_C = (64 * W) / NT;      // stage-C sub-DFTs per thread
-  // Y column swizzle: the first pass's stage C reads 8 k1 x 8 w per wave; w ^ ysw(k1)
-  // spreads them over the banks (2 passes per 512-B wave access, the minimum)
+  // Y column swizzle: the first pass's stage C reads all 64 k1 of one column w per wave
+  // (so its stores are 512-B runs of out[j*R + k]); w ^ ysw(k1) spreads those reads over
+  // the banks, each 8-B bank pair hit twice per 512-B wave access (the minimum). Stage B's
+  // writes and later passes' reads stay permutations within a row (conflict-free).
   __host__ __device__ static constexpr int ysw(int k1) {
-    return W == 8 ? 0 : (W == 16 ? ((k1 >> 1) & 1) * 8 : (k1 & 3) * 8);
+    return W <= 32 ? (k1 / (32 / W)) & (W - 1) : (k1 & 31);
   }
 };
 
@@ -96,10 +114,16 @@ struct GlShape {
 // pass-twiddle table is fetched into that XCD's L2 once per pass, not once per polynomial.
 __device__ __forceinline__ void gl_tile_coords(const GlPassArgs& a, uint32_t tile, uint32_t tiles, uint32_t* poly,
                                                uint32_t* kb) {
-  if (a.xcd_kmajor) {
+  if (a.xcd_kmajor == 1) {
     const uint32_t v = (tile & 7) * (tiles >> 3) + (tile >> 3);
     *kb = v / a.batch;
     *poly = v % a.batch;
+  } else if (a.xcd_kmajor == 2) {
+    // XCD-blocked, polynomial-major: workgroups resident together on one XCD take adjacent
+    // column blocks, so the 128-B lines their W*8-B runs share are fetched into one L2
+    const uint32_t v = (tile & 7) * (tiles >> 3) + (tile >> 3);
+    *poly = v / a.blocks_per_poly;
+    *kb = v % a.blocks_per_poly;
   } else {
     *poly = tile / a.blocks_per_poly;
     *kb = tile % a.blocks_per_poly;
@@ -115,7 +139,7 @@ ntt_gl_pass_kernel(GlPassArgs a) {
   using Sh = GlShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
   static_assert(LOGR >= 6 && LOGR <= 10, "radix 2^6 .. 2^10");
-  static_assert(Sh::LDS * 8 <= 80 * 1024, "two workgroups per CU");
+  static_assert(Sh::LDS * 8 <= (TILE > 8192 ? 160 : 80) * 1024, "LDS budget");
   static_assert(Sh::W >= 8 && Sh::WPQ >= 1, "tile shape");
   __shared__ uint64_t lds[Sh::LDS];
   const FieldArgs f{};
@@ -163,11 +187,15 @@ ntt_gl_pass_kernel(GlPassArgs a) {
           }
         }
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[8 * h + m] = G::mul(v[8 * h + m], tw[m], f);
+        for (int m = 0; m < 8; ++m) PBF_GL_MATH(v[8 * h + m] = G::mul(v[8 * h + m], tw[m], f));
+#ifdef PBF_GL_NOMATH
+#pragma unroll
+        for (int m = 0; m < 8; ++m) v[8 * h + m] ^= tw[m];
+#endif
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f);
+    for (int u = 0; u < 4; ++u) PBF_GL_MATH((dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f)));
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int idx = t + NT * u;  // = s2*(C*W) + (r2*W + w)
@@ -184,6 +212,7 @@ ntt_gl_pass_kernel(GlPassArgs a) {
       const int rw = (wave % Sh::WPQ) * 64 + (t & 63);  // r2*W + w
 #pragma unroll
       for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
+#ifndef PBF_GL_NOMATH
       switch (__builtin_amdgcn_readfirstlane(q1)) {
         case 1: gl_stage_b_twiddle<E64, 1>(v); break;
         case 2: gl_stage_b_twiddle<E64, 2>(v); break;
@@ -191,6 +220,7 @@ ntt_gl_pass_kernel(GlPassArgs a) {
         default: break;
       }
       dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
+#endif
       __syncthreads();
       const int r2 = rw / W, w = rw % W;
 #pragma unroll
@@ -233,18 +263,23 @@ ntt_gl_pass_kernel(GlPassArgs a) {
     }
     if (a.scaled) {
 #pragma unroll
-      for (int m = 0; m < Sh::NSUB_C * C; ++m) x[m] = G::mul(x[m], tw[m], f);
+      for (int m = 0; m < Sh::NSUB_C * C; ++m) PBF_GL_MATH(x[m] = G::mul(x[m], tw[m], f));
     } else {
       // r2 = 0 rows multiply by 1 and are skipped; k1 = 0 lanes multiply by 1 (a per-lane
       // branch would only diverge)
 #pragma unroll
       for (int u = 0; u < Sh::NSUB_C; ++u)
 #pragma unroll
-        for (int r2 = 1; r2 < C; ++r2) x[u * C + r2] = G::mul(x[u * C + r2], tw[u * C + r2], f);
+        for (int r2 = 1; r2 < C; ++r2) {
+          PBF_GL_MATH(x[u * C + r2] = G::mul(x[u * C + r2], tw[u * C + r2], f));
+#ifdef PBF_GL_NOMATH
+          x[u * C + r2] ^= tw[u * C + r2];
+#endif
+        }
     }
     if constexpr (C > 1) {
 #pragma unroll
-      for (int u = 0; u < Sh::NSUB_C; ++u) dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f);
+      for (int u = 0; u < Sh::NSUB_C; ++u) PBF_GL_MATH((dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f)));
     }
 
     // ---------------- store

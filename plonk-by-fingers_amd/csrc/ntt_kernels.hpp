@@ -78,13 +78,27 @@ __device__ __forceinline__ uint64_t tw_pow(const PassArgs& a, uint64_t e) {
 // E >= 0: w_q = 2^E (mod p) — Goldilocks standard roots of order <= 64 are powers
 // of two — so every twiddle is a shift-reduction; a twiddle -2^(S-96) folds its
 // sign into the butterfly's subtraction.
-template <int E, int LOGQ, int H, int A>
-struct TwShift {
-  static constexpr int Q = 1 << LOGQ;
-  static constexpr int RAW = (E * A * (Q / (2 * H))) % 192;
-  static constexpr bool NEG = RAW >= 96;
-  static constexpr int S = NEG ? RAW - 96 : RAW;
+// Twiddle 2^RAW (RAW mod 192; 2^96 = -1) as the cheapest equivalent: x*2^S for S <= 64,
+// else -x*2^-(96-S) (a division by 2^K, K < 32, gl_div_pow2), with the sign folded into
+// the butterfly's subtraction (NEG) — see DESIGN.md "Goldilocks arithmetic".
+template <int RAW_>
+struct ShiftKind {
+  static constexpr int RAW = ((RAW_ % 192) + 192) % 192;
+  static constexpr bool NEG0 = RAW >= 96;
+  static constexpr int S0 = NEG0 ? RAW - 96 : RAW;   // x * 2^RAW = (-1)^NEG0 x * 2^S0
+  static constexpr bool DIV = S0 > 64;               // 2^S0 = -2^-(96-S0)
+  static constexpr bool NEG = DIV ? !NEG0 : NEG0;
+  static constexpr int S = DIV ? 96 - S0 : S0;       // shift (DIV: divisor exponent)
 };
+template <int E, int LOGQ, int H, int A>
+struct TwShift : ShiftKind<(E * A * ((1 << LOGQ) / (2 * H))) % 192> {};
+
+// d * 2^S (mul) or d / 2^S (div) for a ShiftKind
+template <class F, class T>
+__device__ __forceinline__ uint64_t apply_shift(uint64_t d) {
+  if constexpr (T::DIV) return gl_div_pow2<T::S>(d);
+  else return F::template mul_pow2<T::S>(d);
+}
 
 template <class F, int LOGQ, int E, int H, int A>
 __device__ __forceinline__ void dif_bfly(uint64_t* v, int blk, const uint64_t* wq, const FieldArgs& f) {
@@ -98,7 +112,7 @@ __device__ __forceinline__ void dif_bfly(uint64_t* v, int blk, const uint64_t* w
   } else {
     using T = TwShift<E, LOGQ, H, A>;
     const uint64_t d = T::NEG ? F::sub(y, x, f) : F::sub(x, y, f);
-    v[blk + A + H] = F::template mul_pow2<T::S>(d);
+    v[blk + A + H] = apply_shift<F, T>(d);
   }
 }
 

@@ -381,13 +381,16 @@ static GlPassFn gl_fn_t(int logr, bool first) {
 // Tile of R x W elements per workgroup: 4096 (four workgroups per CU) or 8192 (two);
 // radix 2^10 always 8192 (W >= 8: 64-B runs in HBM).
 static int gl_tile(int logr) {
-  if (logr >= 10) return 8192;
   const char* env = getenv("PBF_NTT_TILE");  // A/B override
-  return (env && atoi(env) == 8192) ? 8192 : 4096;
+  const int e = env ? atoi(env) : 0;
+  if (logr >= 10) return e == 16384 ? 16384 : 8192;
+  return e == 8192 ? 8192 : 4096;
 }
 
 template <int E>
 static GlPassFn gl_fn_e(int logr, bool first, int tile) {
+  if (logr == 10 && tile == 16384)
+    return first ? ntt_gl_pass_kernel<10, E, true, 16384> : ntt_gl_pass_kernel<10, E, false, 16384>;
   if (logr == 10) return first ? ntt_gl_pass_kernel<10, E, true, 8192> : ntt_gl_pass_kernel<10, E, false, 8192>;
   return tile == 8192 ? gl_fn_t<E, 8192>(logr, first) : gl_fn_t<E, 4096>(logr, first);
 }
@@ -422,6 +425,10 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     const uint64_t tiles = (uint64_t)a.blocks_per_poly * batch;
     if (tiles > 0x7fffffffull) return fail(1, "batch too large");
     a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
+    if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
+      const uint32_t ord = (uint32_t)atoi(o);
+      a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
+    }
     hipLaunchKernelGGL(fn, dim3((uint32_t)tiles), dim3(tile / 16), 0, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;

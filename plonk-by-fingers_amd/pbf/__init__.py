@@ -15,7 +15,8 @@ from typing import Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libpbf.so")
+# PBF_LIB: an alternative in-tree build (timing experiments, e.g. libpbf_nomath.so)
+LIB_PATH = os.environ.get("PBF_LIB") or os.path.join(os.path.dirname(_HERE), "libpbf.so")
 
 GOLDILOCKS = 0xFFFFFFFF00000001
 

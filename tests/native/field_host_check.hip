@@ -1,6 +1,7 @@
 // Host-side check of the device Goldilocks arithmetic (csrc/field.hpp, compiled for the
 // host by hipcc) against unsigned __int128 arithmetic: edge values and random operands
-// for add/sub/mul/reduce128 and every compile-time shift mul_pow2<S>, S < 96.
+// for add/sub/mul/reduce128, every compile-time shift mul_pow2<S>, S < 96, and every
+// division gl_div_pow2<K>, 1 <= K <= 32.
 #include "../../plonk-by-fingers_amd/csrc/field.hpp"
 #include <cstdio>
 #include <random>
@@ -29,6 +30,21 @@ template <int... S>
 static void all_shifts(const uint64_t* xs, int m, std::integer_sequence<int, S...>) {
   (shift_check<S>(xs, m), ...);
 }
+static uint64_t inv2k(int k) {  // 2^-k mod p
+  u128 x = 1, h = (P + 1) / 2;  // 1/2
+  for (int i = 0; i < k; ++i) x = (x * h) % P;
+  return (uint64_t)x;
+}
+template <int K>
+static void div_check(const uint64_t* xs, int m) {
+  const uint64_t t = inv2k(K);
+  for (int i = 0; i < m; ++i)
+    expect("gl_div_pow2", gl_div_pow2<K>(xs[i]), (uint64_t)(((u128)xs[i] * t) % P), xs[i], K);
+}
+template <int... K>
+static void all_divs(const uint64_t* xs, int m, std::integer_sequence<int, K...>) {
+  (div_check<K + 1>(xs, m), ...);
+}
 int main() {
   std::mt19937_64 g(1);
   const FieldArgs f{P, 0};
@@ -51,6 +67,12 @@ int main() {
     expect("reduce128", Goldilocks::reduce128(lo, hi), (uint64_t)((((u128)hi << 64) | lo) % P), lo, hi);
   }
   all_shifts(xs, 64, std::make_integer_sequence<int, 96>{});
+  all_divs(xs, 64, std::make_integer_sequence<int, 32>{});
+  {
+    uint64_t ys[4096];
+    for (int i = 0; i < 4096; ++i) ys[i] = i < 64 ? xs[i] : g() % P;
+    all_divs(ys, 4096, std::make_integer_sequence<int, 32>{});
+  }
   printf("field_host_check bad=%ld\n", bad);
   return bad != 0;
 }
