@@ -157,7 +157,8 @@ def main() -> int:
                        "passes": os.environ.get("PBF_NTT_PASSES", "default")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.log_n, B),
-                         "kernel": "ntt_pass_kernel (all passes of one batched NTT; 16*n bytes per transform)"},
+                         "kernel": "ntt_gl_pass_kernel (all passes of one batched NTT, HIP events on the launch "
+                                   "stream; algorithmic bytes 16*n per transform)"},
         }
         if world == 1 and not args.no_extra:
             out["extra"] = other_configs(ctx, sp)

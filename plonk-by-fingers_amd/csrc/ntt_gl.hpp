@@ -37,6 +37,14 @@
 #else
 #define PBF_GL_MATH(x) x
 #endif
+// Timing experiment only (make nomem): every tile loads tile 0 of polynomial 0 (L2-resident)
+// and stores only values equal to a sentinel that never occurs: the kernel's compute, LDS
+// and barrier time without HBM traffic.
+#ifdef PBF_GL_NOMEM
+#define PBF_GL_NOMEM_ON 1
+#else
+#define PBF_GL_NOMEM_ON 0
+#endif
 
 namespace pbf {
 
@@ -130,128 +138,166 @@ __device__ __forceinline__ void gl_tile_coords(const GlPassArgs& a, uint32_t til
   }
 }
 
-// One tile per workgroup (a persistent variant that LDS-DMA'd the next tile during stage
-// C measured 0.52 vs 0.47 ms at 2^20 x 32: the loop's address bookkeeping cost more VALU
-// than the overlap gained; two resident workgroups per CU already overlap each other).
-template <int LOGR, int E64, bool FIRST, int TILE>
-__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_gl_pass_kernel(GlPassArgs a) {
+// LDS-DMA of one tile's pass input (R rows x W columns, row-major [r][w] image) into
+// `raw`: 16-B chunks, lane-linear LDS destination, per-lane global source.
+template <int LOGR, int TILE>
+__device__ __forceinline__ void gl_tile_dma(uint64_t* raw, const GlPassArgs& a, uint32_t tile, uint32_t tiles,
+                                            int t) {
+  using Sh = GlShape<LOGR, TILE>;
+  uint32_t poly, kb;
+  gl_tile_coords(a, tile, tiles, &poly, &kb);
+  const uint64_t* in = a.in + (uint64_t)poly * a.n + (uint64_t)kb * Sh::W;
+  const uint64_t stride = a.n >> LOGR;
+  const int wave = t >> 6, lane = t & 63;
+#pragma unroll
+  for (int i = 0; i < TILE / 2 / Sh::NT; ++i) {
+    const int q0 = wave * 64 + i * Sh::NT;  // first chunk of this wave-instruction
+    const int q = q0 + lane;
+    const int row = q / (Sh::W / 2), col = 2 * (q % (Sh::W / 2));
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(in + col + (uint64_t)row * stride),
+                                     (__attribute__((address_space(3))) void*)(raw + 2 * q0), 16, 0, 0);
+  }
+}
+
+// Workgroup barrier. PERSIST kernels keep an LDS-DMA in flight across the tile's stages,
+// so they use a raw s_barrier after lgkmcnt(0): __syncthreads() would also wait vmcnt(0)
+// and drain the DMA and the previous tile's stores.
+template <bool PERSIST>
+__device__ __forceinline__ void gl_bar() {
+  if constexpr (PERSIST) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
+
+// One tile: stages A, B, C and the stores. PERSIST: the tile's raw input is already in LDS
+// (lds[r*W + w]); after stage C has consumed the exchange buffer and its twiddles, the
+// next tile `next` is LDS-DMA'd into it while the C-point DFTs and the stores run.
+template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST>
+__device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t,
+                                        uint32_t next) {
   using Sh = GlShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
-  static_assert(LOGR >= 6 && LOGR <= 10, "radix 2^6 .. 2^10");
-  static_assert(Sh::LDS * 8 <= (TILE > 8192 ? 160 : 80) * 1024, "LDS budget");
-  static_assert(Sh::W >= 8 && Sh::WPQ >= 1, "tile shape");
-  __shared__ uint64_t lds[Sh::LDS];
+  static_assert(Sh::NSUB_C * C == GL_STORES, "stores per thread");
   const FieldArgs f{};
   using G = Goldilocks;
-  const int t = threadIdx.x;
-  const uint32_t tiles = a.blocks_per_poly * a.batch;
-  {
-    const uint32_t tile = blockIdx.x;
-    uint32_t poly, kb;
-    gl_tile_coords(a, tile, tiles, &poly, &kb);
-    const uint64_t j0 = (uint64_t)kb * W;
-    const uint64_t* in = a.in + (uint64_t)poly * a.n;
-    const uint64_t stride = a.n >> LOGR;
+  uint32_t poly, kb;
+  gl_tile_coords(a, tile, tiles, &poly, &kb);
+  if constexpr (PBF_GL_NOMEM_ON) kb &= 1, poly = 0;
+  const uint64_t j0 = (uint64_t)kb * W;
+  const uint64_t* in = a.in + (uint64_t)poly * a.n;
+  const uint64_t stride = a.n >> LOGR;
 
-    // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
-    uint64_t v[16];
+  // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
+  uint64_t v[16];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = t + NT * u;
-      const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
+  for (int u = 0; u < 4; ++u) {
+    const int idx = t + NT * u;
+    const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
 #pragma unroll
-      for (int s1 = 0; s1 < 4; ++s1) v[u * 4 + s1] = in[(j0 + w) + (uint64_t)(16 * C * s1 + C * s2 + r2) * stride];
+    for (int s1 = 0; s1 < 4; ++s1) {
+      const int r = 16 * C * s1 + C * s2 + r2;
+      if constexpr (PERSIST)
+        v[u * 4 + s1] = lds[r * W + w];
+      else
+        v[u * 4 + s1] = in[(j0 + w) + (uint64_t)r * stride];
     }
-    if constexpr (!FIRST) {
-      const uint64_t kmask = (1ull << a.log_ns) - 1;
-      // in groups of 8 elements (loads of a group issue back to back; bounded live registers)
+  }
+  if constexpr (!FIRST) {
+    const uint64_t kmask = (1ull << a.log_ns) - 1;
+    // in groups of 8 elements (loads of a group issue back to back; bounded live registers)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint64_t tw[8];
+    for (int h = 0; h < 2; ++h) {
+      uint64_t tw[8];
 #pragma unroll
-        for (int uu = 0; uu < 2; ++uu) {
-          const int u = 2 * h + uu;
-          const int idx = t + NT * u;
-          const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
-          const uint64_t k = (j0 + w) & kmask;
+      for (int uu = 0; uu < 2; ++uu) {
+        const int u = 2 * h + uu;
+        const int idx = t + NT * u;
+        const int w = idx % W, r2 = (idx / W) % C, s2 = idx / (C * W);
+        const uint64_t k = (j0 + w) & kmask;
 #pragma unroll
-          for (int s1 = 0; s1 < 4; ++s1) {
-            const uint64_t r = (uint64_t)(16 * C * s1 + C * s2 + r2);
-            if (a.twpass) {
-              tw[uu * 4 + s1] = a.twpass[(r << a.log_ns) + k];
-            } else {
-              const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
-              tw[uu * 4 + s1] = G::mul(a.tw0[e & ((1ull << a.tw_bits) - 1)], a.tw1[e >> a.tw_bits], f);
-            }
+        for (int s1 = 0; s1 < 4; ++s1) {
+          const uint64_t r = (uint64_t)(16 * C * s1 + C * s2 + r2);
+          if (a.twpass) {
+            tw[uu * 4 + s1] = a.twpass[(r << a.log_ns) + k];
+          } else {
+            const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
+            tw[uu * 4 + s1] = G::mul(a.tw0[e & ((1ull << a.tw_bits) - 1)], a.tw1[e >> a.tw_bits], f);
           }
         }
+      }
 #pragma unroll
-        for (int m = 0; m < 8; ++m) PBF_GL_MATH(v[8 * h + m] = G::mul(v[8 * h + m], tw[m], f));
+      for (int m = 0; m < 8; ++m) PBF_GL_MATH(v[8 * h + m] = G::mul(v[8 * h + m], tw[m], f));
 #ifdef PBF_GL_NOMATH
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[8 * h + m] ^= tw[m];
+      for (int m = 0; m < 8; ++m) v[8 * h + m] ^= tw[m];
 #endif
-      }
     }
+  }
+  if constexpr (PERSIST) gl_bar<true>();  // raw tile consumed before Z overwrites it
 #pragma unroll
-    for (int u = 0; u < 4; ++u) PBF_GL_MATH((dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f)));
+  for (int u = 0; u < 4; ++u) PBF_GL_MATH((dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f)));
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = t + NT * u;  // = s2*(C*W) + (r2*W + w)
-      const int s2 = idx / (C * W), rw = idx % (C * W);
+  for (int u = 0; u < 4; ++u) {
+    const int idx = t + NT * u;  // = s2*(C*W) + (r2*W + w)
+    const int s2 = idx / (C * W), rw = idx % (C * W);
 #pragma unroll
-      for (int q1 = 0; q1 < 4; ++q1) lds[(q1 * 16 + s2) * (C * W) + rw] = v[u * 4 + bitrev_c(q1, 2)];
-    }
-    __syncthreads();
+    for (int q1 = 0; q1 < 4; ++q1) lds[(q1 * 16 + s2) * (C * W) + rw] = v[u * 4 + bitrev_c(q1, 2)];
+  }
+  gl_bar<PERSIST>();
 
-    // ---------------- stage B: one q1 per wave; shift twiddles; 16-point DFT over s2
-    {
-      const int wave = t >> 6;
-      const int q1 = wave / Sh::WPQ;
-      const int rw = (wave % Sh::WPQ) * 64 + (t & 63);  // r2*W + w
+  // ---------------- stage B: one q1 per wave; shift twiddles; 16-point DFT over s2
+  {
+    const int wave = t >> 6;
+    const int q1 = wave / Sh::WPQ;
+    const int rw = (wave % Sh::WPQ) * 64 + (t & 63);  // r2*W + w
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
+    for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
 #ifndef PBF_GL_NOMATH
-      switch (__builtin_amdgcn_readfirstlane(q1)) {
-        case 1: gl_stage_b_twiddle<E64, 1>(v); break;
-        case 2: gl_stage_b_twiddle<E64, 2>(v); break;
-        case 3: gl_stage_b_twiddle<E64, 3>(v); break;
-        default: break;
-      }
-      dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
+    switch (__builtin_amdgcn_readfirstlane(q1)) {
+      case 1: gl_stage_b_twiddle<E64, 1>(v); break;
+      case 2: gl_stage_b_twiddle<E64, 2>(v); break;
+      case 3: gl_stage_b_twiddle<E64, 3>(v); break;
+      default: break;
+    }
+    dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
 #endif
-      __syncthreads();
-      const int r2 = rw / W, w = rw % W;
+    gl_bar<PERSIST>();
+    const int r2 = rw / W, w = rw % W;
 #pragma unroll
-      for (int q2 = 0; q2 < 16; ++q2) {
-        const int k1 = q1 + 4 * q2;
-        lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))] = v[bitrev_c(q2, 4)];
-      }
+    for (int q2 = 0; q2 < 16; ++q2) {
+      const int k1 = q1 + 4 * q2;
+      lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))] = v[bitrev_c(q2, 4)];
     }
-    __syncthreads();
+  }
+  gl_bar<PERSIST>();
 
-    // ---------------- stage C: table twiddle w_R^(r2*k1); C-point DFT over r2
-    // sub-DFT (k1, w) of thread t: FIRST pass 8 k1 x 8 w per wave (64-B runs of k in the
-    // output rows out[j*R + k]); later passes w fastest (W-element runs of j)
-    auto c_map = [&](int u, int* k1, int* w) {
-      const int idx = t + NT * u;
-      if constexpr (FIRST) {
-        *k1 = (idx & 7) + 8 * ((idx >> 3) / W);
-        *w = (idx >> 3) % W;
-      } else {
-        *k1 = idx / W;
-        *w = idx % W;
-      }
-    };
-    uint64_t x[Sh::NSUB_C * C];
-#pragma unroll
-    for (int u = 0; u < Sh::NSUB_C; ++u) {
-      int k1, w;
-      c_map(u, &k1, &w);
-#pragma unroll
-      for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
+  // ---------------- stage C: table twiddle w_R^(r2*k1); C-point DFT over r2
+  // sub-DFT (k1, w) of thread t: FIRST pass all 64 k1 of one column per wave (512-B runs
+  // of k in the output rows out[j*R + k]); later passes w fastest (W-element runs of j)
+  auto c_map = [&](int u, int* k1, int* w) {
+    const int idx = t + NT * u;
+    if constexpr (FIRST) {
+      *k1 = idx & 63;
+      *w = idx >> 6;
+    } else {
+      *k1 = idx / W;
+      *w = idx % W;
     }
+  };
+  uint64_t x[Sh::NSUB_C * C];
+#pragma unroll
+  for (int u = 0; u < Sh::NSUB_C; ++u) {
+    int k1, w;
+    c_map(u, &k1, &w);
+#pragma unroll
+    for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
+  }
+  {
     uint64_t tw[Sh::NSUB_C * C];
     const int r2lo = a.scaled ? 0 : 1;  // scaled table carries n^-1: every element multiplies
 #pragma unroll
@@ -277,46 +323,99 @@ ntt_gl_pass_kernel(GlPassArgs a) {
 #endif
         }
     }
-    if constexpr (C > 1) {
+  }
+  if constexpr (PERSIST) {
+    // every wave has read the exchange buffer and consumed its twiddle loads: the next
+    // tile's LDS-DMA runs during the C-point DFTs and the stores (no ordinary load is
+    // consumed after it, so no compiler vmcnt wait drains it)
+    gl_bar<true>();
+    if (next < tiles) gl_tile_dma<LOGR, TILE>(lds, a, next, tiles, t);
+  }
+  if constexpr (C > 1) {
 #pragma unroll
-      for (int u = 0; u < Sh::NSUB_C; ++u) PBF_GL_MATH((dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f)));
-    }
+    for (int u = 0; u < Sh::NSUB_C; ++u) PBF_GL_MATH((dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f)));
+  }
 
-    // ---------------- store
-    if constexpr (FIRST) {
-      uint64_t* o = a.out + (uint64_t)poly * a.n;
+  // ---------------- store
+  if constexpr (FIRST) {
+    uint64_t* o = a.out + (uint64_t)poly * a.n;
 #pragma unroll
-      for (int u = 0; u < Sh::NSUB_C; ++u) {
-        int k1, w;
-        c_map(u, &k1, &w);
-        const uint64_t base = (j0 + w) << LOGR;
+    for (int u = 0; u < Sh::NSUB_C; ++u) {
+      int k1, w;
+      c_map(u, &k1, &w);
+      const uint64_t base = (j0 + w) << LOGR;
 #pragma unroll
-        for (int k2 = 0; k2 < C; ++k2) o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
-      }
-    } else {
-      const uint64_t ns_mask = (1ull << a.log_ns) - 1;
-      uint64_t* out = a.out + (uint64_t)poly * a.n;
-      const uint32_t sl = a.out_split_log;
+      for (int k2 = 0; k2 < C; ++k2)
+        if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
+          o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
+    }
+  } else {
+    const uint64_t ns_mask = (1ull << a.log_ns) - 1;
+    uint64_t* out = a.out + (uint64_t)poly * a.n;
+    const uint32_t sl = a.out_split_log;
 #pragma unroll
-      for (int u = 0; u < Sh::NSUB_C; ++u) {
-        int k1, w;
-        c_map(u, &k1, &w);
-        const uint64_t j = j0 + w;
-        const uint64_t base = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask);
-        if (sl == 0) {
+    for (int u = 0; u < Sh::NSUB_C; ++u) {
+      int k1, w;
+      c_map(u, &k1, &w);
+      const uint64_t j = j0 + w;
+      const uint64_t base = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask);
+      if (sl == 0) {
 #pragma unroll
-          for (int k2 = 0; k2 < C; ++k2)
+        for (int k2 = 0; k2 < C; ++k2)
+          if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
             out[base + ((uint64_t)(k1 + 64 * k2) << a.log_ns)] = x[u * C + bitrev_c(k2, LOGC)];
-        } else {
-          const uint64_t smask = (1ull << sl) - 1;
+      } else {
+        const uint64_t smask = (1ull << sl) - 1;
 #pragma unroll
-          for (int k2 = 0; k2 < C; ++k2) {
-            const uint64_t kk = base + ((uint64_t)(k1 + 64 * k2) << a.log_ns);
-            a.out[((((kk >> sl) * a.batch) + poly) << sl) + (kk & smask)] = x[u * C + bitrev_c(k2, LOGC)];
-          }
+        for (int k2 = 0; k2 < C; ++k2) {
+          const uint64_t kk = base + ((uint64_t)(k1 + 64 * k2) << a.log_ns);
+          a.out[((((kk >> sl) * a.batch) + poly) << sl) + (kk & smask)] = x[u * C + bitrev_c(k2, LOGC)];
         }
       }
     }
+  }
+}
+
+template <int LOGR, int TILE>
+__device__ __forceinline__ void gl_shape_checks() {
+  using Sh = GlShape<LOGR, TILE>;
+  static_assert(LOGR >= 6 && LOGR <= 10, "radix 2^6 .. 2^10");
+  static_assert(Sh::LDS * 8 <= (TILE > 8192 ? 160 : 80) * 1024, "LDS budget");
+  static_assert(Sh::W >= 8 && Sh::WPQ >= 1, "tile shape");
+}
+
+// One tile per workgroup.
+template <int LOGR, int E64, bool FIRST, int TILE>
+__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_gl_pass_kernel(GlPassArgs a) {
+  gl_shape_checks<LOGR, TILE>();
+  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
+  const uint32_t tiles = a.blocks_per_poly * a.batch;
+  gl_tile<LOGR, E64, FIRST, TILE, false>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
+}
+
+// Persistent, software-pipelined (PBF_NTT_PERSIST): each workgroup walks tiles blockIdx.x,
+// +gridDim.x, ...; tile i+1's input LDS-DMA overlaps tile i's C-point DFTs and stores. The
+// counted vmcnt(GL_STORES) at the end of an iteration retires the DMA without waiting for
+// the younger stores (loads and stores share vmcnt, in issue order).
+template <int LOGR, int E64, bool FIRST, int TILE>
+__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_gl_pass_pkernel(GlPassArgs a) {
+  gl_shape_checks<LOGR, TILE>();
+  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
+  const uint32_t tiles = a.blocks_per_poly * a.batch;
+  uint32_t tile = blockIdx.x;
+  if (tile >= tiles) return;
+  gl_tile_dma<LOGR, TILE>(lds, a, tile, tiles, threadIdx.x);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (; tile < tiles; tile += gridDim.x) {
+    // opaque copy of the thread index: keeps per-thread address arithmetic inside the loop
+    // (hoisted out of it, its live values would spill the 128-VGPR budget)
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    gl_bar<true>();  // this tile's DMA landed in every wave
+    gl_tile<LOGR, E64, FIRST, TILE, true>(a, lds, tile, tiles, t, tile + gridDim.x);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL_STORES) : "memory");  // next tile's DMA, not the stores
   }
 }
 

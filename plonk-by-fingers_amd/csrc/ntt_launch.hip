@@ -344,8 +344,8 @@ int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, u
 
 // Persistent grid: every resident workgroup slot once (blocks per CU from the
 // occupancy query x CUs), never more than there are tiles.
-static uint32_t persistent_grid(PassFn fn, int nt, uint64_t tiles) {
-  static std::map<std::pair<PassFn, int>, uint32_t> cache;
+static uint32_t persistent_grid(const void* fn, int nt, uint64_t tiles) {
+  static std::map<std::pair<const void*, int>, uint32_t> cache;
   auto key = std::make_pair(fn, nt);
   auto it = cache.find(key);
   uint32_t slots;
@@ -355,7 +355,7 @@ static uint32_t persistent_grid(PassFn fn, int nt, uint64_t tiles) {
     int dev = 0, cus = 256, per_cu = 1;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, nt, 0) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess || per_cu < 1)
       per_cu = 1;
     slots = (uint32_t)(cus * per_cu);
     cache[key] = slots;
@@ -367,13 +367,15 @@ static uint32_t persistent_grid(PassFn fn, int nt, uint64_t tiles) {
 
 typedef void (*GlPassFn)(GlPassArgs);
 
+#define PBF_GL_K(LR, FIRST, T) (persist ? ntt_gl_pass_pkernel<LR, E, FIRST, T> : ntt_gl_pass_kernel<LR, E, FIRST, T>)
+
 template <int E, int T>
-static GlPassFn gl_fn_t(int logr, bool first) {
+static GlPassFn gl_fn_t(int logr, bool first, bool persist) {
   switch (logr) {
-    case 6: return first ? ntt_gl_pass_kernel<6, E, true, T> : ntt_gl_pass_kernel<6, E, false, T>;
-    case 7: return first ? ntt_gl_pass_kernel<7, E, true, T> : ntt_gl_pass_kernel<7, E, false, T>;
-    case 8: return first ? ntt_gl_pass_kernel<8, E, true, T> : ntt_gl_pass_kernel<8, E, false, T>;
-    case 9: return first ? ntt_gl_pass_kernel<9, E, true, T> : ntt_gl_pass_kernel<9, E, false, T>;
+    case 6: return first ? PBF_GL_K(6, true, T) : PBF_GL_K(6, false, T);
+    case 7: return first ? PBF_GL_K(7, true, T) : PBF_GL_K(7, false, T);
+    case 8: return first ? PBF_GL_K(8, true, T) : PBF_GL_K(8, false, T);
+    case 9: return first ? PBF_GL_K(9, true, T) : PBF_GL_K(9, false, T);
     default: return nullptr;
   }
 }
@@ -388,22 +390,42 @@ static int gl_tile(int logr) {
 }
 
 template <int E>
-static GlPassFn gl_fn_e(int logr, bool first, int tile) {
-  if (logr == 10 && tile == 16384)
-    return first ? ntt_gl_pass_kernel<10, E, true, 16384> : ntt_gl_pass_kernel<10, E, false, 16384>;
-  if (logr == 10) return first ? ntt_gl_pass_kernel<10, E, true, 8192> : ntt_gl_pass_kernel<10, E, false, 8192>;
-  return tile == 8192 ? gl_fn_t<E, 8192>(logr, first) : gl_fn_t<E, 4096>(logr, first);
+static GlPassFn gl_fn_e(int logr, bool first, int tile, bool persist) {
+  if (logr == 10 && tile == 16384) return first ? PBF_GL_K(10, true, 16384) : PBF_GL_K(10, false, 16384);
+  if (logr == 10) return first ? PBF_GL_K(10, true, 8192) : PBF_GL_K(10, false, 8192);
+  return tile == 8192 ? gl_fn_t<E, 8192>(logr, first, persist) : gl_fn_t<E, 4096>(logr, first, persist);
 }
+#undef PBF_GL_K
 
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
+static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log);
+
+// Polynomials in groups of G (PBF_NTT_GROUP): all passes of one group before the next, so
+// a group's intermediate stays in the 256 MB Infinity Cache between its passes.
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log) {
+  size_t G = batch;
+  if (const char* g = getenv("PBF_NTT_GROUP")) G = (size_t)atoll(g);
+  if (split_log != 0 || G == 0 || G >= batch) return run_gl_group(p, d_in, d_out, batch, s0, s1, stream, split_log);
+  for (size_t g0 = 0; g0 < batch; g0 += G) {
+    const size_t b = batch - g0 < G ? batch - g0 : G;
+    const int rc = run_gl_group(p, d_in + g0 * p.n, d_out + g0 * p.n, b, s0, s1, stream, 0);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log) {
   const size_t P = p.logr.size();
   uint32_t log_ns = 0;
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
     const int tile = gl_tile(lr);
-    GlPassFn fn = p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile) : gl_fn_e<153>(lr, log_ns == 0, tile);
+    const bool persist = getenv("PBF_NTT_PERSIST") != nullptr;  // A/B: pipelined persistent kernel
+    GlPassFn fn =
+        p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile, persist) : gl_fn_e<153>(lr, log_ns == 0, tile, persist);
     if (!fn) return fail(1, "no Goldilocks pass kernel for this radix");
     const uint64_t W = (uint64_t)tile >> lr;
     if ((p.n >> lr) % W) return fail(1, "transform too small for the pass tile");
@@ -429,7 +451,8 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
     }
-    hipLaunchKernelGGL(fn, dim3((uint32_t)tiles), dim3(tile / 16), 0, stream, a);
+    const uint32_t grid = persist ? persistent_grid((const void*)fn, tile / 16, tiles) : (uint32_t)tiles;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), 0, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;
   }
@@ -493,7 +516,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     const int nt = cfg.nt ? cfg.nt : (W << lr) >> cfg.lq;
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
     if (blocks > 0x7fffffffull) return fail(1, "batch too large");
-    const uint32_t grid = cfg.db ? persistent_grid(fn, nt, blocks) : (uint32_t)blocks;  // modes 1, 2: persistent
+    const uint32_t grid = cfg.db ? persistent_grid((const void*)fn, nt, blocks) : (uint32_t)blocks;  // modes 1, 2: persistent
     a.xcd_kmajor = (!cfg.db && log_ns > 0 && batch > 1 && grid % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(nt), 0, stream, a);
     PBF_HIP(hipGetLastError());

@@ -4,11 +4,11 @@ Writes profiles/<tag>/ntt_kernel_stats.csv (rocprofv3 --stats), profiles/<tag>/p
 (per-kernel averages of every counter) and profiles/pmc_ntt_2p<log_n>_b<batch>.json, the HBM
 traffic per bench step that bench.py reports as roofline.traffic.
 
-Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes
-of a coalesced streaming read, so FETCH bytes = 2 * FETCH_SIZE KiB * 1024; WRITE_SIZE is
-taken as is. The NTT pass loads 8 B per lane in 128-B runs (a width the guide leaves
-uncalibrated); with the factor 2 the fetch is 1.13x the pass input ('fetch_vs_input'), the
-excess being consistent with L2 misses on pass 2's 8 MiB [r][k] twiddle table.
+Calibration (MI355X_MICROARCH.md, HBM section: FETCH_SIZE is exact only for 16-B-per-lane
+streaming reads, "calibrate on a known byte count in your own access pattern"): the same run
+profiles scripts/ubench/tile_copy, whose kernels move a known 256 MiB in the NTT pass's own
+access patterns (8 B per lane, 64-B runs rows n/R apart); the ratio known bytes / counter
+bytes of the matching tile_copy kernel converts the NTT kernels' FETCH_SIZE / WRITE_SIZE.
 """
 import collections
 import csv
@@ -20,30 +20,66 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag="r01", log_n=20, batch=32, passes=2):
+KNOWN = (1 << 20) * 32 * 8  # bytes each tile_copy kernel reads and writes
+CAL_KERNEL = "k_tile<3, 8, 1>"  # strided 64-B runs on both sides, 8 B per lane
+
+
+def counters(path):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        out[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def calibration(src):
+    """bytes per counted KiB for reads and writes, from the tile_copy runs (None if absent)."""
+    cal = {}
+    for f, cname in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
+        path = os.path.join(src, f + "_counter_collection.csv")
+        if not os.path.exists(path):
+            return None
+        c = counters(path)
+        ks = [k for k in c if CAL_KERNEL in k]
+        assert len(ks) == 1, ks
+        v = c[ks[0]][cname]
+        cal[cname] = KNOWN / (sum(v) / len(v) * 1024)
+        cal[cname + "_all"] = {k: KNOWN / (sum(x) / len(x) * 1024) for k, d in c.items() for n, x in d.items()
+                               if n == cname}
+    return cal
+
+
+def main(tag="r01", log_n=20, batch=32):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace_kernel_stats.csv"), os.path.join(dst, f"ntt2p{log_n}_b{batch}_kernel_stats.csv"))
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in ("fetch", "write", "sq"):
-        for r in csv.DictReader(open(os.path.join(src, f + "_counter_collection.csv"))):
-            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in counters(os.path.join(src, f + "_counter_collection.csv")).items():
+            for c, v in d.items():
+                agg[k][c] += v
     summ = {k: {c: {"dispatches": len(v), "mean": sum(v) / len(v)} for c, v in d.items()} for k, d in agg.items()}
+    cal = calibration(src)
+    summ["_calibration"] = cal
     with open(os.path.join(dst, "pmc_counters.json"), "w") as fh:
         json.dump(summ, fh, indent=1)
-    ntt = [k for k in summ if "ntt_pass_kernel" in k]
-    assert len(ntt) == 1, ntt
-    c = summ[ntt[0]]
-    fetch = 2 * c["FETCH_SIZE"]["mean"] * 1024
-    write = c["WRITE_SIZE"]["mean"] * 1024
+    # one dispatch of each pass kernel per step
+    ntt = sorted(k for k in summ if "ntt_gl_pass_kernel" in k or "ntt_pass_kernel" in k)
+    assert ntt, list(summ)
+    fk = cal["FETCH_SIZE"] if cal else 2.0 * 1024  # uncalibrated: the guide's 16-B-lane factor
+    wk = cal["WRITE_SIZE"] if cal else 1024
+    per = {k: {"fetch_bytes": summ[k]["FETCH_SIZE"]["mean"] * fk, "write_bytes": summ[k]["WRITE_SIZE"]["mean"] * wk}
+           for k in ntt}
     data = (1 << log_n) * batch * 8
-    out = {"kernel": ntt[0], "log_n": log_n, "batch": batch, "passes_per_step": passes,
-           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
-           "fetch_vs_input": fetch / data, "write_vs_output": write / data,
-           "hbm_bytes_per_step": passes * (fetch + write),
-           "algorithmic_bytes_per_step": passes * 2 * data,
-           "source": f"profiles/{tag}/pmc_counters.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"}
+    hbm = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
+    out = {"kernels": per, "log_n": log_n, "batch": batch, "passes_per_step": len(ntt),
+           "fetch_vs_input": {k: v["fetch_bytes"] / data for k, v in per.items()},
+           "write_vs_output": {k: v["write_bytes"] / data for k, v in per.items()},
+           "calibration_bytes_per_kib": {"FETCH_SIZE": fk, "WRITE_SIZE": wk, "kernel": CAL_KERNEL if cal else None},
+           "hbm_bytes_per_step": hbm,
+           "algorithmic_bytes_per_step": 2 * data,
+           "source": f"profiles/{tag}/pmc_counters.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
+                     f"passes; calibrated on scripts/ubench/tile_copy)"}
     with open(os.path.join(ROOT, "profiles", f"pmc_ntt_2p{log_n}_b{batch}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
