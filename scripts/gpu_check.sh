@@ -16,7 +16,7 @@ step bench-2p20
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-budget 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 step bench-2p24
-for P in default 12,12 8,8,8; do
+for P in default; do
   if [ $P = default ]; then unset PBF_NTT_PASSES; else export PBF_NTT_PASSES=$P; fi
   timeout -k 10 300 python bench.py --log-n 24 --batch 2 --steps 20 --warmup 3 --no-cpu > gpurun_out/bench24_$P.json 2>> gpurun_out/bench.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/bench24_$P.json'));print('$P', d['ms_per_step'], d['roofline']['achieved'], d['roofline']['frac'])"

@@ -32,7 +32,7 @@ def counters(path):
 
 
 def calibration(src):
-    """bytes per counted KiB for reads and writes, from the tile_copy runs (None if absent)."""
+    """bytes per counter unit for reads and writes, from the tile_copy runs (None if absent)."""
     cal = {}
     for f, cname in (("calib_fetch", "FETCH_SIZE"), ("calib_write", "WRITE_SIZE")):
         path = os.path.join(src, f + "_counter_collection.csv")
@@ -42,8 +42,8 @@ def calibration(src):
         ks = [k for k in c if CAL_KERNEL in k]
         assert len(ks) == 1, ks
         v = c[ks[0]][cname]
-        cal[cname] = KNOWN / (sum(v) / len(v) * 1024)
-        cal[cname + "_all"] = {k: KNOWN / (sum(x) / len(x) * 1024) for k, d in c.items() for n, x in d.items()
+        cal[cname] = KNOWN / (sum(v) / len(v))  # bytes per counted unit
+        cal[cname + "_all"] = {k: KNOWN / (sum(x) / len(x)) for k, d in c.items() for n, x in d.items()
                                if n == cname}
     return cal
 
