@@ -4,17 +4,30 @@
 //
 //   e(P, Q) = ( f_{6u+2,Q}(P) * l_{T,pi(Q)}(P) * l_{T',-pi^2(Q)}(P) )^((q^12-1)/r)
 //
-// Tower: Fq2 = Fq[u]/(u^2+1), Fq6 = Fq2[v]/(v^3-xi), xi = 9+u, Fq12 = Fq6[w]/(w^2-v);
-// G2 on the D-type twist y^2 = x^3 + 3/xi. Miller loop over the bits of 6u+2 with affine
-// T (one Fq2 inversion per step), lines l = yP - lam*xP*w + (lam*xT - yT)*v*w (vertical
-// parts dropped: they lie in Fq6 and die in the final exponentiation). Final
-// exponentiation: easy part f^(q^6-1) (conjugate / inverse) and f^(q^2+1) (Frobenius
-// constants), hard part a plain square-and-multiply by (q^4-q^2+1)/r, so the value is
-// exactly the reduced pairing of oracle/bn254_pairing.py (no exponent multiple).
+// Tower: Fq2 = Fq[u]/(u^2+1), xi = 9+u, Fq12 = Fq2[w]/(w^6 - xi) (= Fq6[w]/(w^2-v) with
+// v = w^2, Fq6 = Fq2[v]/(v^3-xi)); G2 on the D-type twist y^2 = x^3 + 3/xi.
 //
-// One thread per pairing (pairings are few: two per KZG check, batched across proofs —
-// SURVEY.md §8e "replicas only"). Fq elements in Montgomery form inside kernels; the
-// ABI carries canonical little-endian limbs (GT: 12 Fq in tower order).
+// One wave (one 64-thread workgroup) per pairing, Fq12 values in LDS in the flat w-basis
+// g[k] = coefficient of w^k. A product of two Fq12 is 36 Fq2 products, one per lane,
+// and 6 lanes summing them (x xi for the wrapped terms): the latency of one Fq2 product
+// instead of 54 dependent Fq products on one thread. T runs in homogeneous projective
+// coordinates (no inversions in the Miller loop); its formulas are split into stages of
+// independent Fq2 products, one per lane. Lines are scaled by Fq2 factors
+// (doubling: 2 Y Z^2, addition: xQ Z - X), which the final exponentiation removes
+// ((q^12-1)/r is a multiple of q^2-1), so every pairing value is the reduced pairing
+// itself, bit-identical to oracle/bn254_pairing.py.
+//
+// Final exponentiation: easy part f^(q^6-1) (conjugate times inverse; one Fq inversion
+// by binary extended Euclid), f^(q^2+1) (Frobenius); hard part EXACTLY
+// (q^4-q^2+1)/r = l0 + l1 q + l2 q^2 + q^3 with l2 = 6u^2+1, l1 = -36u^3-18u^2-12u+1,
+// l0 = -36u^3-30u^2-18u-2 (an identity of integers, checked in
+// tests/test_bn254_pairing_oracle.py): three exponentiations by u, a few small powers,
+// Frobenius maps, and conjugation for the negative coefficients (the input of the hard
+// part lies in the cyclotomic subgroup, where inversion is conjugation).
+//
+// Fq elements in Montgomery form inside kernels; the ABI carries canonical little-endian
+// limbs (GT: 12 Fq in tower order c0.a0, c0.a1, c0.a2, c1.a0, c1.a1, c1.a2 = w^0, w^2,
+// w^4, w^1, w^3, w^5).
 #include <vector>
 #include "../../include/pbf.h"
 #include "ec_bn254.hpp"
@@ -23,25 +36,31 @@
 namespace pbf {
 
 // ---------------------------------------------------------------- constants
-// Generated from q alone by scripts/gen_pairing_constants.py (canonical, little-endian):
-//   GAMMA_X = xi^((q-1)/3), GAMMA_Y = xi^((q-1)/2) (Fq2: twist Frobenius)
-//   FROB2[k] = xi^(k(q^2-1)/6) (in Fq), k = 1..5 (Fq12 q^2-power Frobenius on w^k)
-//   HARD = (q^4 - q^2 + 1)/r (761 bits), ATE = 6u+2
+// Generated from q and u alone by scripts/gen_pairing_constants.py (canonical, little-endian):
+//   FROB1[k] = xi^(k(q-1)/6) (Fq2, k = 0..5): w^k -> w^(kq) = FROB1[k] w^k
+//   GX = FROB1[2], GY = FROB1[3] (twist Frobenius pi(x, y) = (conj(x) GX, conj(y) GY))
+//   FROB2[k] = xi^(k(q^2-1)/6) (in Fq), R3 = 2^768 mod q, ATE = 6u+2, BN_U = u
 struct PairingConsts {
-  U256 gx0, gx1, gy0, gy1;  // Montgomery
+  U256 frob1[6][2];         // Montgomery
   U256 frob2[6];            // Montgomery
-  U256 one, xi_unused;
-  uint64_t hard[12];
+  U256 one;                 // Montgomery 1
+  U256 r3;                  // plain 2^768 mod q (binary-Euclid inverse -> Montgomery)
   uint64_t ate;             // low 64 bits of 6u+2 (bit 64 is set too)
-  uint64_t qm2[4];          // q - 2 (Fermat inverse)
 };
 
-static const uint64_t K_GX[2][4] = {
-    {0x99e39557176f553dull, 0xb78cc310c2c3330cull, 0x4c0bec3cf559b143ull, 0x2fb347984f7911f7ull},
-    {0x1665d51c640fcba2ull, 0x32ae2a1d0b7c9dceull, 0x4ba4cc8bd75a0794ull, 0x16c9e55061ebae20ull}};
-static const uint64_t K_GY[2][4] = {
-    {0xdc54014671a0135aull, 0xdbaae0eda9c95998ull, 0xdc5ec698b6e2f9b9ull, 0x063cf305489af5dcull},
-    {0x82d37f632623b0e3ull, 0x21807dc98fa25bd2ull, 0x0704b5a7ec796f2bull, 0x07c03cbcac41049aull}};
+static const uint64_t K_FROB1[6][2][4] = {
+    {{0x0000000000000001ull, 0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull},
+     {0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull, 0x0000000000000000ull}},
+    {{0xd60b35dadcc9e470ull, 0x5c521e08292f2176ull, 0xe8b99fdd76e68b60ull, 0x1284b71c2865a7dfull},
+     {0xca5cf05f80f362acull, 0x747992778eeec7e5ull, 0xa6327cfe12150b8eull, 0x246996f3b4fae7e6ull}},
+    {{0x99e39557176f553dull, 0xb78cc310c2c3330cull, 0x4c0bec3cf559b143ull, 0x2fb347984f7911f7ull},
+     {0x1665d51c640fcba2ull, 0x32ae2a1d0b7c9dceull, 0x4ba4cc8bd75a0794ull, 0x16c9e55061ebae20ull}},
+    {{0xdc54014671a0135aull, 0xdbaae0eda9c95998ull, 0xdc5ec698b6e2f9b9ull, 0x063cf305489af5dcull},
+     {0x82d37f632623b0e3ull, 0x21807dc98fa25bd2ull, 0x0704b5a7ec796f2bull, 0x07c03cbcac41049aull}},
+    {{0x848a1f55921ea762ull, 0xd33365f7be94ec72ull, 0x80f3c0b75a181e84ull, 0x05b54f5e64eea801ull},
+     {0xc13b4711cd2b8126ull, 0x3685d2ea1bdec763ull, 0x9f3a80b03b0b1c92ull, 0x2c145edbe7fd8aeeull}},
+    {{0x2ea2c810eab7692full, 0x425c459b55aa1bd3ull, 0xe93a3661a4353ff4ull, 0x0183c1e74f798649ull},
+     {0x24c6b8ee6e0c2c4bull, 0xb080cb99678e2ac0ull, 0xa27fb246c7729f7dull, 0x12acf2ca76fd0675ull}}};
 static const uint64_t K_FROB2[6][4] = {
     {0x0000000000000001ull, 0, 0, 0},
     {0xe4bd44e5607cfd49ull, 0xc28f069fbb966e3dull, 0x5e6dd9e7e0acccb0ull, 0x30644e72e131a029ull},
@@ -49,180 +68,369 @@ static const uint64_t K_FROB2[6][4] = {
     {0x3c208c16d87cfd46ull, 0x97816a916871ca8dull, 0xb85045b68181585dull, 0x30644e72e131a029ull},
     {0x5763473177fffffeull, 0xd4f263f1acdb5c4full, 0x59e26bcea0d48bacull, 0x0000000000000000ull},
     {0x5763473177ffffffull, 0xd4f263f1acdb5c4full, 0x59e26bcea0d48bacull, 0x0000000000000000ull}};
-static const uint64_t K_HARD[12] = {0xe81bb482ccdf42b1ull, 0x5abf5cc4f49c36d4ull, 0xf1154e7e1da014fdull,
-                                    0xdcc7b44c87cdbacfull, 0xaaa441e3954bcf8aull, 0x6b887d56d5095f23ull,
-                                    0x79581e16f3fd90c6ull, 0x3b1b1355d189227dull, 0x4e529a5861876f6bull,
-                                    0x6c0eb522d5b12278ull, 0x331ec15183177fafull, 0x01baaa710b0759adull};
+static const uint64_t K_R3[4] = {0xb1cd6dafda1530dfull, 0x62f210e6a7283db6ull, 0xef7f0b0c0ada0afbull,
+                                 0x20fd6e902d592544ull};
 static const uint64_t K_ATE_LO = 0x9d797039be763ba8ull;  // 6u+2 = 2^64 + K_ATE_LO
+static const uint64_t K_BN_U = 0x44e992b44a6909f1ull;    // u = 4965661367192848881
 
-// ---------------------------------------------------------------- tower arithmetic
+// ---------------------------------------------------------------- Fq / Fq2 (one lane)
 struct Fq2 {
   U256 c0, c1;
 };
-struct Fq6 {
-  Fq2 a0, a1, a2;
-};
-struct Fq12 {
-  Fq6 c0, c1;
-};
 
-__device__ inline Fq2 f2_add(const Fq2& a, const Fq2& b) { return {Fq::add(a.c0, b.c0), Fq::add(a.c1, b.c1)}; }
-__device__ inline Fq2 f2_sub(const Fq2& a, const Fq2& b) { return {Fq::sub(a.c0, b.c0), Fq::sub(a.c1, b.c1)}; }
-__device__ inline Fq2 f2_neg(const Fq2& a) { return {Fq::sub(u256_zero(), a.c0), Fq::sub(u256_zero(), a.c1)}; }
-__device__ inline Fq2 f2_dbl(const Fq2& a) { return f2_add(a, a); }
-__device__ inline Fq2 f2_conj(const Fq2& a) { return {a.c0, Fq::sub(u256_zero(), a.c1)}; }
-__device__ inline Fq2 f2_muls(const Fq2& a, const U256& s) { return {Fq::mul(a.c0, s), Fq::mul(a.c1, s)}; }
-__device__ __noinline__ Fq2 f2_mul(const Fq2& a, const Fq2& b) {
+__device__ __forceinline__ Fq2 f2_add(const Fq2& a, const Fq2& b) { return {Fq::add(a.c0, b.c0), Fq::add(a.c1, b.c1)}; }
+__device__ __forceinline__ Fq2 f2_sub(const Fq2& a, const Fq2& b) { return {Fq::sub(a.c0, b.c0), Fq::sub(a.c1, b.c1)}; }
+__device__ __forceinline__ Fq2 f2_neg(const Fq2& a) { return {Fq::sub(u256_zero(), a.c0), Fq::sub(u256_zero(), a.c1)}; }
+__device__ __forceinline__ Fq2 f2_dbl(const Fq2& a) { return f2_add(a, a); }
+__device__ __forceinline__ Fq2 f2_conj(const Fq2& a) { return {a.c0, Fq::sub(u256_zero(), a.c1)}; }
+__device__ __forceinline__ Fq2 f2_muls(const Fq2& a, const U256& s) { return {Fq::mul(a.c0, s), Fq::mul(a.c1, s)}; }
+__device__ __forceinline__ Fq2 f2_mul(const Fq2& a, const Fq2& b) {
   // Karatsuba: (a0 b0 - a1 b1) + ((a0 + a1)(b0 + b1) - a0 b0 - a1 b1) u
   const U256 t0 = Fq::mul(a.c0, b.c0), t1 = Fq::mul(a.c1, b.c1);
   const U256 t2 = Fq::mul(Fq::add(a.c0, a.c1), Fq::add(b.c0, b.c1));
   return {Fq::sub(t0, t1), Fq::sub(Fq::sub(t2, t0), t1)};
 }
-__device__ inline Fq2 f2_sqr(const Fq2& a) { return f2_mul(a, a); }
+__device__ __forceinline__ Fq2 f2_sqr(const Fq2& a) {
+  // (a0 + a1)(a0 - a1) + 2 a0 a1 u
+  const U256 t = Fq::mul(a.c0, a.c1);
+  return {Fq::mul(Fq::add(a.c0, a.c1), Fq::sub(a.c0, a.c1)), Fq::add(t, t)};
+}
 // (9 + u)(a0 + a1 u) = (9 a0 - a1) + (a0 + 9 a1) u
-__device__ inline Fq2 f2_mul_xi(const Fq2& a) {
+__device__ __forceinline__ Fq2 f2_mul_xi(const Fq2& a) {
   auto nine = [](const U256& x) {
     const U256 x2 = Fq::add(x, x), x4 = Fq::add(x2, x2), x8 = Fq::add(x4, x4);
     return Fq::add(x8, x);
   };
   return {Fq::sub(nine(a.c0), a.c1), Fq::add(a.c0, nine(a.c1))};
 }
-__device__ bool f2_is_zero(const Fq2& a) { return Fq::is_zero(a.c0) && Fq::is_zero(a.c1); }
-__device__ bool f2_eq(const Fq2& a, const Fq2& b) { return Fq::eq(a.c0, b.c0) && Fq::eq(a.c1, b.c1); }
+__device__ __forceinline__ bool f2_eq(const Fq2& a, const Fq2& b) { return Fq::eq(a.c0, b.c0) && Fq::eq(a.c1, b.c1); }
+__device__ __forceinline__ bool f2_is_zero(const Fq2& a) { return Fq::is_zero(a.c0) && Fq::is_zero(a.c1); }
 
-__device__ __noinline__ U256 fq_pow(U256 a, const uint64_t* e, int words) {
-  U256 r = G1::one_m();
-  for (int i = words * 64 - 1; i >= 0; --i) {
-    r = Fq::mul(r, r);
-    if ((e[i >> 6] >> (i & 63)) & 1) r = Fq::mul(r, a);
+__device__ __forceinline__ bool u256_is_one(const U256& a) {
+  uint32_t o = a.w[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) o |= a.w[i];
+  return o == 0;
+}
+__device__ __forceinline__ bool u256_geq(const U256& a, const U256& b) {
+#pragma unroll
+  for (int i = 7; i >= 0; --i)
+    if (a.w[i] != b.w[i]) return a.w[i] > b.w[i];
+  return true;
+}
+__device__ __forceinline__ void u256_shr1(U256& a) {
+#pragma unroll
+  for (int i = 0; i < 7; ++i) a.w[i] = (a.w[i] >> 1) | (a.w[i + 1] << 31);
+  a.w[7] >>= 1;
+}
+__device__ __forceinline__ U256 u256_sub_raw(const U256& a, const U256& b) {
+  U256 d;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t t = (uint64_t)a.w[i] - b.w[i] - borrow;
+    d.w[i] = (uint32_t)t;
+    borrow = (t >> 63) & 1;
   }
-  return r;
+  return d;
 }
-__device__ __noinline__ U256 fq_inv(const U256& a, const PairingConsts& k) { return fq_pow(a, k.qm2, 4); }
-__device__ __noinline__ Fq2 f2_inv(const Fq2& a, const PairingConsts& k) {
-  const U256 n = Fq::add(Fq::mul(a.c0, a.c0), Fq::mul(a.c1, a.c1));
-  const U256 ni = fq_inv(n, k);
-  return {Fq::mul(a.c0, ni), Fq::sub(u256_zero(), Fq::mul(a.c1, ni))};
-}
-
-__device__ inline Fq6 f6_add(const Fq6& a, const Fq6& b) {
-  return {f2_add(a.a0, b.a0), f2_add(a.a1, b.a1), f2_add(a.a2, b.a2)};
-}
-__device__ inline Fq6 f6_sub(const Fq6& a, const Fq6& b) {
-  return {f2_sub(a.a0, b.a0), f2_sub(a.a1, b.a1), f2_sub(a.a2, b.a2)};
-}
-__device__ inline Fq6 f6_neg(const Fq6& a) { return {f2_neg(a.a0), f2_neg(a.a1), f2_neg(a.a2)}; }
-__device__ inline Fq6 f6_mul_v(const Fq6& a) { return {f2_mul_xi(a.a2), a.a0, a.a1}; }
-__device__ __noinline__ Fq6 f6_mul(const Fq6& a, const Fq6& b) {
-  // Karatsuba over Fq2 (v^3 = xi)
-  const Fq2 t0 = f2_mul(a.a0, b.a0), t1 = f2_mul(a.a1, b.a1), t2 = f2_mul(a.a2, b.a2);
-  const Fq2 m12 = f2_sub(f2_sub(f2_mul(f2_add(a.a1, a.a2), f2_add(b.a1, b.a2)), t1), t2);
-  const Fq2 m01 = f2_sub(f2_sub(f2_mul(f2_add(a.a0, a.a1), f2_add(b.a0, b.a1)), t0), t1);
-  const Fq2 m02 = f2_sub(f2_sub(f2_mul(f2_add(a.a0, a.a2), f2_add(b.a0, b.a2)), t0), t2);
-  return {f2_add(t0, f2_mul_xi(m12)), f2_add(m01, f2_mul_xi(t2)), f2_add(m02, t1)};
-}
-__device__ __noinline__ Fq6 f6_inv(const Fq6& a, const PairingConsts& k) {
-  const Fq2 t0 = f2_sub(f2_sqr(a.a0), f2_mul_xi(f2_mul(a.a1, a.a2)));
-  const Fq2 t1 = f2_sub(f2_mul_xi(f2_sqr(a.a2)), f2_mul(a.a0, a.a1));
-  const Fq2 t2 = f2_sub(f2_sqr(a.a1), f2_mul(a.a0, a.a2));
-  const Fq2 n = f2_add(f2_mul(a.a0, t0), f2_mul_xi(f2_add(f2_mul(a.a2, t1), f2_mul(a.a1, t2))));
-  const Fq2 ni = f2_inv(n, k);
-  return {f2_mul(t0, ni), f2_mul(t1, ni), f2_mul(t2, ni)};
-}
-
-__device__ __noinline__ Fq12 f12_mul(const Fq12& a, const Fq12& b) {
-  const Fq6 t0 = f6_mul(a.c0, b.c0), t1 = f6_mul(a.c1, b.c1);
-  const Fq6 m = f6_sub(f6_sub(f6_mul(f6_add(a.c0, a.c1), f6_add(b.c0, b.c1)), t0), t1);
-  return {f6_add(t0, f6_mul_v(t1)), m};
-}
-__device__ inline Fq12 f12_sqr(const Fq12& a) { return f12_mul(a, a); }
-__device__ inline Fq12 f12_conj(const Fq12& a) { return {a.c0, f6_neg(a.c1)}; }
-__device__ __noinline__ Fq12 f12_inv(const Fq12& a, const PairingConsts& k) {
-  const Fq6 n = f6_sub(f6_mul(a.c0, a.c0), f6_mul_v(f6_mul(a.c1, a.c1)));
-  const Fq6 ni = f6_inv(n, k);
-  return {f6_mul(a.c0, ni), f6_neg(f6_mul(a.c1, ni))};
-}
-// x^(q^2): coefficient of w^k (c0: k = 0, 2, 4; c1: k = 1, 3, 5) times xi^(k(q^2-1)/6)
-__device__ Fq12 f12_frob2(const Fq12& a, const PairingConsts& k) {
-  Fq12 r;
-  r.c0.a0 = a.c0.a0;
-  r.c0.a1 = f2_muls(a.c0.a1, k.frob2[2]);
-  r.c0.a2 = f2_muls(a.c0.a2, k.frob2[4]);
-  r.c1.a0 = f2_muls(a.c1.a0, k.frob2[1]);
-  r.c1.a1 = f2_muls(a.c1.a1, k.frob2[3]);
-  r.c1.a2 = f2_muls(a.c1.a2, k.frob2[5]);
-  return r;
-}
-__device__ Fq12 f12_one(const PairingConsts& k) {
-  Fq12 r;
-  const U256 z = u256_zero();
-  r.c0.a0 = {k.one, z};
-  r.c0.a1 = r.c0.a2 = r.c1.a0 = r.c1.a1 = r.c1.a2 = Fq2{z, z};
-  return r;
-}
-
-__device__ __noinline__ Fq12 final_exp(const Fq12& f, const PairingConsts& k) {
-  Fq12 f1 = f12_mul(f12_conj(f), f12_inv(f, k));   // f^(q^6 - 1)
-  Fq12 f2 = f12_mul(f12_frob2(f1, k), f1);          // ^(q^2 + 1)
-  Fq12 r = f12_one(k);                              // ^((q^4 - q^2 + 1)/r)
-  for (int i = 12 * 64 - 1; i >= 0; --i) {
-    if (i >= 761) continue;
-    r = f12_sqr(r);
-    if ((k.hard[i >> 6] >> (i & 63)) & 1) r = f12_mul(r, f2);
-  }
-  return r;
-}
-
-// ---------------------------------------------------------------- Miller loop
-struct G2A {
-  Fq2 x, y;
-};
-
-// f *= (yP) + (-lam xP) w + (lam xT - yT) v w
-__device__ __noinline__ Fq12 mul_line(const Fq12& f, const Fq2& lam, const G2A& t, const U256& xp, const U256& yp) {
-  Fq12 l;
-  const U256 z = u256_zero();
-  l.c0.a0 = {yp, z};
-  l.c0.a1 = l.c0.a2 = Fq2{z, z};
-  l.c1.a0 = f2_neg(f2_muls(lam, xp));
-  l.c1.a1 = f2_sub(f2_mul(lam, t.x), t.y);
-  l.c1.a2 = Fq2{z, z};
-  return f12_mul(f, l);
-}
-
-__device__ __noinline__ Fq12 miller_loop(const U256& xp, const U256& yp, const G2A& q, const PairingConsts& k) {
-  Fq12 f = f12_one(k);
-  G2A t = q;
-  const U256 three = Fq::add(Fq::add(k.one, k.one), k.one);
-  // bits of 6u+2 = 2^64 + ATE_LO below the leading one (bit 64)
-  for (int i = 63; i >= 0; --i) {
-    // doubling step: lam = 3 xT^2 / (2 yT)
-    Fq2 lam = f2_mul(f2_muls(f2_sqr(t.x), three), f2_inv(f2_dbl(t.y), k));
-    f = mul_line(f12_sqr(f), lam, t, xp, yp);
-    Fq2 x3 = f2_sub(f2_sqr(lam), f2_dbl(t.x));
-    t.y = f2_sub(f2_mul(lam, f2_sub(t.x, x3)), t.y);
-    t.x = x3;
-    if ((k.ate >> i) & 1) {
-      lam = f2_mul(f2_sub(q.y, t.y), f2_inv(f2_sub(q.x, t.x), k));
-      f = mul_line(f, lam, t, xp, yp);
-      x3 = f2_sub(f2_sub(f2_sqr(lam), t.x), q.x);
-      t.y = f2_sub(f2_mul(lam, f2_sub(t.x, x3)), t.y);
-      t.x = x3;
+// x / 2 mod q for canonical x (x odd: (x + q) / 2 < q, no overflow since q < 2^254)
+__device__ __forceinline__ void fq_half(U256& x) {
+  if (x.w[0] & 1) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t t = (uint64_t)x.w[i] + Bn254FqParams::P[i] + c;
+      x.w[i] = (uint32_t)t;
+      c = t >> 32;
     }
   }
-  // Q1 = pi(Q), Q2 = -pi^2(Q)
-  const Fq2 gx{k.gx0, k.gx1}, gy{k.gy0, k.gy1};
-  G2A q1{f2_mul(f2_conj(q.x), gx), f2_mul(f2_conj(q.y), gy)};
-  G2A q2{f2_mul(f2_conj(q1.x), gx), f2_neg(f2_mul(f2_conj(q1.y), gy))};
-  for (int s = 0; s < 2; ++s) {
-    const G2A& qq = s ? q2 : q1;
-    const Fq2 lam = f2_mul(f2_sub(qq.y, t.y), f2_inv(f2_sub(qq.x, t.x), k));
-    f = mul_line(f, lam, t, xp, yp);
-    const Fq2 x3 = f2_sub(f2_sub(f2_sqr(lam), t.x), qq.x);
-    t.y = f2_sub(f2_mul(lam, f2_sub(t.x, x3)), t.y);
-    t.x = x3;
+  u256_shr1(x);
+}
+// Montgomery inverse (aR)^-1 -> a^-1 R: binary extended Euclid on the representative, then
+// one Montgomery product with R^3 ((aR)^-1 R^3 R^-1 = a^-1 R). a != 0.
+__device__ __noinline__ U256 fq_inv(const U256& am, const PairingConsts& k) {
+  U256 u = am, v, x1 = u256_zero(), x2 = u256_zero();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v.w[i] = Bn254FqParams::P[i];
+  x1.w[0] = 1;
+  if (Fq::is_zero(am)) return u256_zero();  // no inverse (callers never pass 0)
+  // gcd(a, q) = 1: each round removes >= 1 bit from u or v, so <= 2 * 256 rounds; the cap
+  // only guards the exit
+  for (int round = 0; round < 1024 && !u256_is_one(u) && !u256_is_one(v); ++round) {
+    while (!(u.w[0] & 1)) { u256_shr1(u); fq_half(x1); }
+    while (!(v.w[0] & 1)) { u256_shr1(v); fq_half(x2); }
+    if (u256_geq(u, v)) {
+      u = u256_sub_raw(u, v);
+      x1 = Fq::sub(x1, x2);
+    } else {
+      v = u256_sub_raw(v, u);
+      x2 = Fq::sub(x2, x1);
+    }
   }
-  return f;
+  return Fq::mul(u256_is_one(u) ? x1 : x2, k.r3);
+}
+__device__ __forceinline__ Fq2 f2_inv(const Fq2& a, const PairingConsts& k) {
+  const U256 ni = fq_inv(Fq::add(Fq::mul(a.c0, a.c0), Fq::mul(a.c1, a.c1)), k);
+  return {Fq::mul(a.c0, ni), Fq::sub(u256_zero(), Fq::mul(a.c1, ni))};
+}
+__device__ __forceinline__ Fq2 kfrob1(const PairingConsts& k, int i) { return {k.frob1[i][0], k.frob1[i][1]}; }
+
+// ---------------------------------------------------------------- wave-cooperative Fq12
+// Every function below is called by all 64 lanes of the (single-wave) workgroup and ends
+// with a barrier; operands and results are flat Fq12 (6 Fq2) in LDS and may alias.
+struct PairLds {
+  Fq2 prod[36];    // partial products
+  Fq2 reg[14][6];  // Fq12 registers
+  Fq2 line[3];     // sparse line: w^0, w^1, w^3 coefficients
+  Fq2 tp[16];      // T-step scratch
+  Fq2 T[3];        // X, Y, Z
+  Fq2 Qa[3][2];    // Q, pi(Q), -pi^2(Q) affine
+  Fq2 frob1[6];    // the lane-indexed constants (a lane-indexed kernel argument would be
+  U256 frob2[6];   // copied to scratch)
+};
+
+// constants -> LDS with compile-time indices
+__device__ void load_consts(const PairingConsts& k, PairLds& L, int lane) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (lane == i) {
+      L.frob1[i] = Fq2{k.frob1[i][0], k.frob1[i][1]};
+      L.frob2[i] = k.frob2[i];
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+// dst = x * y
+__device__ void w12_mul(Fq2* dst, const Fq2* x, const Fq2* y, PairLds& L, int lane) {
+  if (lane < 36) {
+    const int i = lane / 6, j = lane - 6 * (lane / 6);
+    Fq2 p = (x == y && i == j) ? f2_sqr(x[i]) : f2_mul(x[i], y[j]);
+    if (i + j >= 6) p = f2_mul_xi(p);
+    L.prod[lane] = p;
+  }
+  wsync();
+  if (lane < 6) {
+    Fq2 s = L.prod[lane];  // i = 0, j = lane
+#pragma unroll
+    for (int i = 1; i < 6; ++i) {
+      const int j = lane - i < 0 ? lane - i + 6 : lane - i;
+      s = f2_add(s, L.prod[6 * i + j]);
+    }
+    dst[lane] = s;
+  }
+  wsync();
+}
+// f *= line (coefficients at w^0, w^1, w^3)
+__device__ void w12_mul_line(Fq2* f, PairLds& L, int lane) {
+  if (lane < 18) {
+    const int i = lane / 3, jj = lane - 3 * (lane / 3);
+    const int j = jj == 2 ? 3 : jj;
+    Fq2 p = f2_mul(f[i], L.line[jj]);
+    if (i + j >= 6) p = f2_mul_xi(p);
+    L.prod[6 * i + j] = p;
+  }
+  wsync();
+  if (lane < 6) {
+    Fq2 s;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+      const int j = jj == 2 ? 3 : jj;
+      const int i = lane - j < 0 ? lane - j + 6 : lane - j;
+      s = jj == 0 ? L.prod[6 * i + j] : f2_add(s, L.prod[6 * i + j]);
+    }
+    f[lane] = s;
+  }
+  wsync();
+}
+__device__ void w12_copy(Fq2* dst, const Fq2* x, int lane) {
+  if (lane < 6) dst[lane] = x[lane];
+  wsync();
+}
+// x^(q^6): w -> -w
+__device__ void w12_conj(Fq2* dst, const Fq2* x, int lane) {
+  if (lane < 6) dst[lane] = (lane & 1) ? f2_neg(x[lane]) : x[lane];
+  wsync();
+}
+// x^q: g_k -> conj(g_k) FROB1[k]
+__device__ void w12_frob1(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
+  if (lane < 6) dst[lane] = lane == 0 ? f2_conj(x[0]) : f2_mul(f2_conj(x[lane]), L.frob1[lane]);
+  wsync();
+}
+// x^(q^2): g_k -> g_k FROB2[k]
+__device__ void w12_frob2(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
+  if (lane < 6) dst[lane] = lane == 0 ? x[0] : f2_muls(x[lane], L.frob2[lane]);
+  wsync();
+}
+__device__ void w12_one(Fq2* dst, const PairingConsts& k, int lane) {
+  if (lane < 6) dst[lane] = Fq2{lane == 0 ? k.one : u256_zero(), u256_zero()};
+  wsync();
+}
+// dst = x^-1: x * conj(x) = N lies in Fq6 = span(w^0, w^2, w^4); N^-1 on lane 0 (Fq6
+// inverse over Fq2, one Fq inversion); dst = conj(x) * N^-1
+__device__ void w12_inv(Fq2* dst, const Fq2* x, Fq2* tmp, Fq2* tmp2, const PairingConsts& k, PairLds& L, int lane) {
+  w12_conj(tmp, x, lane);
+  w12_mul(tmp2, x, tmp, L, lane);
+  if (lane == 0) {
+    const Fq2 n0 = tmp2[0], n1 = tmp2[2], n2 = tmp2[4];  // n0 + n1 v + n2 v^2
+    const Fq2 t0 = f2_sub(f2_sqr(n0), f2_mul_xi(f2_mul(n1, n2)));
+    const Fq2 t1 = f2_sub(f2_mul_xi(f2_sqr(n2)), f2_mul(n0, n1));
+    const Fq2 t2 = f2_sub(f2_sqr(n1), f2_mul(n0, n2));
+    const Fq2 den = f2_add(f2_mul(n0, t0), f2_mul_xi(f2_add(f2_mul(n2, t1), f2_mul(n1, t2))));
+    const Fq2 di = f2_inv(den, k);
+    const Fq2 z{u256_zero(), u256_zero()};
+    tmp2[0] = f2_mul(t0, di);
+    tmp2[1] = z;
+    tmp2[2] = f2_mul(t1, di);
+    tmp2[3] = z;
+    tmp2[4] = f2_mul(t2, di);
+    tmp2[5] = z;
+  }
+  wsync();
+  w12_mul(dst, tmp, tmp2, L, lane);
+}
+// dst = x^u (dst != x)
+__device__ void w12_pow_u(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
+  w12_copy(dst, x, lane);
+  for (int b = 61; b >= 0; --b) {  // u has 63 bits
+    w12_mul(dst, dst, dst, L, lane);
+    if ((K_BN_U >> b) & 1) w12_mul(dst, dst, x, L, lane);
+  }
+}
+__device__ void w12_sqr_n(Fq2* dst, const Fq2* x, int n, PairLds& L, int lane) {
+  w12_mul(dst, x, x, L, lane);
+  for (int i = 1; i < n; ++i) w12_mul(dst, dst, dst, L, lane);
+}
+
+// result = f^((q^12-1)/r), f in L.reg[0]; result in L.reg[0]
+__device__ void final_exp_w(const PairingConsts& k, PairLds& L, int lane) {
+  Fq2 *f = L.reg[0], *a = L.reg[1], *b = L.reg[2], *c = L.reg[3], *t0 = L.reg[4], *t1 = L.reg[5],
+      *t2 = L.reg[6], *x = L.reg[7], *y = L.reg[8], *z = L.reg[9], *b6 = L.reg[10], *s = L.reg[11];
+  // easy part: f^(q^6-1) = conj(f) / f, then ^(q^2+1)
+  w12_inv(t0, f, t1, t2, k, L, lane);
+  w12_conj(t1, f, lane);
+  w12_mul(f, t1, t0, L, lane);
+  w12_frob2(t0, f, L, lane);
+  w12_mul(f, t0, f, L, lane);
+  // hard part
+  w12_pow_u(a, f, L, lane);  // f^u
+  w12_pow_u(b, a, L, lane);  // f^(u^2)
+  w12_pow_u(c, b, L, lane);  // f^(u^3)
+  // c36 = c^36 -> t0
+  w12_sqr_n(x, c, 2, L, lane);        // c^4
+  w12_sqr_n(t0, x, 3, L, lane);       // c^32
+  w12_mul(t0, t0, x, L, lane);        // c^36
+  // b^6, b^18, b^30
+  w12_mul(x, b, b, L, lane);          // b^2
+  w12_mul(b6, x, x, L, lane);         // b^4
+  w12_mul(b6, b6, x, L, lane);        // b^6
+  w12_mul(y, b6, b6, L, lane);        // b^12
+  w12_mul(z, y, b6, L, lane);         // b^18
+  w12_mul(y, y, y, L, lane);          // b^24
+  w12_mul(y, y, b6, L, lane);         // b^30
+  // a^12, a^18
+  w12_mul(x, a, a, L, lane);          // a^2
+  w12_mul(s, x, x, L, lane);          // a^4
+  w12_mul(s, s, x, L, lane);          // a^6
+  w12_mul(x, s, s, L, lane);          // a^12
+  w12_mul(s, x, s, L, lane);          // a^18
+  // t1 = conj(c^36 b^18 a^12) * f  (f^l1)
+  w12_mul(t1, t0, z, L, lane);
+  w12_mul(t1, t1, x, L, lane);
+  w12_conj(t1, t1, lane);
+  w12_mul(t1, t1, f, L, lane);
+  // t2 = b^6 f  (f^l2)
+  w12_mul(t2, b6, f, L, lane);
+  // t0 = conj(c^36 b^30 a^18 f^2)  (f^l0)
+  w12_mul(t0, t0, y, L, lane);
+  w12_mul(t0, t0, s, L, lane);
+  w12_mul(x, f, f, L, lane);
+  w12_mul(t0, t0, x, L, lane);
+  w12_conj(t0, t0, lane);
+  // f^l0 * (f^l1)^q * (f^l2)^(q^2) * f^(q^3)
+  w12_frob1(x, t1, L, lane);
+  w12_mul(t0, t0, x, L, lane);
+  w12_frob2(x, t2, L, lane);
+  w12_mul(t0, t0, x, L, lane);
+  w12_frob1(x, f, L, lane);
+  w12_frob2(y, x, L, lane);
+  w12_mul(f, t0, y, L, lane);
+}
+
+// ---------------------------------------------------------------- Miller loop (wave)
+// T = (X : Y : Z) homogeneous on the twist, P = (xp, yp) affine in G1 (Montgomery).
+// Doubling: w = 3X^2, s = 2YZ, R = Ys, B = (X+R)^2 - X^2 - R^2, h = w^2 - 2B,
+//   X3 = h s, Y3 = w (B - h) - 2 R^2, Z3 = s^3;
+//   line * s Z: (s Z) yp - (w Z) xp w + (w X - R) v w   (v w = w^3)
+__device__ void miller_dbl(Fq2* f, const U256& xp, const U256& yp, PairLds& L, int lane) {
+  Fq2* tp = L.tp;
+  // stage 1: X^2, Y Z
+  if (lane == 0) tp[0] = f2_sqr(L.T[0]);
+  if (lane == 1) tp[1] = f2_mul(L.T[1], L.T[2]);
+  wsync();
+  const Fq2 w = f2_add(f2_dbl(tp[0]), tp[0]), s = f2_dbl(tp[1]);
+  // stage 2: ss, R, sZ, wZ, wX, w^2
+  if (lane == 0) tp[2] = f2_sqr(s);
+  if (lane == 1) tp[3] = f2_mul(L.T[1], s);
+  if (lane == 2) tp[4] = f2_mul(s, L.T[2]);
+  if (lane == 3) tp[5] = f2_mul(w, L.T[2]);
+  if (lane == 4) tp[6] = f2_mul(w, L.T[0]);
+  if (lane == 5) tp[7] = f2_sqr(w);
+  wsync();
+  // stage 3: s^3, R^2, (X+R)^2, line
+  if (lane == 0) tp[8] = f2_mul(s, tp[2]);
+  if (lane == 1) tp[9] = f2_sqr(tp[3]);
+  if (lane == 2) tp[10] = f2_sqr(f2_add(L.T[0], tp[3]));
+  if (lane == 3) L.line[0] = f2_muls(tp[4], yp);
+  if (lane == 4) L.line[1] = f2_neg(f2_muls(tp[5], xp));
+  if (lane == 5) L.line[2] = f2_sub(tp[6], tp[3]);
+  wsync();
+  // stage 4: X3, Y3, Z3
+  const Fq2 B = f2_sub(f2_sub(tp[10], tp[0]), tp[9]);
+  const Fq2 h = f2_sub(tp[7], f2_dbl(B));
+  if (lane == 0) L.T[0] = f2_mul(h, s);
+  if (lane == 1) L.T[1] = f2_sub(f2_mul(w, f2_sub(B, h)), f2_dbl(tp[9]));
+  if (lane == 2) L.T[2] = tp[8];
+  wsync();
+  w12_mul(f, f, f, L, lane);
+  w12_mul_line(f, L, lane);
+}
+// Mixed addition T += Qa[qi] (affine (xq, yq)): N = yq Z - Y, D = xq Z - X,
+//   A = N^2 Z - D^3 - 2 D^2 X, X3 = D A, Y3 = N (D^2 X - A) - D^3 Y, Z3 = D^3 Z;
+//   line * D: D yp - N xp w + (N xq - D yq) v w
+__device__ void miller_add(Fq2* f, int qi, const U256& xp, const U256& yp, PairLds& L, int lane) {
+  Fq2* tp = L.tp;
+  const Fq2 xq = L.Qa[qi][0], yq = L.Qa[qi][1];
+  if (lane == 0) tp[0] = f2_mul(yq, L.T[2]);
+  if (lane == 1) tp[1] = f2_mul(xq, L.T[2]);
+  wsync();
+  const Fq2 N = f2_sub(tp[0], L.T[1]), D = f2_sub(tp[1], L.T[0]);
+  if (lane == 0) tp[2] = f2_sqr(N);
+  if (lane == 1) tp[3] = f2_sqr(D);
+  if (lane == 2) tp[4] = f2_mul(N, xq);
+  if (lane == 3) tp[5] = f2_mul(D, yq);
+  if (lane == 4) L.line[0] = f2_muls(D, yp);
+  if (lane == 5) L.line[1] = f2_neg(f2_muls(N, xp));
+  wsync();
+  if (lane == 0) tp[6] = f2_mul(D, tp[3]);       // D^3
+  if (lane == 1) tp[7] = f2_mul(tp[3], L.T[0]);  // D^2 X
+  if (lane == 2) tp[8] = f2_mul(tp[2], L.T[2]);  // N^2 Z
+  if (lane == 3) L.line[2] = f2_sub(tp[4], tp[5]);
+  wsync();
+  const Fq2 A = f2_sub(f2_sub(tp[8], tp[6]), f2_dbl(tp[7]));
+  if (lane == 0) tp[9] = f2_mul(D, A);
+  if (lane == 1) tp[10] = f2_mul(tp[6], L.T[2]);
+  if (lane == 2) tp[11] = f2_mul(N, f2_sub(tp[7], A));
+  if (lane == 3) tp[12] = f2_mul(tp[6], L.T[1]);
+  wsync();
+  if (lane == 0) L.T[0] = tp[9];
+  if (lane == 1) L.T[2] = tp[10];
+  if (lane == 2) L.T[1] = f2_sub(tp[11], tp[12]);
+  wsync();
+  w12_mul_line(f, L, lane);
 }
 
 // ---------------------------------------------------------------- ABI <-> device layouts
@@ -233,68 +441,107 @@ __device__ inline bool all_zero(const uint64_t* p, int n) {
   for (int i = 0; i < n; ++i) o |= p[i];
   return o == 0;
 }
-__device__ void store_f12(uint64_t* out, const Fq12& f) {
-  const Fq2* c[6] = {&f.c0.a0, &f.c0.a1, &f.c0.a2, &f.c1.a0, &f.c1.a1, &f.c1.a2};
-  for (int i = 0; i < 6; ++i) {
-    st_canon(out + 8 * i, c[i]->c0);
-    st_canon(out + 8 * i + 4, c[i]->c1);
-  }
-}
-__device__ Fq12 load_f12_mont(const uint64_t* in) {  // raw Montgomery limbs (scratch)
-  Fq12 f;
-  Fq2* c[6] = {&f.c0.a0, &f.c0.a1, &f.c0.a2, &f.c1.a0, &f.c1.a1, &f.c1.a2};
-  for (int i = 0; i < 6; ++i) {
-    c[i]->c0 = u256_from_u64(in + 8 * i);
-    c[i]->c1 = u256_from_u64(in + 8 * i + 4);
-  }
-  return f;
-}
-__device__ void store_f12_mont(uint64_t* out, const Fq12& f) {
-  const Fq2* c[6] = {&f.c0.a0, &f.c0.a1, &f.c0.a2, &f.c1.a0, &f.c1.a1, &f.c1.a2};
-  for (int i = 0; i < 6; ++i) {
-    u256_to_u64(c[i]->c0, out + 8 * i);
-    u256_to_u64(c[i]->c1, out + 8 * i + 4);
-  }
-}
+// flat index k (w^k) -> ABI tower slot: c0.a0 c0.a1 c0.a2 c1.a0 c1.a1 c1.a2 = w^0 w^2 w^4 w^1 w^3 w^5
+__device__ __forceinline__ int tower_slot(int k) { return (k & 1) ? 3 + (k >> 1) : (k >> 1); }
 
-// Miller value of pair i (Montgomery Fq12, 48 u64), identity inputs -> 1
-__device__ Fq12 miller_of(const uint64_t* g1, const uint64_t* g2, size_t i, const PairingConsts& k) {
+// Miller value of pair i into f (all lanes); identity inputs -> 1
+__device__ void miller_w(Fq2* f, const uint64_t* g1, const uint64_t* g2, size_t i, const PairingConsts& k,
+                         PairLds& L, int lane) {
   const uint64_t* p = g1 + 8 * i;
   const uint64_t* q = g2 + 16 * i;
-  if (all_zero(p, 8) || all_zero(q, 16)) return f12_one(k);
-  G2A qa{{ld_mont(q), ld_mont(q + 4)}, {ld_mont(q + 8), ld_mont(q + 12)}};
-  return miller_loop(ld_mont(p), ld_mont(p + 4), qa, k);
+  w12_one(f, k, lane);
+  if (all_zero(p, 8) || all_zero(q, 16)) return;  // uniform across the wave
+  const U256 xp = ld_mont(p), yp = ld_mont(p + 4);
+  if (lane == 0) {
+    const Fq2 xq{ld_mont(q), ld_mont(q + 4)}, yq{ld_mont(q + 8), ld_mont(q + 12)};
+    L.Qa[0][0] = xq;
+    L.Qa[0][1] = yq;
+    L.T[0] = xq;
+    L.T[1] = yq;
+    L.T[2] = Fq2{k.one, u256_zero()};
+    // pi(Q) = (conj(x) GX, conj(y) GY), -pi^2(Q) = (conj(x1) GX, -conj(y1) GY)
+    const Fq2 gx = kfrob1(k, 2), gy = kfrob1(k, 3);
+    const Fq2 x1 = f2_mul(f2_conj(xq), gx), y1 = f2_mul(f2_conj(yq), gy);
+    L.Qa[1][0] = x1;
+    L.Qa[1][1] = y1;
+    L.Qa[2][0] = f2_mul(f2_conj(x1), gx);
+    L.Qa[2][1] = f2_neg(f2_mul(f2_conj(y1), gy));
+  }
+  wsync();
+  for (int b = 63; b >= 0; --b) {
+    miller_dbl(f, xp, yp, L, lane);
+    if ((k.ate >> b) & 1) miller_add(f, 0, xp, yp, L, lane);
+  }
+  miller_add(f, 1, xp, yp, L, lane);
+  miller_add(f, 2, xp, yp, L, lane);
 }
 
+__device__ void store_f12_canon(uint64_t* out, const Fq2* f, int lane) {
+  if (lane < 6) {
+    const int s = tower_slot(lane);
+    st_canon(out + 8 * s, f[lane].c0);
+    st_canon(out + 8 * s + 4, f[lane].c1);
+  }
+}
+
+// one pairing per workgroup (one wave)
 __global__ void __launch_bounds__(64) pairing_kernel(const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out,
                                                      PairingConsts k) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ PairLds L;
+  const int lane = threadIdx.x;
+  const size_t i = blockIdx.x;
   if (i >= n) return;
-  store_f12(out + 48 * i, final_exp(miller_of(g1, g2, i, k), k));
+  load_consts(k, L, lane);
+  miller_w(L.reg[0], g1, g2, i, k, L, lane);
+  final_exp_w(k, L, lane);
+  store_f12_canon(out + 48 * i, L.reg[0], lane);
 }
 
+// Miller value of pair i, raw Montgomery flat Fq12 (scratch layout)
 __global__ void __launch_bounds__(64) miller_kernel(const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* acc,
                                                     PairingConsts k) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ PairLds L;
+  const int lane = threadIdx.x;
+  const size_t i = blockIdx.x;
   if (i >= n) return;
-  store_f12_mont(acc + 48 * i, miller_of(g1, g2, i, k));
+  load_consts(k, L, lane);
+  miller_w(L.reg[0], g1, g2, i, k, L, lane);
+  if (lane < 6) {
+    u256_to_u64(L.reg[0][lane].c0, acc + 48 * i + 8 * lane);
+    u256_to_u64(L.reg[0][lane].c1, acc + 48 * i + 8 * lane + 4);
+  }
 }
 
 // product of the n Miller values, final exponentiation, compare with 1
-__global__ void pairing_check_final(const uint64_t* acc, size_t n, int* ok, PairingConsts k) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Fq12 f = load_f12_mont(acc);
-  for (size_t i = 1; i < n; ++i) f = f12_mul(f, load_f12_mont(acc + 48 * i));
-  const Fq12 e = final_exp(f, k);
-  const Fq12 one = f12_one(k);
-  const Fq2* a[6] = {&e.c0.a0, &e.c0.a1, &e.c0.a2, &e.c1.a0, &e.c1.a1, &e.c1.a2};
-  const Fq2* b[6] = {&one.c0.a0, &one.c0.a1, &one.c0.a2, &one.c1.a0, &one.c1.a1, &one.c1.a2};
-  bool eq = true;
-  for (int i = 0; i < 6; ++i) eq = eq && f2_eq(*a[i], *b[i]);
-  *ok = eq ? 1 : 0;
+__global__ void __launch_bounds__(64) pairing_check_final(const uint64_t* acc, size_t n, int* ok, PairingConsts k) {
+  __shared__ PairLds L;
+  const int lane = threadIdx.x;
+  Fq2* f = L.reg[0];
+  Fq2* g = L.reg[12];
+  load_consts(k, L, lane);
+  w12_one(f, k, lane);
+  for (size_t i = 0; i < n; ++i) {
+    if (lane < 6) {
+      g[lane].c0 = u256_from_u64(acc + 48 * i + 8 * lane);
+      g[lane].c1 = u256_from_u64(acc + 48 * i + 8 * lane + 4);
+    }
+    wsync();
+    w12_mul(f, f, g, L, lane);
+  }
+  final_exp_w(k, L, lane);
+  if (lane == 0) {
+    bool eq = Fq::eq(f[0].c0, k.one) && Fq::is_zero(f[0].c1);
+    for (int j = 1; j < 6; ++j) eq = eq && f2_is_zero(f[j]);
+    *ok = eq ? 1 : 0;
+  }
 }
 
 // ---------------------------------------------------------------- G2 scalar multiplication
+struct G2A {
+  Fq2 x, y;
+};
+
+
 // out_i = s_i * Q_i (affine double-and-add, LSB first like the reference's G2P::mul,
 // src/pbh/g2.rs:82-101; identity and P + (-P) handled). Used for the SRS's [s]G2.
 __global__ void __launch_bounds__(64) g2_mul_kernel(const uint64_t* pts, const uint64_t* sc, size_t n, uint64_t* out,
@@ -340,21 +587,12 @@ __global__ void __launch_bounds__(64) g2_mul_kernel(const uint64_t* pts, const u
 
 static PairingConsts make_consts() {
   PairingConsts k;
-  k.gx0 = Fq::to_mont(u256_from_u64(K_GX[0]));
-  k.gx1 = Fq::to_mont(u256_from_u64(K_GX[1]));
-  k.gy0 = Fq::to_mont(u256_from_u64(K_GY[0]));
-  k.gy1 = Fq::to_mont(u256_from_u64(K_GY[1]));
+  for (int i = 0; i < 6; ++i)
+    for (int c = 0; c < 2; ++c) k.frob1[i][c] = Fq::to_mont(u256_from_u64(K_FROB1[i][c]));
   for (int i = 0; i < 6; ++i) k.frob2[i] = Fq::to_mont(u256_from_u64(K_FROB2[i]));
   k.one = Fq::to_mont(Fq::one_plain());
-  k.xi_unused = u256_zero();
-  for (int i = 0; i < 12; ++i) k.hard[i] = K_HARD[i];
+  k.r3 = u256_from_u64(K_R3);
   k.ate = K_ATE_LO;
-  U256 p;
-  for (int i = 0; i < 8; ++i) p.w[i] = Bn254FqParams::P[i];
-  uint64_t pl[4];
-  u256_to_u64(p, pl);
-  pl[0] -= 2;  // q is odd and its low limb is > 2: no borrow
-  for (int i = 0; i < 4; ++i) k.qm2[i] = pl[i];
   return k;
 }
 
@@ -381,6 +619,7 @@ static int check_coords(const uint64_t* v, size_t count) {
 extern "C" int pbf_pairing_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, uint64_t* out) {
   if (!ctx || (n && (!g1 || !g2 || !out))) return fail(1, "null argument");
   if (n == 0) return 0;
+  if (n > 0x7fffffffu) return fail(1, "batch too large");
   int rc = check_coords(g1, 2 * n);
   if (!rc) rc = check_coords(g2, 4 * n);
   if (rc) return rc;
@@ -388,7 +627,7 @@ extern "C" int pbf_pairing_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_
   if ((rc = ctx->io0.ensure(n * 64)) || (rc = ctx->io1.ensure(n * 128)) || (rc = ctx->io2.ensure(n * 384))) return rc;
   PBF_HIP(hipMemcpyAsync(ctx->io0.p, g1, n * 64, hipMemcpyHostToDevice, s));
   PBF_HIP(hipMemcpyAsync(ctx->io1.p, g2, n * 128, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(pairing_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (const uint64_t*)ctx->io0.p,
+  hipLaunchKernelGGL(pairing_kernel, dim3(n), dim3(64), 0, s, (const uint64_t*)ctx->io0.p,
                      (const uint64_t*)ctx->io1.p, n, (uint64_t*)ctx->io2.p, make_consts());
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipMemcpyAsync(out, ctx->io2.p, n * 384, hipMemcpyDeviceToHost, s));
@@ -400,7 +639,8 @@ extern "C" int pbf_pairing_bn254_dev(pbf_ctx* ctx, const uint64_t* d_g1, const u
                                      uint64_t* d_out, void* stream) {
   if (!ctx) return fail(1, "null context");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(pairing_kernel, dim3((n + 63) / 64), dim3(64), 0, pbf_ctx::pick(stream), d_g1, d_g2, n, d_out,
+  if (n > 0x7fffffffu) return fail(1, "batch too large");
+  hipLaunchKernelGGL(pairing_kernel, dim3(n), dim3(64), 0, pbf_ctx::pick(stream), d_g1, d_g2, n, d_out,
                      make_consts());
   PBF_HIP(hipGetLastError());
   return 0;
@@ -413,6 +653,7 @@ extern "C" int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const u
     *ok = 1;  // empty product
     return 0;
   }
+  if (n > 0x7fffffffu) return fail(1, "batch too large");
   int rc = check_coords(g1, 2 * n);
   if (!rc) rc = check_coords(g2, 4 * n);
   if (rc) return rc;
@@ -424,7 +665,7 @@ extern "C" int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const u
   const PairingConsts k = make_consts();
   uint64_t* acc = (uint64_t*)ctx->io2.p;
   int* d_ok = (int*)(acc + 48 * n);
-  hipLaunchKernelGGL(miller_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (const uint64_t*)ctx->io0.p,
+  hipLaunchKernelGGL(miller_kernel, dim3(n), dim3(64), 0, s, (const uint64_t*)ctx->io0.p,
                      (const uint64_t*)ctx->io1.p, n, acc, k);
   PBF_HIP(hipGetLastError());
   hipLaunchKernelGGL(pairing_check_final, dim3(1), dim3(64), 0, s, (const uint64_t*)acc, n, d_ok, k);
