@@ -66,7 +66,7 @@ struct Fp256 {
       c = t >> 32;
     }
     // a, b < p < 2^254: no carry out of 256 bits
-    return geq_p(s) ? sub_p(s) : s;
+    return reduce_once(s);
   }
   __host__ __device__ __forceinline__ static U256 sub(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
     U256 d;
@@ -88,15 +88,93 @@ struct Fp256 {
     }
     return d;
   }
-  // CIOS Montgomery product a*b*2^-256 mod p.
-  __host__ __device__ __forceinline__ static U256 mul(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
-    uint32_t t[10];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) t[i] = 0;
+  // a - p if a >= p, else a (a < 2p): one borrow chain and a select, no branches
+  __host__ __device__ __forceinline__ static U256 reduce_once(const U256& a) {
+    U256 d;
+    uint64_t borrow = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      uint64_t C = 0;
+      const uint64_t t = (uint64_t)a.w[i] - Prm::P[i] - borrow;
+      d.w[i] = (uint32_t)t;
+      borrow = (t >> 63) & 1;
+    }
+    U256 r;
 #pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = borrow ? a.w[i] : d.w[i];
+    return r;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Accumulators are 96-bit: c0 (64) + c1 (32) * 2^64. v_mad_u64_u32 returns the carry out
+  // of its 64-bit sum in an SGPR pair, which a v_addc folds into c1. On gfx950 a VALU SGPR
+  // write read as a carry by the next VALU needs 2 wait states: two independent chains
+  // are interleaved so the pad is one s_nop 0 per two products.
+  __device__ __forceinline__ static void mac2(uint64_t& a0, uint32_t& a1, uint32_t xa, uint32_t ya, uint64_t& b0,
+                                              uint32_t& b1, uint32_t xb, uint32_t yb) {
+    uint64_t ca, cb;
+    asm("v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+        "v_mad_u64_u32 %1, %3, %8, %9, %1\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %4, %2, %4, 0, %2\n\t"
+        "v_addc_co_u32_e64 %5, %3, %5, 0, %3"
+        : "+v"(a0), "+v"(b0), "=&s"(ca), "=&s"(cb), "+v"(a1), "+v"(b1)
+        : "v"(xa), "v"(ya), "v"(xb), "v"(yb));
+  }
+  __device__ __forceinline__ static void mac1(uint64_t& a0, uint32_t& a1, uint32_t x, uint32_t y) {
+    uint64_t c;
+    asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32_e64 %2, %1, %2, 0, %1"
+        : "+v"(a0), "=&s"(c), "+v"(a1)
+        : "v"(x), "v"(y));
+  }
+  // Montgomery product a*b*2^-256 mod p by finely integrated product scanning: column k
+  // accumulates every a_i b_j and m_i p_j with i + j = k, one v_mad_u64_u32 plus one
+  // carry add per product and no carry chains between limbs (the row-wise CIOS form
+  // rebuilds a 64-bit addend around every product).
+  __device__ __forceinline__ static U256 mul(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    uint32_t m[8];
+    U256 r;
+    uint64_t c0 = 0;
+    uint32_t c1 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      // the column's products: a_i b_(k-i), then m_i p_(k-i) (i < k for k < 8)
+      const int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+      const int na = hi - lo + 1, nm = k < 8 ? k : 8 - lo;
+      uint32_t xs[16], ys[16];
+      int n = 0;
+#pragma unroll
+      for (int i = lo; i <= hi; ++i) { xs[n] = a.w[i]; ys[n] = b.w[k - i]; ++n; }
+#pragma unroll
+      for (int i = lo; i < lo + nm; ++i) { xs[n] = m[i]; ys[n] = Prm::P[k - i]; ++n; }
+      (void)na;
+      uint64_t d0 = 0;
+      uint32_t d1 = 0;
+#pragma unroll
+      for (int t = 0; t + 1 < n; t += 2) mac2(c0, c1, xs[t], ys[t], d0, d1, xs[t + 1], ys[t + 1]);
+      if (n & 1) mac1(c0, c1, xs[n - 1], ys[n - 1]);
+      const uint64_t s0 = c0 + d0;
+      c1 = c1 + d1 + (s0 < c0 ? 1u : 0u);
+      c0 = s0;
+      if (k < 8) {
+        m[k] = (uint32_t)c0 * Prm::NP;
+        mac1(c0, c1, m[k], Prm::P[0]);  // the column's low 32 bits become 0
+      } else {
+        r.w[k - 8] = (uint32_t)c0;
+      }
+      c0 = (c0 >> 32) | ((uint64_t)c1 << 32);
+      c1 = 0;
+    }
+    r.w[7] = (uint32_t)c0;  // the result is < 2p < 2^256: nothing above
+    return reduce_once(r);
+  }
+#else
+  // CIOS Montgomery product a*b*2^-256 mod p (host).
+  static U256 mul(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    uint32_t t[10];
+    for (int i = 0; i < 10; ++i) t[i] = 0;
+    for (int i = 0; i < 8; ++i) {
+      uint64_t C = 0;
       for (int j = 0; j < 8; ++j) {
         uint64_t s = (uint64_t)a.w[j] * b.w[i] + t[j] + C;
         t[j] = (uint32_t)s;
@@ -108,7 +186,6 @@ struct Fp256 {
       const uint32_t m = t[0] * Prm::NP;
       s = (uint64_t)m * Prm::P[0] + t[0];
       C = s >> 32;
-#pragma unroll
       for (int j = 1; j < 8; ++j) {
         s = (uint64_t)m * Prm::P[j] + t[j] + C;
         t[j - 1] = (uint32_t)s;
@@ -119,10 +196,10 @@ struct Fp256 {
       t[8] = t[9] + (uint32_t)(s >> 32);
     }
     U256 r;
-#pragma unroll
     for (int i = 0; i < 8; ++i) r.w[i] = t[i];
     return geq_p(r) ? sub_p(r) : r;
   }
+#endif
   __host__ __device__ __forceinline__ static U256 r2() {
     U256 v;
 #pragma unroll

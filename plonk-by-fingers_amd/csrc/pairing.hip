@@ -174,24 +174,25 @@ __device__ __forceinline__ Fq2 f2_inv(const Fq2& a, const PairingConsts& k) {
   const U256 ni = fq_inv(Fq::add(Fq::mul(a.c0, a.c0), Fq::mul(a.c1, a.c1)), k);
   return {Fq::mul(a.c0, ni), Fq::sub(u256_zero(), Fq::mul(a.c1, ni))};
 }
-__device__ __forceinline__ Fq2 kfrob1(const PairingConsts& k, int i) { return {k.frob1[i][0], k.frob1[i][1]}; }
 
 // ---------------------------------------------------------------- wave-cooperative Fq12
 // Every function below is called by all 64 lanes of the (single-wave) workgroup and ends
 // with a barrier; operands and results are flat Fq12 (6 Fq2) in LDS and may alias.
+// Miller-step slots: T = (X : Y : Z), the affine point added (xq, yq), P as Fq2 (xp, 0),
+// (yp, 0), the line's w^0, w^1, w^3 coefficients, temporaries from SL_T
+enum { SL_X, SL_Y, SL_Z, SL_XQ, SL_YQ, SL_XP, SL_YP, SL_L0, SL_L1, SL_L3, SL_T };
+
 struct PairLds {
   Fq2 prod[36];    // partial products
   Fq2 reg[14][6];  // Fq12 registers
-  Fq2 line[3];     // sparse line: w^0, w^1, w^3 coefficients
-  Fq2 tp[16];      // T-step scratch
-  Fq2 T[3];        // X, Y, Z
+  Fq2 sl[32];      // Miller-step slots (SL_* above)
   Fq2 Qa[3][2];    // Q, pi(Q), -pi^2(Q) affine
   Fq2 frob1[6];    // the lane-indexed constants (a lane-indexed kernel argument would be
   U256 frob2[6];   // copied to scratch)
 };
 
 // constants -> LDS with compile-time indices
-__device__ void load_consts(const PairingConsts& k, PairLds& L, int lane) {
+__device__ __forceinline__ void load_consts(const PairingConsts& k, PairLds& L, int lane) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (lane == i) {
@@ -204,11 +205,15 @@ __device__ void load_consts(const PairingConsts& k, PairLds& L, int lane) {
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
-// dst = x * y
-__device__ void w12_mul(Fq2* dst, const Fq2* x, const Fq2* y, PairLds& L, int lane) {
+// dst = x * y: 36 Fq2 products (one per lane, x xi for the wrapped terms), then 6 lanes
+// sum them (a three-level Karatsuba split into 54 Fq products measured slower: its operand
+// selection diverges across lanes and adds three reconstruction stages)
+__device__ __forceinline__ void w12_mul(Fq2* dst, const Fq2* x, const Fq2* y, PairLds& L, int lane) {
   if (lane < 36) {
     const int i = lane / 6, j = lane - 6 * (lane / 6);
-    Fq2 p = (x == y && i == j) ? f2_sqr(x[i]) : f2_mul(x[i], y[j]);
+    // one f2_mul for every lane (a separate squaring path for the diagonal would only
+    // serialise two code paths across the wave)
+    Fq2 p = f2_mul(x[i], y[j]);
     if (i + j >= 6) p = f2_mul_xi(p);
     L.prod[lane] = p;
   }
@@ -225,11 +230,11 @@ __device__ void w12_mul(Fq2* dst, const Fq2* x, const Fq2* y, PairLds& L, int la
   wsync();
 }
 // f *= line (coefficients at w^0, w^1, w^3)
-__device__ void w12_mul_line(Fq2* f, PairLds& L, int lane) {
+__device__ __forceinline__ void w12_mul_line(Fq2* f, PairLds& L, int lane) {
   if (lane < 18) {
     const int i = lane / 3, jj = lane - 3 * (lane / 3);
     const int j = jj == 2 ? 3 : jj;
-    Fq2 p = f2_mul(f[i], L.line[jj]);
+    Fq2 p = f2_mul(f[i], L.sl[SL_L0 + jj]);
     if (i + j >= 6) p = f2_mul_xi(p);
     L.prod[6 * i + j] = p;
   }
@@ -246,118 +251,123 @@ __device__ void w12_mul_line(Fq2* f, PairLds& L, int lane) {
   }
   wsync();
 }
-__device__ void w12_copy(Fq2* dst, const Fq2* x, int lane) {
+__device__ __forceinline__ void w12_copy(Fq2* dst, const Fq2* x, int lane) {
   if (lane < 6) dst[lane] = x[lane];
   wsync();
 }
 // x^(q^6): w -> -w
-__device__ void w12_conj(Fq2* dst, const Fq2* x, int lane) {
+__device__ __forceinline__ void w12_conj(Fq2* dst, const Fq2* x, int lane) {
   if (lane < 6) dst[lane] = (lane & 1) ? f2_neg(x[lane]) : x[lane];
   wsync();
 }
 // x^q: g_k -> conj(g_k) FROB1[k]
-__device__ void w12_frob1(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
+__device__ __forceinline__ void w12_frob1(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
   if (lane < 6) dst[lane] = lane == 0 ? f2_conj(x[0]) : f2_mul(f2_conj(x[lane]), L.frob1[lane]);
   wsync();
 }
 // x^(q^2): g_k -> g_k FROB2[k]
-__device__ void w12_frob2(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
+__device__ __forceinline__ void w12_frob2(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
   if (lane < 6) dst[lane] = lane == 0 ? x[0] : f2_muls(x[lane], L.frob2[lane]);
   wsync();
 }
-__device__ void w12_one(Fq2* dst, const PairingConsts& k, int lane) {
+__device__ __forceinline__ void w12_one(Fq2* dst, const PairingConsts& k, int lane) {
   if (lane < 6) dst[lane] = Fq2{lane == 0 ? k.one : u256_zero(), u256_zero()};
   wsync();
 }
-// dst = x^-1: x * conj(x) = N lies in Fq6 = span(w^0, w^2, w^4); N^-1 on lane 0 (Fq6
-// inverse over Fq2, one Fq inversion); dst = conj(x) * N^-1
-__device__ void w12_inv(Fq2* dst, const Fq2* x, Fq2* tmp, Fq2* tmp2, const PairingConsts& k, PairLds& L, int lane) {
-  w12_conj(tmp, x, lane);
-  w12_mul(tmp2, x, tmp, L, lane);
-  if (lane == 0) {
-    const Fq2 n0 = tmp2[0], n1 = tmp2[2], n2 = tmp2[4];  // n0 + n1 v + n2 v^2
-    const Fq2 t0 = f2_sub(f2_sqr(n0), f2_mul_xi(f2_mul(n1, n2)));
-    const Fq2 t1 = f2_sub(f2_mul_xi(f2_sqr(n2)), f2_mul(n0, n1));
-    const Fq2 t2 = f2_sub(f2_sqr(n1), f2_mul(n0, n2));
-    const Fq2 den = f2_add(f2_mul(n0, t0), f2_mul_xi(f2_add(f2_mul(n2, t1), f2_mul(n1, t2))));
-    const Fq2 di = f2_inv(den, k);
-    const Fq2 z{u256_zero(), u256_zero()};
-    tmp2[0] = f2_mul(t0, di);
-    tmp2[1] = z;
-    tmp2[2] = f2_mul(t1, di);
-    tmp2[3] = z;
-    tmp2[4] = f2_mul(t2, di);
-    tmp2[5] = z;
-  }
-  wsync();
-  w12_mul(dst, tmp, tmp2, L, lane);
-}
-// dst = x^u (dst != x)
-__device__ void w12_pow_u(Fq2* dst, const Fq2* x, PairLds& L, int lane) {
-  w12_copy(dst, x, lane);
-  for (int b = 61; b >= 0; --b) {  // u has 63 bits
-    w12_mul(dst, dst, dst, L, lane);
-    if ((K_BN_U >> b) & 1) w12_mul(dst, dst, x, L, lane);
-  }
-}
-__device__ void w12_sqr_n(Fq2* dst, const Fq2* x, int n, PairLds& L, int lane) {
-  w12_mul(dst, x, x, L, lane);
-  for (int i = 1; i < n; ++i) w12_mul(dst, dst, dst, L, lane);
+// In-place inverse of the Fq6 element n0 + n1 v + n2 v^2 held at flat slots 0, 2, 4 of n
+// (one lane; one Fq inversion)
+__device__ __noinline__ void fq6_inv_flat(Fq2* n, const PairingConsts& k) {
+  const Fq2 n0 = n[0], n1 = n[2], n2 = n[4];
+  const Fq2 t0 = f2_sub(f2_sqr(n0), f2_mul_xi(f2_mul(n1, n2)));
+  const Fq2 t1 = f2_sub(f2_mul_xi(f2_sqr(n2)), f2_mul(n0, n1));
+  const Fq2 t2 = f2_sub(f2_sqr(n1), f2_mul(n0, n2));
+  const Fq2 den = f2_add(f2_mul(n0, t0), f2_mul_xi(f2_add(f2_mul(n2, t1), f2_mul(n1, t2))));
+  const Fq2 di = f2_inv(den, k);
+  const Fq2 z{u256_zero(), u256_zero()};
+  n[0] = f2_mul(t0, di);
+  n[1] = z;
+  n[2] = f2_mul(t1, di);
+  n[3] = z;
+  n[4] = f2_mul(t2, di);
+  n[5] = z;
 }
 
+// The final exponentiation as a program over the LDS Fq12 registers, run by one
+// interpreter loop: one inlined copy of each wave primitive and no calls (a call would
+// save and restore the callee's VGPRs through scratch every time).
+enum : uint8_t { FE_MUL, FE_CONJ, FE_FROB1, FE_FROB2, FE_COPY, FE_INVN };
+struct FeOp {
+  uint8_t op, dst, a, b;
+};
+constexpr int FE_MAX = 320;
+struct FeProg {
+  FeOp ops[FE_MAX];
+  int n;
+};
+// registers: 0 f (in/out), 1 a = f^u, 2 b = f^u^2, 3 c = f^u^3, 4..11 temporaries, 12, 13 inverse
+constexpr FeProg make_fe_prog() {
+  FeProg p{};
+  int n = 0;
+  auto op = [&](uint8_t o, int d, int a, int b) { p.ops[n++] = FeOp{o, (uint8_t)d, (uint8_t)a, (uint8_t)b}; };
+  auto mul = [&](int d, int a, int b) { op(FE_MUL, d, a, b); };
+  auto powu = [&](int d, int x) {  // d = x^u, u = K_BN_U (63 bits)
+    op(FE_COPY, d, x, 0);
+    for (int bit = 61; bit >= 0; --bit) {
+      mul(d, d, d);
+      if ((0x44e992b44a6909f1ull >> bit) & 1) mul(d, d, x);
+    }
+  };
+  // easy part: f^(q^6-1) = conj(f) / f (f^-1 = conj(f) * (f conj(f))^-1), then ^(q^2+1)
+  op(FE_CONJ, 12, 0, 0);
+  mul(13, 0, 12);
+  op(FE_INVN, 13, 0, 0);
+  mul(4, 12, 13);          // f^-1
+  mul(0, 12, 4);           // conj(f) f^-1
+  op(FE_FROB2, 4, 0, 0);
+  mul(0, 4, 0);
+  // hard part: l0 + l1 q + l2 q^2 + q^3 (see file header)
+  powu(1, 0);
+  powu(2, 1);
+  powu(3, 2);
+  mul(7, 3, 3); mul(7, 7, 7);                   // c^4
+  mul(4, 7, 7); mul(4, 4, 4); mul(4, 4, 4);     // c^32
+  mul(4, 4, 7);                                 // c^36
+  mul(7, 2, 2); mul(10, 7, 7); mul(10, 10, 7);  // b^2, b^4, b^6
+  mul(8, 10, 10); mul(9, 8, 10);                // b^12, b^18
+  mul(8, 8, 8); mul(8, 8, 10);                  // b^24, b^30
+  mul(7, 1, 1); mul(11, 7, 7); mul(11, 11, 7);  // a^2, a^4, a^6
+  mul(7, 11, 11); mul(11, 7, 11);               // a^12, a^18
+  mul(5, 4, 9); mul(5, 5, 7); op(FE_CONJ, 5, 5, 0); mul(5, 5, 0);  // f^l1
+  mul(6, 10, 0);                                                  // f^l2
+  mul(4, 4, 8); mul(4, 4, 11); mul(7, 0, 0); mul(4, 4, 7); op(FE_CONJ, 4, 4, 0);  // f^l0
+  op(FE_FROB1, 7, 5, 0); mul(4, 4, 7);
+  op(FE_FROB2, 7, 6, 0); mul(4, 4, 7);
+  op(FE_FROB1, 7, 0, 0); op(FE_FROB2, 8, 7, 0); mul(0, 4, 8);
+  p.n = n;
+  return p;
+}
+__constant__ FeProg c_fe_prog = make_fe_prog();
+static_assert(make_fe_prog().n <= FE_MAX, "program size");
+
 // result = f^((q^12-1)/r), f in L.reg[0]; result in L.reg[0]
-__device__ void final_exp_w(const PairingConsts& k, PairLds& L, int lane) {
-  Fq2 *f = L.reg[0], *a = L.reg[1], *b = L.reg[2], *c = L.reg[3], *t0 = L.reg[4], *t1 = L.reg[5],
-      *t2 = L.reg[6], *x = L.reg[7], *y = L.reg[8], *z = L.reg[9], *b6 = L.reg[10], *s = L.reg[11];
-  // easy part: f^(q^6-1) = conj(f) / f, then ^(q^2+1)
-  w12_inv(t0, f, t1, t2, k, L, lane);
-  w12_conj(t1, f, lane);
-  w12_mul(f, t1, t0, L, lane);
-  w12_frob2(t0, f, L, lane);
-  w12_mul(f, t0, f, L, lane);
-  // hard part
-  w12_pow_u(a, f, L, lane);  // f^u
-  w12_pow_u(b, a, L, lane);  // f^(u^2)
-  w12_pow_u(c, b, L, lane);  // f^(u^3)
-  // c36 = c^36 -> t0
-  w12_sqr_n(x, c, 2, L, lane);        // c^4
-  w12_sqr_n(t0, x, 3, L, lane);       // c^32
-  w12_mul(t0, t0, x, L, lane);        // c^36
-  // b^6, b^18, b^30
-  w12_mul(x, b, b, L, lane);          // b^2
-  w12_mul(b6, x, x, L, lane);         // b^4
-  w12_mul(b6, b6, x, L, lane);        // b^6
-  w12_mul(y, b6, b6, L, lane);        // b^12
-  w12_mul(z, y, b6, L, lane);         // b^18
-  w12_mul(y, y, y, L, lane);          // b^24
-  w12_mul(y, y, b6, L, lane);         // b^30
-  // a^12, a^18
-  w12_mul(x, a, a, L, lane);          // a^2
-  w12_mul(s, x, x, L, lane);          // a^4
-  w12_mul(s, s, x, L, lane);          // a^6
-  w12_mul(x, s, s, L, lane);          // a^12
-  w12_mul(s, x, s, L, lane);          // a^18
-  // t1 = conj(c^36 b^18 a^12) * f  (f^l1)
-  w12_mul(t1, t0, z, L, lane);
-  w12_mul(t1, t1, x, L, lane);
-  w12_conj(t1, t1, lane);
-  w12_mul(t1, t1, f, L, lane);
-  // t2 = b^6 f  (f^l2)
-  w12_mul(t2, b6, f, L, lane);
-  // t0 = conj(c^36 b^30 a^18 f^2)  (f^l0)
-  w12_mul(t0, t0, y, L, lane);
-  w12_mul(t0, t0, s, L, lane);
-  w12_mul(x, f, f, L, lane);
-  w12_mul(t0, t0, x, L, lane);
-  w12_conj(t0, t0, lane);
-  // f^l0 * (f^l1)^q * (f^l2)^(q^2) * f^(q^3)
-  w12_frob1(x, t1, L, lane);
-  w12_mul(t0, t0, x, L, lane);
-  w12_frob2(x, t2, L, lane);
-  w12_mul(t0, t0, x, L, lane);
-  w12_frob1(x, f, L, lane);
-  w12_frob2(y, x, L, lane);
-  w12_mul(f, t0, y, L, lane);
+__device__ __forceinline__ void final_exp_w(const PairingConsts& k, PairLds& L, int lane) {
+  const int n = c_fe_prog.n;
+  for (int pc = 0; pc < n; ++pc) {
+    const FeOp o = c_fe_prog.ops[pc];
+    Fq2* d = L.reg[o.dst];
+    const Fq2* a = L.reg[o.a];
+    switch (o.op) {
+      case FE_MUL: w12_mul(d, a, L.reg[o.b], L, lane); break;
+      case FE_CONJ: w12_conj(d, a, lane); break;
+      case FE_FROB1: w12_frob1(d, a, L, lane); break;
+      case FE_FROB2: w12_frob2(d, a, L, lane); break;
+      case FE_COPY: w12_copy(d, a, lane); break;
+      default:  // FE_INVN
+        if (lane == 0) fq6_inv_flat(d, k);
+        wsync();
+        break;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- Miller loop (wave)
@@ -365,72 +375,98 @@ __device__ void final_exp_w(const PairingConsts& k, PairLds& L, int lane) {
 // Doubling: w = 3X^2, s = 2YZ, R = Ys, B = (X+R)^2 - X^2 - R^2, h = w^2 - 2B,
 //   X3 = h s, Y3 = w (B - h) - 2 R^2, Z3 = s^3;
 //   line * s Z: (s Z) yp - (w Z) xp w + (w X - R) v w   (v w = w^3)
-__device__ void miller_dbl(Fq2* f, const U256& xp, const U256& yp, PairLds& L, int lane) {
-  Fq2* tp = L.tp;
-  // stage 1: X^2, Y Z
-  if (lane == 0) tp[0] = f2_sqr(L.T[0]);
-  if (lane == 1) tp[1] = f2_mul(L.T[1], L.T[2]);
-  wsync();
-  const Fq2 w = f2_add(f2_dbl(tp[0]), tp[0]), s = f2_dbl(tp[1]);
-  // stage 2: ss, R, sZ, wZ, wX, w^2
-  if (lane == 0) tp[2] = f2_sqr(s);
-  if (lane == 1) tp[3] = f2_mul(L.T[1], s);
-  if (lane == 2) tp[4] = f2_mul(s, L.T[2]);
-  if (lane == 3) tp[5] = f2_mul(w, L.T[2]);
-  if (lane == 4) tp[6] = f2_mul(w, L.T[0]);
-  if (lane == 5) tp[7] = f2_sqr(w);
-  wsync();
-  // stage 3: s^3, R^2, (X+R)^2, line
-  if (lane == 0) tp[8] = f2_mul(s, tp[2]);
-  if (lane == 1) tp[9] = f2_sqr(tp[3]);
-  if (lane == 2) tp[10] = f2_sqr(f2_add(L.T[0], tp[3]));
-  if (lane == 3) L.line[0] = f2_muls(tp[4], yp);
-  if (lane == 4) L.line[1] = f2_neg(f2_muls(tp[5], xp));
-  if (lane == 5) L.line[2] = f2_sub(tp[6], tp[3]);
-  wsync();
-  // stage 4: X3, Y3, Z3
-  const Fq2 B = f2_sub(f2_sub(tp[10], tp[0]), tp[9]);
-  const Fq2 h = f2_sub(tp[7], f2_dbl(B));
-  if (lane == 0) L.T[0] = f2_mul(h, s);
-  if (lane == 1) L.T[1] = f2_sub(f2_mul(w, f2_sub(B, h)), f2_dbl(tp[9]));
-  if (lane == 2) L.T[2] = tp[8];
-  wsync();
-  w12_mul(f, f, f, L, lane);
-  w12_mul_line(f, L, lane);
-}
-// Mixed addition T += Qa[qi] (affine (xq, yq)): N = yq Z - Y, D = xq Z - X,
+// Mixed addition T += (xq, yq): N = yq Z - Y, D = xq Z - X,
 //   A = N^2 Z - D^3 - 2 D^2 X, X3 = D A, Y3 = N (D^2 X - A) - D^3 Y, Z3 = D^3 Z;
 //   line * D: D yp - N xp w + (N xq - D yq) v w
-__device__ void miller_add(Fq2* f, int qi, const U256& xp, const U256& yp, PairLds& L, int lane) {
-  Fq2* tp = L.tp;
-  const Fq2 xq = L.Qa[qi][0], yq = L.Qa[qi][1];
-  if (lane == 0) tp[0] = f2_mul(yq, L.T[2]);
-  if (lane == 1) tp[1] = f2_mul(xq, L.T[2]);
-  wsync();
-  const Fq2 N = f2_sub(tp[0], L.T[1]), D = f2_sub(tp[1], L.T[0]);
-  if (lane == 0) tp[2] = f2_sqr(N);
-  if (lane == 1) tp[3] = f2_sqr(D);
-  if (lane == 2) tp[4] = f2_mul(N, xq);
-  if (lane == 3) tp[5] = f2_mul(D, yq);
-  if (lane == 4) L.line[0] = f2_muls(D, yp);
-  if (lane == 5) L.line[1] = f2_neg(f2_muls(N, xp));
-  wsync();
-  if (lane == 0) tp[6] = f2_mul(D, tp[3]);       // D^3
-  if (lane == 1) tp[7] = f2_mul(tp[3], L.T[0]);  // D^2 X
-  if (lane == 2) tp[8] = f2_mul(tp[2], L.T[2]);  // N^2 Z
-  if (lane == 3) L.line[2] = f2_sub(tp[4], tp[5]);
-  wsync();
-  const Fq2 A = f2_sub(f2_sub(tp[8], tp[6]), f2_dbl(tp[7]));
-  if (lane == 0) tp[9] = f2_mul(D, A);
-  if (lane == 1) tp[10] = f2_mul(tp[6], L.T[2]);
-  if (lane == 2) tp[11] = f2_mul(N, f2_sub(tp[7], A));
-  if (lane == 3) tp[12] = f2_mul(tp[6], L.T[1]);
-  wsync();
-  if (lane == 0) L.T[0] = tp[9];
-  if (lane == 1) L.T[2] = tp[10];
-  if (lane == 2) L.T[1] = f2_sub(tp[11], tp[12]);
-  wsync();
-  w12_mul_line(f, L, lane);
+// Both steps are micro-op programs over the slot file: a MULS group is up to 6
+// independent Fq2 products, one per lane (one inlined f2_mul for the whole wave); a LIN
+// group is a short run of additions on lane 0; F12 ops update f. One interpreter loop
+// runs them, so the kernel holds one copy of each primitive (I-cache, registers).
+enum : uint8_t { U_MULS, U_LIN, U_F12SQR, U_F12LINE, L_ADD, L_SUB, L_DBL, L_TRP, L_NEG, L_COPY, U_MUL };
+struct Uop {
+  uint8_t code, d, a, b;
+};
+#define MUL(d, a, b) Uop{U_MUL, (uint8_t)(d), (uint8_t)(a), (uint8_t)(b)}
+#define LIN(c, d, a, b) Uop{c, (uint8_t)(d), (uint8_t)(a), (uint8_t)(b)}
+#define GRP(c, n) Uop{c, (uint8_t)(n), 0, 0}
+constexpr int T0 = SL_T;
+__constant__ Uop c_dbl_prog[] = {
+    GRP(U_MULS, 2), MUL(T0 + 0, SL_X, SL_X), MUL(T0 + 1, SL_Y, SL_Z),                // X^2, YZ
+    GRP(U_LIN, 2), LIN(L_TRP, T0 + 2, T0 + 0, 0), LIN(L_DBL, T0 + 3, T0 + 1, 0),    // w, s
+    GRP(U_MULS, 6), MUL(T0 + 4, T0 + 3, T0 + 3), MUL(T0 + 5, SL_Y, T0 + 3),          // s^2, R
+    MUL(T0 + 6, T0 + 3, SL_Z), MUL(T0 + 7, T0 + 2, SL_Z),                            // sZ, wZ
+    MUL(T0 + 8, T0 + 2, SL_X), MUL(T0 + 9, T0 + 2, T0 + 2),                          // wX, w^2
+    GRP(U_LIN, 1), LIN(L_ADD, T0 + 10, SL_X, T0 + 5),                                // X + R
+    GRP(U_MULS, 5), MUL(T0 + 11, T0 + 3, T0 + 4), MUL(T0 + 12, T0 + 5, T0 + 5),      // s^3, R^2
+    MUL(T0 + 13, T0 + 10, T0 + 10), MUL(SL_L0, T0 + 6, SL_YP), MUL(T0 + 14, T0 + 7, SL_XP),
+    GRP(U_LIN, 9), LIN(L_NEG, SL_L1, T0 + 14, 0), LIN(L_SUB, SL_L3, T0 + 8, T0 + 5),
+    LIN(L_SUB, T0 + 15, T0 + 13, T0 + 0), LIN(L_SUB, T0 + 15, T0 + 15, T0 + 12),     // B
+    LIN(L_DBL, T0 + 16, T0 + 15, 0), LIN(L_SUB, T0 + 16, T0 + 9, T0 + 16),           // h
+    LIN(L_SUB, T0 + 17, T0 + 15, T0 + 16), LIN(L_DBL, T0 + 18, T0 + 12, 0),          // B - h, 2R^2
+    LIN(L_COPY, SL_Z, T0 + 11, 0),                                                    // Z3
+    GRP(U_MULS, 2), MUL(SL_X, T0 + 16, T0 + 3), MUL(T0 + 19, T0 + 2, T0 + 17),         // X3, w(B-h)
+    GRP(U_LIN, 1), LIN(L_SUB, SL_Y, T0 + 19, T0 + 18),                                // Y3
+    GRP(U_F12SQR, 0), GRP(U_F12LINE, 0)};
+__constant__ Uop c_add_prog[] = {
+    GRP(U_MULS, 2), MUL(T0 + 0, SL_YQ, SL_Z), MUL(T0 + 1, SL_XQ, SL_Z),
+    GRP(U_LIN, 2), LIN(L_SUB, T0 + 2, T0 + 0, SL_Y), LIN(L_SUB, T0 + 3, T0 + 1, SL_X),  // N, D
+    GRP(U_MULS, 6), MUL(T0 + 4, T0 + 2, T0 + 2), MUL(T0 + 5, T0 + 3, T0 + 3),         // N^2, D^2
+    MUL(T0 + 6, T0 + 2, SL_XQ), MUL(T0 + 7, T0 + 3, SL_YQ),                           // N xq, D yq
+    MUL(SL_L0, T0 + 3, SL_YP), MUL(T0 + 8, T0 + 2, SL_XP),                            // D yp, N xp
+    GRP(U_LIN, 2), LIN(L_NEG, SL_L1, T0 + 8, 0), LIN(L_SUB, SL_L3, T0 + 6, T0 + 7),
+    GRP(U_MULS, 3), MUL(T0 + 9, T0 + 3, T0 + 5), MUL(T0 + 10, T0 + 5, SL_X),          // D^3, D^2 X
+    MUL(T0 + 11, T0 + 4, SL_Z),                                                       // N^2 Z
+    GRP(U_LIN, 4), LIN(L_SUB, T0 + 12, T0 + 11, T0 + 9), LIN(L_DBL, T0 + 13, T0 + 10, 0),
+    LIN(L_SUB, T0 + 12, T0 + 12, T0 + 13), LIN(L_SUB, T0 + 14, T0 + 10, T0 + 12),    // A, D^2X - A
+    GRP(U_MULS, 4), MUL(T0 + 15, T0 + 3, T0 + 12), MUL(T0 + 16, T0 + 9, SL_Z),
+    MUL(T0 + 17, T0 + 2, T0 + 14), MUL(T0 + 18, T0 + 9, SL_Y),
+    GRP(U_LIN, 3), LIN(L_COPY, SL_X, T0 + 15, 0), LIN(L_COPY, SL_Z, T0 + 16, 0),
+    LIN(L_SUB, SL_Y, T0 + 17, T0 + 18),
+    GRP(U_F12LINE, 0)};
+#undef MUL
+#undef LIN
+#undef GRP
+constexpr int DBL_LEN = sizeof(c_dbl_prog) / sizeof(Uop), ADD_LEN = sizeof(c_add_prog) / sizeof(Uop);
+static_assert(SL_T + 20 <= 32, "slot file");
+
+__device__ __forceinline__ void run_uops(const Uop* prog, int len, Fq2* f, PairLds& L, int lane) {
+  Fq2* sl = L.sl;
+  for (int pc = 0; pc < len;) {
+    const Uop u = prog[pc];
+    if (u.code == U_MULS) {
+      if (lane < u.d) {
+        const Uop m = prog[pc + 1 + lane];
+        sl[m.d] = f2_mul(sl[m.a], sl[m.b]);
+      }
+      wsync();
+      pc += 1 + u.d;
+    } else if (u.code == U_LIN) {
+      if (lane == 0) {
+        for (int i = 0; i < u.d; ++i) {
+          const Uop m = prog[pc + 1 + i];
+          const Fq2 a = sl[m.a], b = sl[m.b];
+          Fq2 r;
+          switch (m.code) {
+            case L_ADD: r = f2_add(a, b); break;
+            case L_SUB: r = f2_sub(a, b); break;
+            case L_DBL: r = f2_dbl(a); break;
+            case L_TRP: r = f2_add(f2_dbl(a), a); break;
+            case L_NEG: r = f2_neg(a); break;
+            default: r = a; break;  // L_COPY
+          }
+          sl[m.d] = r;
+        }
+      }
+      wsync();
+      pc += 1 + u.d;
+    } else if (u.code == U_F12SQR) {
+      w12_mul(f, f, f, L, lane);
+      ++pc;
+    } else {  // U_F12LINE
+      w12_mul_line(f, L, lane);
+      ++pc;
+    }
+  }
 }
 
 // ---------------------------------------------------------------- ABI <-> device layouts
@@ -445,22 +481,25 @@ __device__ inline bool all_zero(const uint64_t* p, int n) {
 __device__ __forceinline__ int tower_slot(int k) { return (k & 1) ? 3 + (k >> 1) : (k >> 1); }
 
 // Miller value of pair i into f (all lanes); identity inputs -> 1
-__device__ void miller_w(Fq2* f, const uint64_t* g1, const uint64_t* g2, size_t i, const PairingConsts& k,
-                         PairLds& L, int lane) {
+__device__ __forceinline__ void miller_w(Fq2* f, const uint64_t* g1, const uint64_t* g2, size_t i,
+                                         const PairingConsts& k, PairLds& L, int lane) {
   const uint64_t* p = g1 + 8 * i;
   const uint64_t* q = g2 + 16 * i;
   w12_one(f, k, lane);
   if (all_zero(p, 8) || all_zero(q, 16)) return;  // uniform across the wave
-  const U256 xp = ld_mont(p), yp = ld_mont(p + 4);
   if (lane == 0) {
     const Fq2 xq{ld_mont(q), ld_mont(q + 4)}, yq{ld_mont(q + 8), ld_mont(q + 12)};
     L.Qa[0][0] = xq;
     L.Qa[0][1] = yq;
-    L.T[0] = xq;
-    L.T[1] = yq;
-    L.T[2] = Fq2{k.one, u256_zero()};
+    L.sl[SL_X] = xq;
+    L.sl[SL_Y] = yq;
+    L.sl[SL_Z] = Fq2{k.one, u256_zero()};
+    L.sl[SL_XQ] = xq;
+    L.sl[SL_YQ] = yq;
+    L.sl[SL_XP] = Fq2{ld_mont(p), u256_zero()};
+    L.sl[SL_YP] = Fq2{ld_mont(p + 4), u256_zero()};
     // pi(Q) = (conj(x) GX, conj(y) GY), -pi^2(Q) = (conj(x1) GX, -conj(y1) GY)
-    const Fq2 gx = kfrob1(k, 2), gy = kfrob1(k, 3);
+    const Fq2 gx = L.frob1[2], gy = L.frob1[3];
     const Fq2 x1 = f2_mul(f2_conj(xq), gx), y1 = f2_mul(f2_conj(yq), gy);
     L.Qa[1][0] = x1;
     L.Qa[1][1] = y1;
@@ -468,15 +507,30 @@ __device__ void miller_w(Fq2* f, const uint64_t* g1, const uint64_t* g2, size_t 
     L.Qa[2][1] = f2_neg(f2_mul(f2_conj(y1), gy));
   }
   wsync();
-  for (int b = 63; b >= 0; --b) {
-    miller_dbl(f, xp, yp, L, lane);
-    if ((k.ate >> b) & 1) miller_add(f, 0, xp, yp, L, lane);
+  // bits 63..0 of 6u+2 below its leading bit: double, and add Q on a one; then T + pi(Q)
+  // and T - pi^2(Q). One run_uops call site (one inlined copy of the step code).
+  int b = 63;
+  bool dbl = true;
+  while (b >= -2) {
+    if (!dbl && b < 0) {
+      if (lane == 0) {
+        L.sl[SL_XQ] = L.Qa[b == -1 ? 1 : 2][0];
+        L.sl[SL_YQ] = L.Qa[b == -1 ? 1 : 2][1];
+      }
+      wsync();
+    }
+    run_uops(dbl ? c_dbl_prog : c_add_prog, dbl ? DBL_LEN : ADD_LEN, f, L, lane);
+    // next step: after a doubling at bit b, the addition if bit b is set; else the next bit
+    if (dbl && ((k.ate >> b) & 1)) {
+      dbl = false;
+    } else {
+      --b;
+      dbl = b >= 0;
+    }
   }
-  miller_add(f, 1, xp, yp, L, lane);
-  miller_add(f, 2, xp, yp, L, lane);
 }
 
-__device__ void store_f12_canon(uint64_t* out, const Fq2* f, int lane) {
+__device__ __forceinline__ void store_f12_canon(uint64_t* out, const Fq2* f, int lane) {
   if (lane < 6) {
     const int s = tower_slot(lane);
     st_canon(out + 8 * s, f[lane].c0);
