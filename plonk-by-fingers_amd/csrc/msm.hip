@@ -7,7 +7,11 @@
 //   1. msm_digits: key = (window << 16) | digit per (point, window), digit 0 skipped
 //   2. hipCUB radix sort of (key, point index) pairs  -> points grouped by bucket
 //   3. msm_bucket_bounds: [start, end) of every bucket in the sorted order
-//   4. msm_bucket_acc: one thread per bucket, XYZZ accumulation of affine points
+//   4. msm_chunk_acc: the sorted list cut into fixed chunks of MSM_CH entries, one thread
+//      per chunk accumulating its runs of equal keys in XYZZ (every thread does the same
+//      number of additions whatever the bucket sizes); runs that cross a chunk boundary
+//      leave partial sums, which msm_chunk_join adds up (one thread per bucket that starts
+//      in a chunk and ends in a later one)
 //   5. msm_window_reduce: per window, 256 segments of 256 buckets; running sums give
 //      sum_k (k-a) B_k and sum_k B_k per segment, + a * (segment sum), LDS tree
 //   6. host: Horner over the 16 window sums (2^16 steps), one inversion to affine.
@@ -71,14 +75,69 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
   }
 }
 
-__global__ void __launch_bounds__(256) msm_bucket_acc(const Affine* pts, const uint32_t* vals, const uint32_t* start,
-                                                      const uint32_t* end, Xyzz* buckets, uint32_t nbuckets) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbuckets) return;
+constexpr uint32_t MSM_CH = 32;  // sorted entries per accumulation thread
+
+struct ChunkPart {
+  Xyzz acc;
+  uint32_t key;  // MSM_SENTINEL: no partial
+  uint32_t pad[3];
+};
+
+// Chunk t = entries [t*CH, (t+1)*CH) of the sorted list (m valid entries). Complete runs
+// (the whole bucket inside the chunk) are written to their bucket. head[t]: the first run
+// if its bucket started in an earlier chunk; tail[t]: the last run if its bucket starts in
+// this chunk and ends in a later one. Buckets with no entry stay zero (ZZ = 0: identity).
+__global__ void __launch_bounds__(256) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
+                                                     const uint32_t* start, const uint32_t* end, uint32_t m,
+                                                     Xyzz* buckets, ChunkPart* head, ChunkPart* tail) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c0 = t * MSM_CH;
+  if (c0 >= m) return;
+  const uint32_t c1 = c0 + MSM_CH < m ? c0 + MSM_CH : m;
+  uint32_t cur = keys[c0], rs = c0;
   Xyzz acc = G1::identity();
-  const uint32_t e = end[b];
-  for (uint32_t j = start[b]; j < e; ++j) acc = G1::madd(acc, pts[vals[j]]);
-  buckets[b] = acc;
+  head[t].key = MSM_SENTINEL;
+  tail[t].key = MSM_SENTINEL;
+  if (cur == MSM_SENTINEL) return;  // past the valid prefix (zero digits sort last)
+  auto flush = [&](uint32_t re) {
+    const uint32_t bs = start[cur], be = end[cur];
+    if (bs < rs) {  // continues a bucket of an earlier chunk (possibly spanning this one)
+      head[t].acc = acc;
+      head[t].key = cur;
+    } else if (be > re) {  // starts here, ends in a later chunk
+      tail[t].acc = acc;
+      tail[t].key = cur;
+    } else {
+      buckets[cur] = acc;
+    }
+  };
+  uint32_t j = c0;
+  for (; j < c1; ++j) {
+    const uint32_t k = keys[j];
+    if (k != cur) {
+      flush(j);
+      if (k == MSM_SENTINEL) return;
+      cur = k;
+      rs = j;
+      acc = G1::identity();
+    }
+    acc = G1::madd(acc, pts[vals[j]]);
+  }
+  flush(c1);
+}
+
+// one thread per chunk owning a boundary-crossing bucket: its tail plus the heads of the
+// following chunks the bucket covers
+__global__ void __launch_bounds__(256) msm_chunk_join(const ChunkPart* head, const ChunkPart* tail,
+                                                      const uint32_t* end, uint32_t nchunks, Xyzz* buckets) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nchunks) return;
+  const uint32_t k = tail[t].key;
+  if (k == MSM_SENTINEL) return;
+  Xyzz acc = tail[t].acc;
+  const uint32_t be = end[k];
+  for (uint32_t u = t + 1; u < nchunks && u * MSM_CH < be; ++u) acc = G1::add(acc, head[u].acc);
+  buckets[k] = acc;
 }
 
 __device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
@@ -153,14 +212,15 @@ static uint64_t grid1(uint64_t count) {
 }
 
 struct MsmWork {
-  DevBuf pts, inf, keys, vals, keys2, vals2, start, end, buckets, shares, sums, temp;
+  DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &temp, &head, &tail;
 };
 
-static MsmWork& msm_work(pbf_ctx* ctx) {
-  static std::map<pbf_ctx*, std::unique_ptr<MsmWork>> m;
-  auto& p = m[ctx];
-  if (!p) p.reset(new MsmWork());
-  return *p;
+// scratch owned by the context (freed with it)
+static MsmWork msm_work(pbf_ctx* ctx) {
+  return MsmWork{ctx->buf("msm.pts"),     ctx->buf("msm.inf"),    ctx->buf("msm.keys"),   ctx->buf("msm.vals"),
+                 ctx->buf("msm.keys2"),   ctx->buf("msm.vals2"),  ctx->buf("msm.start"),  ctx->buf("msm.end"),
+                 ctx->buf("msm.buckets"), ctx->buf("msm.shares"), ctx->buf("msm.sums"),   ctx->buf("msm.temp"),
+                 ctx->buf("msm.head"),    ctx->buf("msm.tail")};
 }
 
 // Enqueue the device part; window sums land in w.sums (MSM_NW Xyzz, Montgomery).
@@ -174,7 +234,9 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
       (rc = w.start.ensure((uint64_t)MSM_NW * MSM_NB * 4)) || (rc = w.end.ensure((uint64_t)MSM_NW * MSM_NB * 4)) ||
       (rc = w.buckets.ensure((uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz))) ||
       (rc = w.shares.ensure((uint64_t)MSM_NW * MSM_NSEG * sizeof(Xyzz))) ||
-      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))))
+      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))) ||
+      (rc = w.head.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))) ||
+      (rc = w.tail.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))))
     return rc;
   hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, (Affine*)w.pts.p,
                      (uint8_t*)w.inf.p, n);
@@ -192,10 +254,16 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
                      (uint32_t*)w.start.p, (uint32_t*)w.end.p);
-  const uint32_t nb = MSM_NW * MSM_NB;
-  hipLaunchKernelGGL(msm_bucket_acc, dim3((nb + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
-                     (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p, (const uint32_t*)w.end.p,
-                     (Xyzz*)w.buckets.p, nb);
+  // the valid (non-sentinel) prefix of the sorted list: the sentinel sorts last; its
+  // length is known only on the device, so chunks past it return at once
+  PBF_HIP(hipMemsetAsync(w.buckets.p, 0, (uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz), s));
+  const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
+  hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
+                     (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
+                     (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
+                     (ChunkPart*)w.tail.p);
+  hipLaunchKernelGGL(msm_chunk_join, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const ChunkPart*)w.head.p,
+                     (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p);
   hipLaunchKernelGGL(msm_segments, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
                      (Xyzz*)w.shares.p);
   hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.shares.p,
@@ -249,7 +317,7 @@ int pbf_msm_g1_bn254(pbf_ctx* ctx, const uint64_t* points, const uint64_t* scala
   if ((rc = ctx->io0.ensure(n * 64)) || (rc = ctx->io1.ensure(n * 32))) return rc;
   PBF_HIP(hipMemcpyAsync(ctx->io0.p, points, n * 64, hipMemcpyHostToDevice, s));
   PBF_HIP(hipMemcpyAsync(ctx->io1.p, scalars, n * 32, hipMemcpyHostToDevice, s));
-  MsmWork& w = msm_work(ctx);
+  MsmWork w = msm_work(ctx);
   if ((rc = msm_device(ctx, (const uint64_t*)ctx->io0.p, (const uint64_t*)ctx->io1.p, n, s, w))) return rc;
   std::vector<Xyzz> sums(MSM_NW);
   PBF_HIP(hipMemcpyAsync(sums.data(), w.sums.p, MSM_NW * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
@@ -264,7 +332,7 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
   if (!ctx || !out || (n && (!d_points || !d_scalars))) return fail(PBF_EINVAL, "null argument");
   if (n == 0) { for (int i = 0; i < 8; ++i) out[i] = 0; return PBF_OK; }
   hipStream_t s = (hipStream_t)stream;
-  MsmWork& w = msm_work(ctx);
+  MsmWork w = msm_work(ctx);
   int rc = msm_device(ctx, d_points, d_scalars, n, s, w);
   if (rc) return rc;
   std::vector<Xyzz> sums(MSM_NW);
