@@ -123,7 +123,9 @@ struct G1 {
   // k * p for a small non-negative k (double-and-add, MSB first)
   __host__ __device__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
     Xyzz r = identity();
-    for (int b = 31; b >= 0; --b) {
+    int top = 31;
+    while (top >= 0 && !((k >> top) & 1)) --top;  // from the leading one
+    for (int b = top; b >= 0; --b) {
       r = dbl(r);
       if ((k >> b) & 1) r = add(r, p);
     }

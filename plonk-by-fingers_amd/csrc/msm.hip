@@ -26,8 +26,12 @@ namespace pbf {
 
 constexpr int MSM_C = 16;
 constexpr int MSM_NW = 16;
-constexpr uint32_t MSM_NB = 1u << MSM_C;
-constexpr uint32_t MSM_SENTINEL = (uint32_t)MSM_NW << MSM_C;  // sorts after every real key
+// signed digits in [-2^15, 2^15]: bucket j of a window holds the points whose digit has
+// |d| = j + 1 (negated for d < 0), so a window has 2^15 buckets
+constexpr int MSM_BB = MSM_C - 1;                            // bucket-index bits
+constexpr uint32_t MSM_NB = 1u << MSM_BB;                    // buckets per window
+constexpr uint32_t MSM_SENTINEL = (uint32_t)MSM_NW << MSM_BB;  // sorts after every real key
+constexpr uint32_t MSM_NEG = 0x80000000u;                    // sign flag in the point index
 constexpr int MSM_SEG_THREADS = 256;
 
 __device__ __forceinline__ U256 load_u256(const uint64_t* p) {
@@ -53,15 +57,26 @@ __global__ void msm_points_to_mont(const uint64_t* pts, Affine* out, uint8_t* in
   }
 }
 
+// 16-bit windows recoded to signed digits (d >= 2^15 -> d - 2^16, carry 1 upward); the
+// top window of a < 2^254 scalar stays below 2^14 + 1, so 16 windows hold every carry
 __global__ void msm_digits(const uint64_t* scalars, const uint8_t* inf, uint32_t* keys, uint32_t* vals, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = scalars + 4 * i;
     const bool skip = inf[i] != 0;
+    uint32_t carry = 0;
 #pragma unroll
     for (int w = 0; w < MSM_NW; ++w) {
-      const uint32_t d = (uint32_t)((s[w / 4] >> (16 * (w % 4))) & 0xFFFF);
-      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? MSM_SENTINEL : (((uint32_t)w << MSM_C) | d);
-      vals[(uint64_t)w * n + i] = (uint32_t)i;
+      uint32_t d = (uint32_t)((s[w / 4] >> (16 * (w % 4))) & 0xFFFF) + carry;
+      bool neg = false;
+      if (d > MSM_NB) {  // d - 2^16 < 0
+        d = (1u << MSM_C) - d;
+        neg = true;
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? MSM_SENTINEL : (((uint32_t)w << MSM_BB) | (d - 1));
+      vals[(uint64_t)w * n + i] = (uint32_t)i | (neg ? MSM_NEG : 0u);
     }
   }
 }
@@ -121,7 +136,10 @@ __global__ void __launch_bounds__(256) msm_chunk_acc(const Affine* pts, const ui
       rs = j;
       acc = G1::identity();
     }
-    acc = G1::madd(acc, pts[vals[j]]);
+    const uint32_t v = vals[j];
+    Affine p = pts[v & ~MSM_NEG];
+    if (v & MSM_NEG) p.y = Fq::sub(u256_zero(), p.y);
+    acc = G1::madd(acc, p);
   }
   flush(c1);
 }
@@ -146,10 +164,10 @@ __device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
   return r;
 }
 
-// S_w = sum_{k>=1} k * B_{w,k}, in two launches. (a) one thread per (window, segment
-// of MSM_SEG buckets starting at a): running sums give sum (k-a+1) B_k and sum B_k, and
-// the segment's share is wsum + (a-1) * running. (b) one workgroup per window sums its
-// segment shares (sequential per thread, then an LDS tree).
+// S_w = sum_j (j + 1) * B_{w,j}, in two launches. (a) one thread per (window, segment of
+// MSM_SEG buckets starting at a): running sums give sum (j - a + 1) B_j and sum B_j, and
+// the segment's share is wsum + a * running. (b) one workgroup per window sums its segment
+// shares (sequential per thread, then an LDS tree).
 constexpr uint32_t MSM_SEG = 16;
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
 
@@ -164,7 +182,7 @@ __global__ void __launch_bounds__(256) msm_segments(const Xyzz* buckets, Xyzz* s
     running = G1::add(running, B[k]);
     wsum = G1::add(wsum, running);
   }
-  shares[id] = (a == 0) ? G1::add(wsum, xyzz_neg(running)) : G1::add(wsum, G1::mul_small(running, a - 1));
+  shares[id] = (a == 0) ? wsum : G1::add(wsum, G1::mul_small(running, a));
 }
 
 __global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz* shares, Xyzz* sums) {
@@ -245,11 +263,11 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   size_t temp_bytes = 0;
   PBF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (const uint32_t*)w.keys.p, (uint32_t*)w.keys2.p,
                                              (const uint32_t*)w.vals.p, (uint32_t*)w.vals2.p, (int)m, 0,
-                                             MSM_C + 5, s));
+                                             MSM_BB + 5, s));
   if ((rc = w.temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
   PBF_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp.p, temp_bytes, (const uint32_t*)w.keys.p, (uint32_t*)w.keys2.p,
                                              (const uint32_t*)w.vals.p, (uint32_t*)w.vals2.p, (int)m, 0,
-                                             MSM_C + 5, s));
+                                             MSM_BB + 5, s));
   PBF_HIP(hipMemsetAsync(w.start.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,

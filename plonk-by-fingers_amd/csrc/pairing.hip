@@ -71,7 +71,7 @@ static const uint64_t K_FROB2[6][4] = {
 static const uint64_t K_R3[4] = {0xb1cd6dafda1530dfull, 0x62f210e6a7283db6ull, 0xef7f0b0c0ada0afbull,
                                  0x20fd6e902d592544ull};
 static const uint64_t K_ATE_LO = 0x9d797039be763ba8ull;  // 6u+2 = 2^64 + K_ATE_LO
-static const uint64_t K_BN_U = 0x44e992b44a6909f1ull;    // u = 4965661367192848881
+constexpr uint64_t K_BN_U = 0x44e992b44a6909f1ull;  // u = 4965661367192848881
 
 // ---------------------------------------------------------------- Fq / Fq2 (one lane)
 struct Fq2 {
@@ -314,7 +314,7 @@ constexpr FeProg make_fe_prog() {
     op(FE_COPY, d, x, 0);
     for (int bit = 61; bit >= 0; --bit) {
       mul(d, d, d);
-      if ((0x44e992b44a6909f1ull >> bit) & 1) mul(d, d, x);
+      if ((K_BN_U >> bit) & 1) mul(d, d, x);
     }
   };
   // easy part: f^(q^6-1) = conj(f) / f (f^-1 = conj(f) * (f conj(f))^-1), then ^(q^2+1)
