@@ -45,7 +45,7 @@ struct G1 {
   __host__ __device__ __forceinline__ static U256 dbl_f(const U256& a) { return F::add(a, a); }
 
   // mdbl-2008-s-1: 2*(x, y) for an affine point (y != 0 on BN254 G1: no 2-torsion)
-  __host__ __device__ static Xyzz mdbl(const Affine& a) {
+  __host__ __device__ __forceinline__ static Xyzz mdbl(const Affine& a) {
     const U256 U = dbl_f(a.y);
     const U256 V = F::mul(U, U);
     const U256 W = F::mul(U, V);
@@ -60,7 +60,7 @@ struct G1 {
     return r;
   }
   // dbl-2008-s-1
-  __host__ __device__ static Xyzz dbl(const Xyzz& p) {
+  __host__ __device__ __forceinline__ static Xyzz dbl(const Xyzz& p) {
     if (is_identity(p)) return p;
     const U256 U = dbl_f(p.Y);
     const U256 V = F::mul(U, U);
@@ -76,7 +76,7 @@ struct G1 {
     return r;
   }
   // madd-2008-s: p + a (a affine, not the identity)
-  __host__ __device__ static Xyzz madd(const Xyzz& p, const Affine& a) {
+  __host__ __device__ __forceinline__ static Xyzz madd(const Xyzz& p, const Affine& a) {
     if (is_identity(p)) return from_affine(a);
     const U256 U2 = F::mul(a.x, p.ZZ);
     const U256 S2 = F::mul(a.y, p.ZZZ);
@@ -97,7 +97,7 @@ struct G1 {
     return r;
   }
   // add-2008-s: p + q
-  __host__ __device__ static Xyzz add(const Xyzz& p, const Xyzz& q) {
+  __host__ __device__ __forceinline__ static Xyzz add(const Xyzz& p, const Xyzz& q) {
     if (is_identity(p)) return q;
     if (is_identity(q)) return p;
     const U256 U1 = F::mul(p.X, q.ZZ);

@@ -1,0 +1,33 @@
+"""MSM probe (run under rocprofv3 for the per-kernel split): python scripts/bench_msm.py [log_n] [reps]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "plonk-by-fingers_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import pbf  # noqa: E402
+
+
+def main(log_n=20, reps=5):
+    ctx = pbf.Context(0)
+    m = 1 << log_n
+    rng = np.random.default_rng(4)
+    top = np.uint64(pbf.BN254_R >> 192)
+    sc = rng.integers(0, 1 << 64, size=(m, 4), dtype=np.uint64)
+    sc[:, 3] %= top
+    s = torch.from_numpy(sc.reshape(-1).view(np.int64)).cuda()
+    t = torch.from_numpy(rng.integers(1, 1 << 62, size=(m, 4), dtype=np.uint64).reshape(-1).view(np.int64)).cuda()
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m)
+    torch.cuda.synchronize()
+    ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m)
+    print("msm 2^%d ms %.3f" % (log_n, (time.perf_counter() - t0) / reps * 1e3))
+
+
+if __name__ == "__main__":
+    main(*[int(a) for a in sys.argv[1:]])
