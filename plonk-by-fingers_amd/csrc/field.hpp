@@ -22,16 +22,19 @@ struct Goldilocks {
   static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
   static constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p = 2^32 - 1
 
+  // The corrections below add or subtract a select of EPS (a 32-bit value) instead of
+  // selecting between two 64-bit candidates: one v_cndmask instead of two per result.
   __host__ __device__ __forceinline__ static uint64_t add(uint64_t a, uint64_t b, const FieldArgs&) {
-    uint64_t s = a + b;
-    // wrap (s < a) means the true sum is s + 2^64 = s + EPS (mod p); s + EPS cannot
-    // wrap again because a + b - 2^64 < p - 2^32. Otherwise subtract p when s >= p.
-    uint64_t t = s + EPS;
-    return (s < a || s >= P) ? t : s;
+    uint64_t s;
+    const bool wrap = __builtin_add_overflow(a, b, &s);
+    // wrap: the true sum is s + 2^64 = s + EPS (mod p), and s + EPS cannot wrap again
+    // (a + b - 2^64 < p - 2^32); s >= p: s - p = s + EPS (mod 2^64). Never both.
+    return s + ((wrap || s >= P) ? EPS : 0);
   }
   __host__ __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
-    uint64_t d = a - b;
-    return (a < b) ? d - EPS : d;  // d + p (mod 2^64)
+    uint64_t d;
+    const bool borrow = __builtin_sub_overflow(a, b, &d);
+    return d - (borrow ? EPS : 0);  // d + p (mod 2^64); d > EPS when borrowing
   }
   // 128-bit value lo + hi*2^64 reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
   __host__ __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {
@@ -56,9 +59,9 @@ struct Goldilocks {
   // lo + t (mod p) for any lo < 2^64 and t <= (2^32-1)*EPS: one wrap/one
   // conditional subtraction suffice (see DESIGN.md "Goldilocks arithmetic").
   __host__ __device__ __forceinline__ static uint64_t add_small(uint64_t lo, uint64_t t) {
-    uint64_t s = lo + t;
-    uint64_t u = s + EPS;
-    return (s < t || s >= P) ? u : s;
+    uint64_t s;
+    const bool wrap = __builtin_add_overflow(lo, t, &s);
+    return s + ((wrap || s >= P) ? EPS : 0);
   }
   // x * 2^S (mod p) for a compile-time 0 <= S < 96, x canonical.
   template <int S>
