@@ -64,6 +64,7 @@ struct GlPassArgs {
   uint32_t scaled;         // tc carries n^-1: multiply every element, k1 = 0 / r2 = 0 too
   uint32_t out_split_log;  // != 0: store destination-major [n/S][batch][S] (multi-GPU send layout)
   uint32_t xcd_kmajor;     // XCD-aware column-major block order (pass-twiddle table reuse in L2)
+  uint32_t blk_log;        // BLK first pass: log2 of the blocked layout's block width W2
 };
 
 // x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1. Exponents in
@@ -177,7 +178,12 @@ constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
 // One tile: stages A, B, C and the stores. PERSIST: the tile's raw input is already in LDS
 // (lds[r*W + w]); after stage C has consumed the exchange buffer and its twiddles, the
 // next tile `next` is LDS-DMA'd into it while the C-point DFTs and the stores run.
-template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST>
+// BLK (two-pass plans): the intermediate between the passes is stored blocked,
+// y(j, k) at (k / W2) * (W2 * R2) + j * W2 + (k mod W2), so the second pass reads each
+// tile as one contiguous 64-KiB block instead of 64-B runs n/R apart; the first pass
+// stores 512-B runs (a wave covers 8 k x 8 j). FIRST && BLK: blocked store; !FIRST &&
+// BLK: blocked load.
+template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false>
 __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t,
                                         uint32_t next) {
   using Sh = GlShape<LOGR, TILE>;
@@ -203,6 +209,8 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
       const int r = 16 * C * s1 + C * s2 + r2;
       if constexpr (PERSIST)
         v[u * 4 + s1] = lds[r * W + w];
+      else if constexpr (BLK && !FIRST)
+        v[u * 4 + s1] = in[(uint64_t)kb * TILE + r * W + w];
       else
         v[u * 4 + s1] = in[(j0 + w) + (uint64_t)r * stride];
     }
@@ -281,7 +289,10 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   // of k in the output rows out[j*R + k]); later passes w fastest (W-element runs of j)
   auto c_map = [&](int u, int* k1, int* w) {
     const int idx = t + NT * u;
-    if constexpr (FIRST) {
+    if constexpr (FIRST && BLK) {  // 8 k1 x 8 w per wave: 512-B runs of the blocked layout
+      *k1 = (idx & 7) + 8 * ((idx >> 3) / W);
+      *w = (idx >> 3) % W;
+    } else if constexpr (FIRST) {
       *k1 = idx & 63;
       *w = idx >> 6;
     } else {
@@ -343,11 +354,22 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     for (int u = 0; u < Sh::NSUB_C; ++u) {
       int k1, w;
       c_map(u, &k1, &w);
-      const uint64_t base = (j0 + w) << LOGR;
+      if constexpr (BLK) {
+        const uint32_t bl = a.blk_log;
+        const uint64_t jw = (j0 + w) << bl;
+        const uint64_t bstride = stride << bl;  // W2 * R2 (R2 = n / R columns)
 #pragma unroll
-      for (int k2 = 0; k2 < C; ++k2)
-        if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
-          o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
+        for (int k2 = 0; k2 < C; ++k2) {
+          const uint32_t k = k1 + 64 * k2;
+          o[(uint64_t)(k >> bl) * bstride + jw + (k & ((1u << bl) - 1))] = x[u * C + bitrev_c(k2, LOGC)];
+        }
+      } else {
+        const uint64_t base = (j0 + w) << LOGR;
+#pragma unroll
+        for (int k2 = 0; k2 < C; ++k2)
+          if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
+            o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
+      }
     }
   } else {
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
@@ -385,13 +407,13 @@ __device__ __forceinline__ void gl_shape_checks() {
 }
 
 // One tile per workgroup.
-template <int LOGR, int E64, bool FIRST, int TILE>
+template <int LOGR, int E64, bool FIRST, int TILE, bool BLK = false>
 __global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_gl_pass_kernel(GlPassArgs a) {
   gl_shape_checks<LOGR, TILE>();
   __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
   const uint32_t tiles = a.blocks_per_poly * a.batch;
-  gl_tile<LOGR, E64, FIRST, TILE, false>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
+  gl_tile<LOGR, E64, FIRST, TILE, false, BLK>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
 }
 
 // Persistent, software-pipelined (PBF_NTT_PERSIST): each workgroup walks tiles blockIdx.x,

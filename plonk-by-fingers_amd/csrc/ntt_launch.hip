@@ -397,6 +397,21 @@ static GlPassFn gl_fn_e(int logr, bool first, int tile, bool persist) {
 }
 #undef PBF_GL_K
 
+// blocked-intermediate variants (two-pass plans), the default tile of each radix
+template <int E>
+static GlPassFn gl_fn_blk(int logr, bool first) {
+#define PBF_GL_B(LR, T) (first ? ntt_gl_pass_kernel<LR, E, true, T, true> : ntt_gl_pass_kernel<LR, E, false, T, true>)
+  switch (logr) {
+    case 6: return PBF_GL_B(6, 4096);
+    case 7: return PBF_GL_B(7, 4096);
+    case 8: return PBF_GL_B(8, 4096);
+    case 9: return PBF_GL_B(9, 4096);
+    case 10: return PBF_GL_B(10, 8192);
+    default: return nullptr;
+  }
+#undef PBF_GL_B
+}
+
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log);
@@ -419,6 +434,19 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log) {
   const size_t P = p.logr.size();
+  // two-pass plans with equal tile widths may keep the intermediate blocked (ntt_gl.hpp BLK)
+  bool blk = false;
+  uint32_t blk_log = 0;
+  // opt-in (PBF_NTT_BLK): measured level with the natural layout
+  if (P == 2 && getenv("PBF_NTT_BLK") && !getenv("PBF_NTT_PERSIST")) {
+    const int t0 = gl_tile(p.logr[0]), t1 = gl_tile(p.logr[1]);
+    const uint64_t w0 = (uint64_t)t0 >> p.logr[0], w1 = (uint64_t)t1 >> p.logr[1];
+    const bool dflt = (t0 == (p.logr[0] >= 10 ? 8192 : 4096)) && (t1 == (p.logr[1] >= 10 ? 8192 : 4096));
+    if (w0 == w1 && dflt && (p.n >> p.logr[0]) % w0 == 0 && (p.n >> p.logr[1]) % w1 == 0) {
+      blk = true;
+      while ((1ull << blk_log) < w1) ++blk_log;
+    }
+  }
   uint32_t log_ns = 0;
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
@@ -426,6 +454,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     const bool persist = getenv("PBF_NTT_PERSIST") != nullptr;  // A/B: pipelined persistent kernel
     GlPassFn fn =
         p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile, persist) : gl_fn_e<153>(lr, log_ns == 0, tile, persist);
+    if (blk) fn = p.e64 == 39 ? gl_fn_blk<39>(lr, log_ns == 0) : gl_fn_blk<153>(lr, log_ns == 0);
     if (!fn) return fail(1, "no Goldilocks pass kernel for this radix");
     const uint64_t W = (uint64_t)tile >> lr;
     if ((p.n >> lr) % W) return fail(1, "transform too small for the pass tile");
@@ -447,6 +476,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     const uint64_t tiles = (uint64_t)a.blocks_per_poly * batch;
     if (tiles > 0x7fffffffull) return fail(1, "batch too large");
     a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
+    a.blk_log = blk_log;
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;

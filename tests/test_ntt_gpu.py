@@ -135,6 +135,33 @@ def test_batch_dev_matches_single(ctx):
     assert np.array_equal(d_in.cpu().numpy().view(np.uint64), got)
 
 
+@pytest.mark.parametrize("env", [{"PBF_NTT_BLK": "1"}, {"PBF_NTT_PERSIST": "1"}, {"PBF_NTT_GROUP": "2"},
+                                 {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"}, {"PBF_NTT_NO_KMAJOR": "1"}])
+@pytest.mark.parametrize("logn", [16, 20])
+def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
+    """Every opt-in schedule of the Goldilocks pass kernel (blocked intermediate, persistent
+    pipelined kernel, polynomial groups, tile orders; ntt_launch.hip) gives the oracle's
+    answer, forward and inverse, on a batch."""
+    import torch
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, batch = 1 << logn, 3
+    w = root(GOLD, n)
+    host = np.stack([oracle.splitmix_field(GOLD, 700 + i, n) for i in range(batch)])
+    d_in = torch.from_numpy(host.view(np.int64)).cuda()
+    d_out = torch.empty_like(d_in)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.ntt_batch_dev(GOLD, w, d_in.data_ptr(), d_out.data_ptr(), n, batch, stream=stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.uint64)
+    for i in range(batch):
+        assert np.array_equal(got[i], oracle.ntt_iter(GOLD, w, host[i]))
+    ctx.ntt_batch_dev(GOLD, w, d_out.data_ptr(), d_out.data_ptr(), n, batch, inverse=True, stream=stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy().view(np.uint64), host)
+
+
 def test_fill_random_matches_host_generator(ctx):
     import torch
 
