@@ -12,8 +12,15 @@ src/fft.rs:94-96, become the rank index). Forward, on every rank:
 
 The inverse runs the same three steps backwards. The exchange is the only
 collective; there is no other data-path communication.
+
+The batch runs in `chunks` groups of polynomials (independent transforms), software-
+pipelined: group c's all-to-all (RCCL's stream, async) overlaps group c+1's local NTT
+and group c-1's combine on the compute stream, so a step costs about
+max(compute, exchange) instead of their sum.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -40,7 +47,7 @@ class ShardedNtt:
     """Batched forward / inverse NTT of `batch` polynomials of N = world * nl points."""
 
     def __init__(self, ops, comm, rank: int, world: int, nl: int, batch: int, modulus: int = GOLD,
-                 omega: int | None = None, device: str | torch.device = "cuda"):
+                 omega: int | None = None, device: str | torch.device = "cuda", chunks: int | None = None):
         if world not in (2, 4, 8):
             raise ValueError("world size must be 2, 4 or 8")
         self.ops, self.comm = ops, comm
@@ -51,24 +58,52 @@ class ShardedNtt:
         shape = (batch * nl,)
         self.send = torch.empty(shape, dtype=torch.int64, device=device)
         self.recv = torch.empty(shape, dtype=torch.int64, device=device)
+        if chunks is None:
+            chunks = int(os.environ.get("PBF_MG_CHUNKS", "4"))
+        while chunks > 1 and batch % chunks:
+            chunks -= 1
+        self.chunks = max(1, chunks)
 
-    def _exchange(self):
-        # equal splits along dim 0: chunk r of `send` goes to rank r, chunk g of `recv` came from rank g
-        self.comm.all_to_all_single(self.recv, self.send)
+    def _exchange(self, c: int):
+        # equal splits along dim 0 of group c's slice: part r of `send` goes to rank r, part g
+        # of `recv` came from rank g (layout [peer][polynomial of the group][kk])
+        sl = self._slice(c)
+        return self.comm.all_to_all_single(self.recv[sl], self.send[sl], async_op=True)
+
+    def _slice(self, c: int) -> slice:
+        L = (self.batch // self.chunks) * self.nl
+        return slice(c * L, (c + 1) * L)
+
+    def _pipeline(self, first, second):
+        """first(c) produces send[c]; the exchange fills recv[c]; second(c) consumes it."""
+        works = []
+        for c in range(self.chunks):
+            first(c)
+            works.append(self._exchange(c))
+            if c >= 1:
+                works[c - 1].wait()
+                second(c - 1)
+        works[-1].wait()
+        second(self.chunks - 1)
 
     def forward(self, shard: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """shard[b][m] = a_b[rank + world*m]  ->  out[b][q*S + kk] = X_b[q*nl + rank*S + kk]."""
-        self.ops.local(self.modulus, self.omega, self.world, shard, self.send, self.nl, self.batch, False)
-        self._exchange()
-        self.ops.combine(self.modulus, self.omega, self.world, self.rank, self.recv, out, self.nl, self.batch, False)
+        bc = self.batch // self.chunks
+        self._pipeline(
+            lambda c: self.ops.local(self.modulus, self.omega, self.world, shard[self._slice(c)],
+                                     self.send[self._slice(c)], self.nl, bc, False),
+            lambda c: self.ops.combine(self.modulus, self.omega, self.world, self.rank, self.recv[self._slice(c)],
+                                       out[self._slice(c)], self.nl, bc, False))
         return out
 
     def inverse(self, blocked: torch.Tensor, shard_out: torch.Tensor) -> torch.Tensor:
         """Exact inverse of forward(): blocked outputs -> the stride shard of the coefficients."""
-        self.ops.combine(self.modulus, self.omega, self.world, self.rank, blocked, self.send, self.nl, self.batch,
-                         True)
-        self._exchange()
-        self.ops.local(self.modulus, self.omega, self.world, self.recv, shard_out, self.nl, self.batch, True)
+        bc = self.batch // self.chunks
+        self._pipeline(
+            lambda c: self.ops.combine(self.modulus, self.omega, self.world, self.rank, blocked[self._slice(c)],
+                                       self.send[self._slice(c)], self.nl, bc, True),
+            lambda c: self.ops.local(self.modulus, self.omega, self.world, self.recv[self._slice(c)],
+                                     shard_out[self._slice(c)], self.nl, bc, True))
         return shard_out
 
     # ---- layout helpers (host side, for tests and the whole-vector entry point)

@@ -68,7 +68,7 @@ class OracleShardOps:
                         send[g, b, kk] = acc * pow(w, g * k, m) % m * ginv % m
 
 
-def _worker(rank, world, port, nl, batch, q):
+def _worker(rank, world, port, nl, batch, q, chunks=1):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "plonk-by-fingers_amd"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -81,7 +81,8 @@ def _worker(rank, world, port, nl, batch, q):
         N = world * nl
         glob = np.stack([oracle.splitmix_field(GOLD, 700 + b, N) for b in range(batch)])
         shard = torch.from_numpy(np.ascontiguousarray(glob[:, rank::world]).view(np.int64).reshape(-1).copy())
-        nt = ShardedNtt(OracleShardOps(), dist, rank, world, nl, batch, device="cpu")
+        nt = ShardedNtt(OracleShardOps(), dist, rank, world, nl, batch, device="cpu", chunks=chunks)
+        assert nt.chunks == chunks
         out = torch.empty_like(shard)
         nt.forward(shard, out)
         w = nt.omega
@@ -105,12 +106,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_ntt_gloo(world):
+@pytest.mark.parametrize("world,batch,chunks", [(2, 2, 1), (4, 2, 1), (8, 2, 1), (2, 4, 4), (4, 4, 2)])
+def test_sharded_ntt_gloo(world, batch, chunks):
+    """chunks > 1: the pipelined schedule (async all-to-all per polynomial group)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 64, 2, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 64, batch, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
