@@ -126,9 +126,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
       buckets[cur] = acc;
     }
   };
-  uint32_t j = c0;
-  for (; j < c1; ++j) {
-    const uint32_t k = keys[j];
+  // the next entry's key, index and point are loaded while the current addition runs
+  // (the point gathers are random: their latency would otherwise stall every step)
+  uint32_t k_nx = cur, v_nx = vals[c0];
+  Affine p_nx = pts[v_nx & ~MSM_NEG];
+  for (uint32_t j = c0; j < c1; ++j) {
+    const uint32_t k = k_nx, v = v_nx;
+    Affine p = p_nx;
+    if (j + 1 < c1) {
+      k_nx = keys[j + 1];
+      v_nx = vals[j + 1];
+      p_nx = pts[v_nx & ~MSM_NEG];  // a sentinel entry's index is still a valid point
+    }
     if (k != cur) {
       flush(j);
       if (k == MSM_SENTINEL) return;
@@ -136,8 +145,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
       rs = j;
       acc = G1::identity();
     }
-    const uint32_t v = vals[j];
-    Affine p = pts[v & ~MSM_NEG];
     if (v & MSM_NEG) p.y = Fq::sub(u256_zero(), p.y);
     acc = G1::madd(acc, p);
   }
