@@ -12,8 +12,9 @@
 //      number of additions whatever the bucket sizes); runs that cross a chunk boundary
 //      leave partial sums, which msm_chunk_join adds up (one thread per bucket that starts
 //      in a chunk and ends in a later one)
-//   5. msm_window_reduce: per window, 256 segments of 256 buckets; running sums give
-//      sum_k (k-a) B_k and sum_k B_k per segment, + a * (segment sum), LDS tree
+//   5. msm_segments + msm_window_reduce: per window, segments of 8 buckets; running sums
+//      give sum (j-a+1) B_j and sum B_j per segment, + a * (segment sum); the segment
+//      shares are summed by LDS trees over (window, part) workgroups, then per window
 //   6. host: Horner over the 16 window sums (2^16 steps), one inversion to affine.
 // The result is a group element, so the canonical affine output is unique.
 #include <hipcub/hipcub.hpp>
@@ -192,19 +193,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) m
   shares[id] = (a == 0) ? wsum : G1::add(wsum, G1::mul_small(running, a));
 }
 
-__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz* shares, Xyzz* sums) {
+// tree sum of `count` points (count <= MSM_SEG_THREADS) into out
+__device__ __forceinline__ void msm_tree_sum(const Xyzz* in, uint32_t count, Xyzz* out) {
   __shared__ Xyzz red[MSM_SEG_THREADS];
-  const uint32_t w = blockIdx.x, t = threadIdx.x;
-  const Xyzz* S = shares + (uint64_t)w * MSM_NSEG;
-  Xyzz acc = G1::identity();
-  for (uint32_t i = t; i < MSM_NSEG; i += MSM_SEG_THREADS) acc = G1::add(acc, S[i]);
-  red[t] = acc;
+  const uint32_t t = threadIdx.x;
+  red[t] = t < count ? in[t] : G1::identity();
   __syncthreads();
   for (uint32_t st = MSM_SEG_THREADS / 2; st > 0; st >>= 1) {
     if (t < st) red[t] = G1::add(red[t], red[t + st]);
     __syncthreads();
   }
-  if (t == 0) sums[w] = red[0];
+  if (t == 0) *out = red[0];
+}
+constexpr uint32_t MSM_NPART = MSM_NSEG / MSM_SEG_THREADS;  // partial sums per window
+static_assert(MSM_NSEG % MSM_SEG_THREADS == 0 && MSM_NPART <= MSM_SEG_THREADS, "reduction shape");
+
+// workgroup (window, part): the tree sum of MSM_SEG_THREADS segment shares
+__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz* shares, Xyzz* parts) {
+  msm_tree_sum(shares + (uint64_t)blockIdx.x * MSM_SEG_THREADS, MSM_SEG_THREADS, parts + blockIdx.x);
+}
+// workgroup w: the window sum from its MSM_NPART partial sums
+__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* parts, Xyzz* sums) {
+  msm_tree_sum(parts + (uint64_t)blockIdx.x * MSM_NPART, MSM_NPART, sums + blockIdx.x);
 }
 
 // out_i = s_i * G (affine, canonical); scalars canonical Fr, 4 x u64 each
@@ -237,7 +247,8 @@ static uint64_t grid1(uint64_t count) {
 }
 
 struct MsmWork {
-  DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &temp, &head, &tail;
+  DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &temp, &head, &tail,
+      &parts;
 };
 
 // scratch owned by the context (freed with it)
@@ -245,7 +256,7 @@ static MsmWork msm_work(pbf_ctx* ctx) {
   return MsmWork{ctx->buf("msm.pts"),     ctx->buf("msm.inf"),    ctx->buf("msm.keys"),   ctx->buf("msm.vals"),
                  ctx->buf("msm.keys2"),   ctx->buf("msm.vals2"),  ctx->buf("msm.start"),  ctx->buf("msm.end"),
                  ctx->buf("msm.buckets"), ctx->buf("msm.shares"), ctx->buf("msm.sums"),   ctx->buf("msm.temp"),
-                 ctx->buf("msm.head"),    ctx->buf("msm.tail")};
+                 ctx->buf("msm.head"),    ctx->buf("msm.tail"),   ctx->buf("msm.parts")};
 }
 
 // Enqueue the device part; window sums land in w.sums (MSM_NW Xyzz, Montgomery).
@@ -259,7 +270,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
       (rc = w.start.ensure((uint64_t)MSM_NW * MSM_NB * 4)) || (rc = w.end.ensure((uint64_t)MSM_NW * MSM_NB * 4)) ||
       (rc = w.buckets.ensure((uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz))) ||
       (rc = w.shares.ensure((uint64_t)MSM_NW * MSM_NSEG * sizeof(Xyzz))) ||
-      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))) ||
+      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))) || (rc = w.parts.ensure(MSM_NW * MSM_NPART * sizeof(Xyzz))) ||
       (rc = w.head.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))) ||
       (rc = w.tail.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))))
     return rc;
@@ -291,7 +302,9 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
                      (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p);
   hipLaunchKernelGGL(msm_segments, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
                      (Xyzz*)w.shares.p);
-  hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.shares.p,
+  hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW * MSM_NPART), dim3(MSM_SEG_THREADS), 0, s,
+                     (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
+  hipLaunchKernelGGL(msm_window_final, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.parts.p,
                      (Xyzz*)w.sums.p);
   PBF_HIP(hipGetLastError());
   return 0;
