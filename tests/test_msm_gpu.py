@@ -78,3 +78,52 @@ def test_msm_config4_discrete_log_identity(ctx):
     got = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n, stream=st)
     z = sum(a * b for a, b in zip(si, ti)) % R
     assert got == enc(bn254.g1_mul(bn254.G1_GEN, z))
+
+
+def _dlog_msm(ctx, t_ints, s_ints):
+    """MSM of P_i = t_i G with scalars s_i, checked against (sum s_i t_i) G."""
+    import torch
+
+    n = len(t_ints)
+    t = np.array([[(x >> (64 * k)) & ((1 << 64) - 1) for k in range(4)] for x in t_ints], dtype=np.uint64)
+    s = np.array([[(x >> (64 * k)) & ((1 << 64) - 1) for k in range(4)] for x in s_ints], dtype=np.uint64)
+    dt = torch.from_numpy(t.reshape(-1).view(np.int64)).cuda()
+    ds = torch.from_numpy(s.reshape(-1).view(np.int64)).cuda()
+    dp = torch.empty(n * 8, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ctx.g1_mul_base_dev(dt.data_ptr(), dp.data_ptr(), n, stream=st)
+    torch.cuda.synchronize()
+    got = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n, stream=st)
+    z = sum(a * b for a, b in zip(s_ints, t_ints)) % R
+    return got == enc(bn254.g1_mul(bn254.G1_GEN, z) if z else None)
+
+
+@pytest.mark.parametrize("kind", ["equal", "digit_edges", "sparse", "chunk_sizes"])
+def test_msm_bucket_chunking_and_signed_digits(ctx, kind):
+    """Load-balanced accumulation (csrc/msm.hip msm_chunk_acc / msm_chunk_join) and the
+    signed-digit recoding: buckets spanning many 32-entry chunks, digits at the recoding
+    boundaries (0x7fff, 0x8000, 0x8001, 0xffff carry chains), mostly-zero windows, and sizes
+    around the chunk length."""
+    rnd = random.Random(hash(kind) & 0xFFFF)
+    if kind == "equal":  # one bucket per window holding all n points (spans n/32 chunks)
+        n = 5000
+        c = rnd.randrange(R)
+        sc = [c] * n
+    elif kind == "digit_edges":
+        n = 3000
+        digs = [0x7FFF, 0x8000, 0x8001, 0xFFFF, 0x0001, 0x0000]
+        sc = []
+        for _ in range(n):
+            v = sum(rnd.choice(digs) << (16 * w) for w in range(16))
+            sc.append(v % R)
+    elif kind == "sparse":  # a few nonzero windows, many equal buckets
+        n = 4000
+        sc = [(rnd.randrange(1, 4) << (16 * rnd.randrange(16))) % R for _ in range(n)]
+    else:
+        for n in (31, 32, 33, 63, 64, 65, 97):
+            t = [rnd.randrange(1, R) for _ in range(n)]
+            s = [rnd.randrange(R) for _ in range(n)]
+            assert _dlog_msm(ctx, t, s), n
+        return
+    t = [rnd.randrange(1, R) for _ in range(n)]
+    assert _dlog_msm(ctx, t, sc)
