@@ -414,25 +414,63 @@ static GlPassFn gl_fn_blk(int logr, bool first) {
 
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log);
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
 
-// Polynomials in groups of G (PBF_NTT_GROUP): all passes of one group before the next, so
-// a group's intermediate stays in the 256 MB Infinity Cache between its passes.
+// extra streams of the multi-stream group schedule (PBF_NTT_STREAMS), per device
+constexpr int GL_MAX_STREAMS = 8;
+static hipStream_t aux_stream(int i) {
+  static std::map<std::pair<int, int>, hipStream_t> m;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  auto key = std::make_pair(dev, i);
+  auto it = m.find(key);
+  if (it != m.end()) return it->second;
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  m[key] = st;
+  return st;
+}
+
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log) {
-  size_t G = batch;
+  // default schedule (measured best at 2^20 x 32): groups of 4
+  // polynomials alternating over two streams once the batch has at least 8
+  size_t G = batch >= 8 ? 4 : batch;
   if (const char* g = getenv("PBF_NTT_GROUP")) G = (size_t)atoll(g);
   if (split_log != 0 || G == 0 || G >= batch) return run_gl_group(p, d_in, d_out, batch, s0, s1, stream, split_log);
-  for (size_t g0 = 0; g0 < batch; g0 += G) {
+  // PBF_NTT_STREAMS=k: groups round-robin over the caller's stream and k-1 more (disjoint
+  // scratch), so the passes of k groups run concurrently and their phases interleave
+  int ns = getenv("PBF_NTT_STREAMS") ? atoi(getenv("PBF_NTT_STREAMS")) : 2;
+  ns = ns < 1 ? 1 : (ns > GL_MAX_STREAMS ? GL_MAX_STREAMS : ns);
+  hipStream_t sts[GL_MAX_STREAMS];
+  sts[0] = stream;
+  for (int i = 1; i < ns; ++i)
+    if (!(sts[i] = aux_stream(i))) return fail(1, "stream creation failed");
+  hipEvent_t ev = nullptr;
+  if (ns > 1) {
+    PBF_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    PBF_HIP(hipEventRecord(ev, stream));
+    for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], ev, 0));
+  }
+  int gi = 0;
+  for (size_t g0 = 0; g0 < batch; g0 += G, ++gi) {
     const size_t b = batch - g0 < G ? batch - g0 : G;
-    const int rc = run_gl_group(p, d_in + g0 * p.n, d_out + g0 * p.n, b, s0, s1, stream, 0);
+    const int rc = run_gl_group(p, d_in + g0 * p.n, d_out + g0 * p.n, b, s0, s1, sts[gi % ns], 0,
+                                ns > 1 ? g0 * p.n : 0);
     if (rc) return rc;
+  }
+  if (ns > 1) {
+    for (int i = 1; i < ns; ++i) {
+      PBF_HIP(hipEventRecord(ev, sts[i]));
+      PBF_HIP(hipStreamWaitEvent(stream, ev, 0));
+    }
+    PBF_HIP(hipEventDestroy(ev));
   }
   return 0;
 }
 
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log) {
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff) {
   const size_t P = p.logr.size();
   // two-pass plans with equal tile widths may keep the intermediate blocked (ntt_gl.hpp BLK)
   bool blk = false;
@@ -459,8 +497,8 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     const uint64_t W = (uint64_t)tile >> lr;
     if ((p.n >> lr) % W) return fail(1, "transform too small for the pass tile");
     GlPassArgs a;
-    a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p);
-    a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p);
+    a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p) + soff;
+    a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p) + soff;
     a.twpass = (const uint64_t*)p.twpass[i]->p;
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;

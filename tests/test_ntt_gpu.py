@@ -136,7 +136,9 @@ def test_batch_dev_matches_single(ctx):
 
 
 @pytest.mark.parametrize("env", [{"PBF_NTT_BLK": "1"}, {"PBF_NTT_PERSIST": "1"}, {"PBF_NTT_GROUP": "2"},
-                                 {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"}, {"PBF_NTT_NO_KMAJOR": "1"}])
+                                 {"PBF_NTT_GROUP": "1", "PBF_NTT_STREAMS": "3"}, {"PBF_NTT_STREAMS": "1"},
+                                 {"PBF_NTT_GROUP": "0"}, {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"},
+                                 {"PBF_NTT_NO_KMAJOR": "1"}])
 @pytest.mark.parametrize("logn", [16, 20])
 def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     """Every opt-in schedule of the Goldilocks pass kernel (blocked intermediate, persistent
@@ -146,7 +148,7 @@ def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
 
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    n, batch = 1 << logn, 3
+    n, batch = 1 << logn, (9 if logn == 16 else 3)  # 9: the default 4-polynomial groups, 2 streams
     w = root(GOLD, n)
     host = np.stack([oracle.splitmix_field(GOLD, 700 + i, n) for i in range(batch)])
     d_in = torch.from_numpy(host.view(np.int64)).cuda()
