@@ -66,29 +66,42 @@ static uint32_t blocks_for(uint64_t threads) {
   return (uint32_t)(b ? b : 1);
 }
 
-// out[i] = i < len ? in[i] * base^(i + off) : 0, i < count (coset scaling, zero padding;
-// base = 1 plain copy). Chunks of PV_CHUNK consecutive elements per thread.
+// Chunked kernels: the wave of thread t owns 64 * PV_CHUNK consecutive elements and lane l
+// takes i = first + 64 k (k < PV_CHUNK), so every load and store instruction of the wave
+// touches consecutive elements; a running power steps by base^64.
+__device__ __forceinline__ uint64_t chunk_first(uint64_t t) { return (t / 64) * 64 * PV_CHUNK + (t % 64); }
+__device__ __forceinline__ U256 pow64(U256 b) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) b = Fr::mul(b, b);
+  return b;
+}
+
+// out[i] = i < len ? in[i] * base^(i + off) : 0, i < count (coset scaling, zero padding).
+// The product of a canonical value and a Montgomery-form power is the canonical product
+// (a * xR * R^-1), so the element needs no conversions.
 __global__ void k_scale_pow(const uint64_t* in, uint64_t len, uint64_t* out, uint64_t count, U256 base, uint64_t off) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = t * PV_CHUNK;
+  const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
   U256 x = fr_pow(base, i0 + off);
-  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < count; ++i) {
-    if (i < len) str(out + 4 * i, Fr::mul(ldr(in + 4 * i), x));
-    else for (int k = 0; k < 4; ++k) out[4 * i + k] = 0;
-    x = Fr::mul(x, base);
+  const U256 step = pow64(base);
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
+    if (i < len) u256_to_u64(Fr::mul(u256_from_u64(in + 4 * i), x), out + 4 * i);
+    else for (int j = 0; j < 4; ++j) out[4 * i + j] = 0;
+    x = Fr::mul(x, step);
   }
 }
 
 // out[i] = start * base^i
 __global__ void k_powers(uint64_t* out, uint64_t count, U256 base, U256 start) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = t * PV_CHUNK;
+  const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
   U256 x = Fr::mul(start, fr_pow(base, i0));
-  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < count; ++i) {
+  const U256 step = pow64(base);
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     str(out + 4 * i, x);
-    x = Fr::mul(x, base);
+    x = Fr::mul(x, step);
   }
 }
 
@@ -285,10 +298,11 @@ struct QuotArgs {
 };
 __global__ void k_quotient(QuotArgs q, uint64_t* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = t * PV_CHUNK;
+  const uint64_t i0 = chunk_first(t);
   if (i0 >= q.N) return;
   U256 x = Fr::mul(q.g, fr_pow(q.wN, i0));
-  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < q.N; ++i, x = Fr::mul(x, q.wN)) {
+  const U256 step = pow64(q.wN);
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < q.N; ++k, i += 64, x = Fr::mul(x, step)) {
     const uint64_t o = 4 * i;
     const U256 a = ldr(q.a + o), b = ldr(q.b + o), c = ldr(q.c + o), z = ldr(q.z + o);
     const U256 zw = ldr(q.z + 4 * ((i + 4) % q.N));  // z(w x_i): w = w_N^4
@@ -319,10 +333,12 @@ __global__ void k_quotient(QuotArgs q, uint64_t* out) {
 // out[i] = (P(x_i) - y) / (x_i - z) on the coset, inv_xz[i] = 1/(x_i - z) precomputed
 __global__ void k_coset_minus(uint64_t* out, uint64_t N, U256 g, U256 wN, U256 zpt) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = t * PV_CHUNK;
+  const uint64_t i0 = chunk_first(t);
   if (i0 >= N) return;
   U256 x = Fr::mul(g, fr_pow(wN, i0));
-  for (uint64_t i = i0; i < i0 + PV_CHUNK && i < N; ++i, x = Fr::mul(x, wN)) str(out + 4 * i, Fr::sub(x, zpt));
+  const U256 step = pow64(wN);
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < N; ++k, i += 64, x = Fr::mul(x, step))
+    str(out + 4 * i, Fr::sub(x, zpt));
 }
 __global__ void k_sub_mul(const uint64_t* p, U256 y, const uint64_t* inv, uint64_t* out, uint64_t N) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
