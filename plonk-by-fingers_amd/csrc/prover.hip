@@ -666,8 +666,12 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     if (cmap[k] == -1) { src = zx; len = n + 3; }
     else if (cmap[k] == -2) { src = (const uint64_t*)B.tmp0.p; len = n; }
     else { src = C(cmap[k]); len = cmap[k] < 3 ? n + 2 : n; }
-    if ((rc = P.coset_ntt(src, len, CE(k)))) return rc;
+    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, src, len,
+                       CE(k), N, P.g, (uint64_t)0);
+    PBF_HIP(hipGetLastError());
   }
+  // the 13 coset slots are contiguous: one batched NTT (fuller GPU, one plan lookup)
+  if ((rc = P.ntt(P.wN_plain, CE(0), CE(0), N, 13, 0))) return rc;
   P.mark("round 3 coset NTTs (13)");
   QuotArgs qa;
   qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
