@@ -48,7 +48,9 @@ def calibration(src):
     return cal
 
 
-def main(tag="r01", log_n=20, batch=32):
+def main(tag="r01", log_n=20, batch=32, steps=12):
+    """steps: bench steps the profiled command ran (profile_round.sh: 10 timed + 2 warm-up);
+    a kernel dispatched more than once per step (the grouped schedule) is summed per step."""
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -68,11 +70,16 @@ def main(tag="r01", log_n=20, batch=32):
     assert ntt, list(summ)
     fk = cal["FETCH_SIZE"] if cal else 2.0 * 1024  # uncalibrated: the guide's 16-B-lane factor
     wk = cal["WRITE_SIZE"] if cal else 1024
-    per = {k: {"fetch_bytes": summ[k]["FETCH_SIZE"]["mean"] * fk, "write_bytes": summ[k]["WRITE_SIZE"]["mean"] * wk}
-           for k in ntt}
+    per = {}
+    for k in ntt:
+        per_step = summ[k]["FETCH_SIZE"]["dispatches"] / steps  # dispatches of this kernel per step
+        per[k] = {"dispatches_per_step": per_step,
+                  "fetch_bytes": summ[k]["FETCH_SIZE"]["mean"] * fk * per_step,
+                  "write_bytes": summ[k]["WRITE_SIZE"]["mean"] * wk * per_step}
     data = (1 << log_n) * batch * 8
     hbm = sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values())
     out = {"kernels": per, "log_n": log_n, "batch": batch, "passes_per_step": len(ntt),
+           "note": "bytes per bench step (all dispatches of each pass kernel in one step)",
            "fetch_vs_input": {k: v["fetch_bytes"] / data for k, v in per.items()},
            "write_vs_output": {k: v["write_bytes"] / data for k, v in per.items()},
            "calibration_bytes_per_kib": {"FETCH_SIZE": fk, "WRITE_SIZE": wk, "kernel": CAL_KERNEL if cal else None},
