@@ -79,6 +79,24 @@ int pbf_mul_ntt_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const uint64
 int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, size_t n,
                       const uint64_t* xs, size_t nx, uint64_t* ys);
 
+/* ---- Poly arithmetic (poly.rs:165-247) -----------------------------------------------
+ * Results normalised as Poly::normalize (poly.rs:96-105): trailing zeros stripped, at least
+ * one coefficient; *lout / *lq / *lr receive the lengths. Inputs: >= 1 coefficient each.
+ * pbf_poly_add_u64 / pbf_poly_sub_u64: AddAssign / SubAssign<&Poly> (poly.rs:165-176,
+ *   192-203); `out` holds max(la, lb). Subtraction keeps the reference's quirk: where only
+ *   b has a coefficient it is appended as +b[i] (poly.rs:196).
+ * pbf_poly_div_u64: Div for Poly (poly.rs:230-247), num = q * den + r, deg r < deg den,
+ *   computed in O(n log n) (reversed-series inverse by Newton's iteration, NTT products);
+ *   `root` has multiplicative order 2^root_log and bounds the NTT sizes (Goldilocks:
+ *   7^((p-1)/2^32), 32). q holds >= nn, r >= nn coefficients. PBF_ENOINV when the divisor's
+ *   leading coefficient has no inverse (the reference's unwrap at poly.rs:238).         */
+int pbf_poly_add_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* a, size_t la, const uint64_t* b, size_t lb,
+                     uint64_t* out, size_t* lout);
+int pbf_poly_sub_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* a, size_t la, const uint64_t* b, size_t lb,
+                     uint64_t* out, size_t* lout);
+int pbf_poly_div_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t root, uint32_t root_log, const uint64_t* num,
+                     size_t nn, const uint64_t* den, size_t nd, uint64_t* q, size_t* lq, uint64_t* r, size_t* lr);
+
 /* ---- multi-GPU stride-sharded NTT ---------------------------
  * A transform of N = G * nl points (G = world size 2, 4 or 8; omega of order N) is
  * sharded by coefficient stride: rank g holds a[g + G*m], m < nl, for `batch`

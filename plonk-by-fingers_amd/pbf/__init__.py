@@ -47,6 +47,10 @@ SIGNATURES = [
     ("pbf_ntt_u64_batch_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
     ("pbf_mul_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
     ("pbf_poly_eval_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_poly_add_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64, ctypes.POINTER(_sz)]),
+    ("pbf_poly_sub_u64", ctypes.c_int, [_vp, _u64, _p64, _sz, _p64, _sz, _p64, ctypes.POINTER(_sz)]),
+    ("pbf_poly_div_u64", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _p64, _sz, _p64, _sz, _p64,
+                                        ctypes.POINTER(_sz), _p64, ctypes.POINTER(_sz)]),
     ("pbf_fill_random_u64_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _sz, _vp]),
     ("pbf_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _p64, _sz, ctypes.c_int]),
     ("pbf_ntt_fr256_batch_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
@@ -177,6 +181,32 @@ class Context:
         y = np.empty_like(x)
         _check(self.lib.pbf_poly_eval_u64(self.h, modulus, _ptr(c), c.size, _ptr(x), x.size, _ptr(y)))
         return y
+
+    # poly.rs:165-203 AddAssign / SubAssign<&Poly> (normalised; sub keeps the :196 quirk)
+    def poly_add(self, modulus: int, a, b) -> np.ndarray:
+        return self._addsub(self.lib.pbf_poly_add_u64, modulus, a, b)
+
+    def poly_sub(self, modulus: int, a, b) -> np.ndarray:
+        return self._addsub(self.lib.pbf_poly_sub_u64, modulus, a, b)
+
+    def _addsub(self, fn, modulus, a, b):
+        x, y = _as_u64(a), _as_u64(b)
+        out = np.empty(max(x.size, y.size), dtype=np.uint64)
+        ln = _sz()
+        _check(fn(self.h, modulus, _ptr(x), x.size, _ptr(y), y.size, _ptr(out), ctypes.byref(ln)))
+        return out[: ln.value].copy()
+
+    # poly.rs:230-247 Div for Poly -> (q, r); `root` of order 2^root_log bounds the NTT sizes
+    def poly_div(self, modulus: int, num, den, root: int | None = None, root_log: int | None = None):
+        if root is None:
+            root, root_log = default_root(modulus)
+        n, d = _as_u64(num), _as_u64(den)
+        q = np.empty(max(n.size, 1), dtype=np.uint64)
+        r = np.empty(max(n.size, 1), dtype=np.uint64)
+        lq, lr = _sz(), _sz()
+        _check(self.lib.pbf_poly_div_u64(self.h, modulus, root, root_log, _ptr(n), n.size, _ptr(d), d.size, _ptr(q),
+                                         ctypes.byref(lq), _ptr(r), ctypes.byref(lr)))
+        return q[: lq.value].copy(), r[: lr.value].copy()
 
     # multi-GPU stride-sharded NTT pieces (include/pbf.h)
     def shard_local_dev(self, modulus: int, omega: int, world: int, d_in: int, d_out: int, nl: int, batch: int,
@@ -358,6 +388,19 @@ class Context:
     def fill_random_dev(self, modulus: int, seed: int, d_out: int, count: int, stream: int = 0) -> None:
         _check(self.lib.pbf_fill_random_u64_dev(self.h, modulus, seed, _vp(d_out), count,
                                                 _vp(stream) if stream else None))
+
+
+Q32 = 3221225473  # 3 * 2^30 + 1 (the reference-literal cross-check prime)
+
+
+def default_root(modulus: int):
+    """(root, log2 of its order) of a maximal 2-power root of unity for the supported NTT
+    primes: Goldilocks (generator 7, 2-adicity 32) and q32 (generator 5, 2-adicity 30)."""
+    if modulus == GOLDILOCKS:
+        return pow(7, (modulus - 1) >> 32, modulus), 32
+    if modulus == Q32:
+        return pow(5, (modulus - 1) >> 30, modulus), 30
+    raise ValueError("pass root and root_log for this modulus")
 
 
 BN254_R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
