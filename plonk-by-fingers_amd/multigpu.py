@@ -127,3 +127,48 @@ class BenchSharded:
 
     def step(self):
         self.nt.forward(self.shard, self.out)
+
+
+class GpuMsmOps:
+    """The MSM of csrc/msm.hip on device-resident ranges, and the sum of G affine points as an
+    MSM with unit scalars (the identity encodes as (0, 0))."""
+
+    def __init__(self, ctx, stream: int = 0):
+        self.ctx, self.stream = ctx, stream
+
+    def partial(self, d_points: int, d_scalars: int, count: int) -> tuple:
+        return self.ctx.msm_g1_dev(d_points, d_scalars, count, stream=self.stream) if count else (0, 0)
+
+    def combine(self, points) -> tuple:
+        return self.ctx.msm_g1(points, [1] * len(points))
+
+
+class ShardedMsm:
+    """Multi-GPU G1 MSM (independent point ranges). Rank r owns points and
+    scalars [start, end) of split(n, G, r) in HBM and runs its MSM locally; the G partial
+    sums (affine, 8 u64 each) are all-gathered and added on every rank. One collective of
+    G x 64 B; no other traffic."""
+
+    def __init__(self, ops, comm, rank: int, world: int, device: str | torch.device = "cuda"):
+        self.ops, self.comm, self.rank, self.world, self.device = ops, comm, rank, world, device
+
+    @staticmethod
+    def split(n: int, world: int, rank: int):
+        """[start, end) of rank's point range (the first n % world ranks take one more)."""
+        base, extra = divmod(n, world)
+        start = rank * base + min(rank, extra)
+        return start, start + base + (1 if rank < extra else 0)
+
+    def msm(self, points, scalars, count: int) -> tuple:
+        """The MSM of the whole point set, on every rank, from this rank's `count` points."""
+        x, y = self.ops.partial(points, scalars, count)
+        m = (1 << 64) - 1
+        limbs = [(v >> (64 * k)) & m for v in (x, y) for k in range(4)]
+        mine = torch.tensor([v - (1 << 64) if v >> 63 else v for v in limbs], dtype=torch.int64, device=self.device)
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        self.comm.all_gather(parts, mine)
+        pts = []
+        for p in parts:
+            u = [int(v) & m for v in p.cpu().tolist()]
+            pts.append((sum(u[k] << (64 * k) for k in range(4)), sum(u[4 + k] << (64 * k) for k in range(4))))
+        return self.ops.combine(pts)

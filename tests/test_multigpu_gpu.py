@@ -98,3 +98,30 @@ def test_shard_errors(ctx):
     w128 = pow(7, (GOLD - 1) // 128, GOLD)
     with pytest.raises(pbf.PbfError):
         ctx.shard_combine_dev(GOLD, w128, 2, 0, d.data_ptr(), d.data_ptr(), 64, 1)  # in == out
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_sharded_msm_ranges_gpu(ctx, G):
+    """Point-range MSM sharding (multigpu.ShardedMsm) with the real kernels: G virtual ranks
+    on one GPU, each a partial MSM of its range, the partial sums combined by GpuMsmOps —
+    equal to the MSM of the whole set (the pieces bench.py runs one per GPU)."""
+    import bn254
+    import torch
+    from multigpu import GpuMsmOps, ShardedMsm
+
+    n = 5000
+    t = bn254.random_limbs(n, 811)
+    s = bn254.random_limbs(n, 812)
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    ds = torch.from_numpy(s.view(np.int64)).cuda()
+    dp = torch.empty(n * 8, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ctx.g1_mul_base_dev(dt.data_ptr(), dp.data_ptr(), n, stream=st)
+    torch.cuda.synchronize()
+    ops = GpuMsmOps(ctx, st)
+    parts = []
+    for r in range(G):
+        a, b = ShardedMsm.split(n, G, r)
+        parts.append(ops.partial(dp[8 * a:].data_ptr(), ds[4 * a:].data_ptr(), b - a))
+    full = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n, stream=st)
+    assert ops.combine(parts) == full
