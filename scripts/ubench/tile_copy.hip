@@ -101,5 +101,9 @@ int main() {
   run<3, 16, 1>("strided W=16 both sides, 8B", in, out, n, batch);
   run<3, 16, 2>("strided W=16 both sides, 16B", in, out, n, batch);
   run<3, 32, 2>("strided W=32 both sides, 16B", in, out, n, batch);
+  run<2, 4, 1>("strided W=4 load + LDS + contiguous store, 8B", in, out, n, batch);
+  run<3, 4, 1>("strided W=4 both sides, 8B", in, out, n, batch);
+  run<3, 4, 2>("strided W=4 both sides, 16B", in, out, n, batch);
+  run<2, 4, 2>("strided W=4 load + LDS + contiguous store, 16B", in, out, n, batch);
   return 0;
 }
