@@ -217,7 +217,51 @@ __global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* 
   msm_tree_sum(parts + (uint64_t)blockIdx.x * MSM_NPART, MSM_NPART, sums + blockIdx.x);
 }
 
-// out_i = s_i * G (affine, canonical); scalars canonical Fr, 4 x u64 each
+// Fixed-base comb for s * G (SRS::create): table[w][d-1] = d * 2^(8w) * G (affine,
+// Montgomery), 32 byte windows x 255 digits (510 KiB, L2-resident); a scalar costs at most
+// 32 mixed additions and no doublings (double-and-add: 256 doublings + ~128 additions).
+constexpr int G1_TBL_W = 32, G1_TBL_D = 255;
+__global__ void __launch_bounds__(256) g1_base_table_kernel(Affine* table) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= G1_TBL_W * G1_TBL_D) return;
+  const uint32_t w = id / G1_TBL_D, d = id % G1_TBL_D + 1;
+  Affine g;
+  {
+    U256 one = Fq::one_plain(), two = Fq::one_plain();
+    two.w[0] = 2;
+    g.x = Fq::to_mont(one);
+    g.y = Fq::to_mont(two);
+  }
+  Xyzz acc = G1::identity();
+  for (int b = 7; b >= 0; --b) {
+    acc = G1::dbl(acc);
+    if ((d >> b) & 1) acc = G1::madd(acc, g);
+  }
+  for (uint32_t i = 0; i < 8 * w; ++i) acc = G1::dbl(acc);
+  U256 x, y;
+  G1::to_affine_plain(acc, &x, &y);  // d 2^(8w) < r: never the identity
+  table[id].x = Fq::to_mont(x);
+  table[id].y = Fq::to_mont(y);
+}
+__global__ void __launch_bounds__(256) g1_mul_base_comb(const uint64_t* scalars, const Affine* table, uint64_t* out,
+                                                        uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = scalars + 4 * i;
+    Xyzz acc = G1::identity();
+#pragma unroll 4
+    for (int w = 0; w < G1_TBL_W; ++w) {
+      const uint32_t d = (uint32_t)(s[w >> 3] >> (8 * (w & 7))) & 0xFF;
+      if (d) acc = G1::madd(acc, table[w * G1_TBL_D + d - 1]);
+    }
+    U256 x, y;
+    G1::to_affine_plain(acc, &x, &y);
+    store_u256(out + 8 * i, x);
+    store_u256(out + 8 * i + 4, y);
+  }
+}
+
+// out_i = s_i * G (affine, canonical); scalars canonical Fr, 4 x u64 each (double-and-add;
+// kept as the reference for the comb)
 __global__ void __launch_bounds__(256) g1_mul_base_kernel(const uint64_t* scalars, uint64_t* out, uint64_t n) {
   Affine g;
   {
@@ -384,7 +428,21 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
 int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t* d_out, size_t n, void* stream) {
   if (!ctx || (n && (!d_scalars || !d_out))) return fail(PBF_EINVAL, "null argument");
   if (n == 0) return PBF_OK;
-  hipLaunchKernelGGL(g1_mul_base_kernel, dim3(grid1(n)), dim3(256), 0, (hipStream_t)stream, d_scalars, d_out,
+  hipStream_t st = (hipStream_t)stream;
+  if (getenv("PBF_G1_DOUBLE_AND_ADD")) {  // A/B and cross-check of the comb
+    hipLaunchKernelGGL(g1_mul_base_kernel, dim3(grid1(n)), dim3(256), 0, st, d_scalars, d_out, (uint64_t)n);
+    PBF_HIP(hipGetLastError());
+    return PBF_OK;
+  }
+  DevBuf& tbl = ctx->buf("g1.base_table");
+  if (tbl.bytes == 0) {  // built once per context
+    int rc = tbl.ensure((size_t)G1_TBL_W * G1_TBL_D * sizeof(Affine));
+    if (rc) return rc;
+    hipLaunchKernelGGL(g1_base_table_kernel, dim3((G1_TBL_W * G1_TBL_D + 255) / 256), dim3(256), 0, st,
+                       (Affine*)tbl.p);
+    PBF_HIP(hipGetLastError());
+  }
+  hipLaunchKernelGGL(g1_mul_base_comb, dim3(grid1(n)), dim3(256), 0, st, d_scalars, (const Affine*)tbl.p, d_out,
                      (uint64_t)n);
   PBF_HIP(hipGetLastError());
   return PBF_OK;

@@ -127,3 +127,26 @@ def test_msm_bucket_chunking_and_signed_digits(ctx, kind):
         return
     t = [rnd.randrange(1, R) for _ in range(n)]
     assert _dlog_msm(ctx, t, sc)
+
+
+def test_fixed_base_comb_matches_double_and_add(ctx, monkeypatch):
+    """The byte-window comb of pbf_g1_bn254_mul_base_dev (SRS::create) against the plain
+    double-and-add kernel, including zero bytes, 0xff bytes, 0 and r - 1."""
+    import torch
+
+    n = 4096
+    t = bn254.random_limbs(n, 901)
+    t[0:4] = 0
+    t[4:8] = [0xFFFFFFFFFFFFFFFF, 0xFF00FF00FF00FF00, 0x00FF00FF00FF00FF, 0x0FFFFFFFFFFFFFFF]
+    rm1 = R - 1
+    t[8:12] = [(rm1 >> (64 * k)) & ((1 << 64) - 1) for k in range(4)]
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    a = torch.empty(n * 8, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    ctx.g1_mul_base_dev(dt.data_ptr(), a.data_ptr(), n, stream=st)
+    monkeypatch.setenv("PBF_G1_DOUBLE_AND_ADD", "1")
+    ctx.g1_mul_base_dev(dt.data_ptr(), b.data_ptr(), n, stream=st)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert a[:8].tolist() == [0] * 8  # 0 * G = identity
