@@ -91,7 +91,16 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
   }
 }
 
-constexpr uint32_t MSM_CH = 32;  // sorted entries per accumulation thread
+#ifndef PBF_MSM_CH
+#define PBF_MSM_CH 32
+#endif
+#ifndef PBF_MSM_ACC_WPE
+#define PBF_MSM_ACC_WPE 3
+#endif
+#ifndef PBF_MSM_SEG_WPE
+#define PBF_MSM_SEG_WPE 1
+#endif
+constexpr uint32_t MSM_CH = PBF_MSM_CH;  // sorted entries per accumulation thread
 
 struct ChunkPart {
   Xyzz acc;
@@ -103,7 +112,7 @@ struct ChunkPart {
 // (the whole bucket inside the chunk) are written to their bucket. head[t]: the first run
 // if its bucket started in an earlier chunk; tail[t]: the last run if its bucket starts in
 // this chunk and ends in a later one. Buckets with no entry stay zero (ZZ = 0: identity).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE))) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
                                                      const uint32_t* start, const uint32_t* end, uint32_t m,
                                                      Xyzz* buckets, ChunkPart* head, ChunkPart* tail) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -176,10 +185,13 @@ __device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
 // MSM_SEG buckets starting at a): running sums give sum (j - a + 1) B_j and sum B_j, and
 // the segment's share is wsum + a * running. (b) one workgroup per window sums its segment
 // shares (sequential per thread, then an LDS tree).
-constexpr uint32_t MSM_SEG = 8;
+#ifndef PBF_MSM_SEG
+#define PBF_MSM_SEG 8
+#endif
+constexpr uint32_t MSM_SEG = PBF_MSM_SEG;
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) msm_segments(const Xyzz* buckets, Xyzz* shares) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_SEG_WPE))) msm_segments(const Xyzz* buckets, Xyzz* shares) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= MSM_NW * MSM_NSEG) return;
   const uint32_t w = id / MSM_NSEG, seg = id % MSM_NSEG;

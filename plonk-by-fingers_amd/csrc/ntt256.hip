@@ -171,7 +171,10 @@ __device__ __forceinline__ void stage256(U256* v, U256* lds, const U256* wq, con
 }
 
 template <int LOGR, int W, int NT, int LQ>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) ntt256_pass_kernel(Pass256 a) {
+#ifndef PBF_NTT256_WPE
+#define PBF_NTT256_WPE 4
+#endif
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PBF_NTT256_WPE))) ntt256_pass_kernel(Pass256 a) {
   constexpr int R = 1 << LOGR;
   constexpr int E = R * W;
   constexpr int PER = E / NT;

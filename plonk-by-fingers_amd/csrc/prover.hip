@@ -144,7 +144,7 @@ __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64
 }
 
 // round 2 terms (plonk.rs:282-297) for row j < n-1: num_j = dend, den_j = dsor
-__global__ void k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n, U256 beta,
+__global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n, U256 beta,
                              U256 gamma, U256 k1, U256 k2, uint64_t* num, uint64_t* den) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j + 1 >= n) return;
@@ -164,7 +164,7 @@ __global__ void k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const u
 // out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
 // chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297)
 constexpr int INV_CHUNK = 32;
-__global__ void k_div_batch(const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad) {
+__global__ void __launch_bounds__(256) k_div_batch(const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = t * INV_CHUNK;
   if (i0 >= count) return;
@@ -296,7 +296,7 @@ struct QuotArgs {
   U256 alpha, beta, gamma, k1, k2, alpha2, g, wN;
   U256 zh_inv[4];
 };
-__global__ void k_quotient(QuotArgs q, uint64_t* out) {
+__global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= q.N) return;

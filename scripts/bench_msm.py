@@ -1,4 +1,4 @@
-"""MSM probe (run under rocprofv3 for the per-kernel split): python scripts/bench_msm.py [log_n] [reps]"""
+"""MSM probe (PBF_LIB selects a variant build; prints a result hash to compare variants) (run under rocprofv3 for the per-kernel split): python scripts/bench_msm.py [log_n] [reps]"""
 import os
 import sys
 import time
@@ -22,7 +22,8 @@ def main(log_n=20, reps=5):
     pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
     ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m)
     torch.cuda.synchronize()
-    ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m)
+    r = ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m)
+    print("msm result hash", hex(hash(r) & 0xFFFFFFFF))
     t0 = time.perf_counter()
     for _ in range(reps):
         ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m)
