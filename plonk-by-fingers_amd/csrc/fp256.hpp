@@ -169,8 +169,72 @@ struct Fp256 {
     return reduce_once(r);
   }
 #else
-  // CIOS Montgomery product a*b*2^-256 mod p (host).
+  // -p^-1 mod 2^64 from the 32-bit constant's modulus by Newton's iteration (x <- x(2 - p x)
+  // doubles the correct low bits; p is odd so x = p is right mod 2^3)
+  static constexpr uint64_t np64() {
+    const uint64_t p0 = (uint64_t)Prm::P[0] | ((uint64_t)Prm::P[1] << 32);
+    uint64_t x = p0;
+    for (int i = 0; i < 6; ++i) x *= 2 - p0 * x;
+    return 0 - x;
+  }
+  // CIOS Montgomery product a*b*2^-256 mod p (host) over 4 x 64-bit limbs with 128-bit
+  // products: the MSM's host Horner over the window sums (~2600 products per MSM) runs
+  // ~2.3x faster than over 8 x 32-bit limbs (mul_cios32, kept as the cross-check;
+  // tests/native/fp256_host_check.hip).
   static U256 mul(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    typedef unsigned __int128 u128;
+    constexpr uint64_t NP = np64();
+    uint64_t x[4], y[4], p[4], t[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 4; ++i) {
+      x[i] = (uint64_t)a.w[2 * i] | ((uint64_t)a.w[2 * i + 1] << 32);
+      y[i] = (uint64_t)b.w[2 * i] | ((uint64_t)b.w[2 * i + 1] << 32);
+      p[i] = (uint64_t)Prm::P[2 * i] | ((uint64_t)Prm::P[2 * i + 1] << 32);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u128 s;
+      uint64_t C = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s = (u128)x[j] * y[i] + t[j] + C;
+        t[j] = (uint64_t)s;
+        C = (uint64_t)(s >> 64);
+      }
+      s = (u128)t[4] + C;
+      t[4] = (uint64_t)s;
+      t[5] = (uint64_t)(s >> 64);
+      const uint64_t m = t[0] * NP;
+      s = (u128)m * p[0] + t[0];
+      C = (uint64_t)(s >> 64);
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        s = (u128)m * p[j] + t[j] + C;
+        t[j - 1] = (uint64_t)s;
+        C = (uint64_t)(s >> 64);
+      }
+      s = (u128)t[4] + C;
+      t[3] = (uint64_t)s;
+      t[4] = t[5] + (uint64_t)(s >> 64);
+    }
+    // t < 2p: subtract p once unless that borrows (branch-free select)
+    uint64_t d[4], br = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const u128 v = (u128)t[i] - p[i] - br;
+      d[i] = (uint64_t)v;
+      br = (uint64_t)(v >> 64) & 1;
+    }
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t o = br ? t[i] : d[i];
+      r.w[2 * i] = (uint32_t)o;
+      r.w[2 * i + 1] = (uint32_t)(o >> 32);
+    }
+    return r;
+  }
+  // CIOS Montgomery product over 8 x 32-bit limbs (host cross-check of mul)
+  static U256 mul_cios32(const U256& a, const U256& b) {
     uint32_t t[10];
     for (int i = 0; i < 10; ++i) t[i] = 0;
     for (int i = 0; i < 8; ++i) {
