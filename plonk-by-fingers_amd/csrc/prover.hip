@@ -59,7 +59,10 @@ __device__ U256 fr_inv(const U256& a) {
   return r;
 }
 
-constexpr int PV_CHUNK = 64;  // elements per thread in the chunked kernels
+#ifndef PBF_PV_CHUNK
+#define PBF_PV_CHUNK 32
+#endif
+constexpr int PV_CHUNK = PBF_PV_CHUNK;  // elements per thread in the chunked kernels
 
 static uint32_t blocks_for(uint64_t threads) {
   uint64_t b = (threads + 255) / 256;
