@@ -166,7 +166,10 @@ __global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const u
 
 // out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
 // chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297)
-constexpr int INV_CHUNK = 32;
+#ifndef PBF_INV_CHUNK
+#define PBF_INV_CHUNK 32
+#endif
+constexpr int INV_CHUNK = PBF_INV_CHUNK;
 __global__ void __launch_bounds__(256) k_div_batch(const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = t * INV_CHUNK;
