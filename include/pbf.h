@@ -14,14 +14,20 @@
  *   - Vectors are natural order (fft.rs:98-104 writes o[i] / o[i+len/2]).
  *   - Host-pointer entry points are synchronous: copy in, compute, copy out, on
  *     the context's host stream. `_dev` entry points take device pointers and a
- *     hipStream_t (void*) and only enqueue work on exactly that stream (NULL = the
- *     HIP null stream, as everywhere in HIP).
+ *     hipStream_t (void*) and are stream-ordered on that stream (NULL = the HIP null
+ *     stream, as everywhere in HIP): their work starts after everything enqueued on
+ *     it before the call and finishes before anything enqueued after. Internally a
+ *     batched Goldilocks NTT of >= 8 polynomials (pbf_ntt_u64_batch_dev) forks half
+ *     its groups onto a stream private to the context (an event fork/join pair, also
+ *     the context's) and joins back before returning; nothing else is ever enqueued
+ *     on streams the caller did not pass.
  *   - Input and output may alias (in-place is allowed).
  *   - Supported moduli for the u64 entry points: Goldilocks p = 2^64-2^32+1, and any
  *     odd M < 2^32 (the range where the reference's `(a*b)%M` in u64 is exact,
  *     u64field.rs:177).
  *   - Errors are returned, never aborted on. pbf_last_error() gives the text.
- *   - One pbf_ctx per host thread; distinct contexts are independent.
+ *   - One pbf_ctx per host thread; distinct contexts are independent (no shared
+ *     streams, buffers or caches; every entry point selects the context's device).
  */
 #ifndef PBF_H
 #define PBF_H

@@ -70,6 +70,7 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
   PBF_HIP(hipSetDevice(device));
   pbf_ctx* c = new pbf_ctx();
   c->device = device;
+  c->fork.device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -125,7 +126,8 @@ int pbf_ntt_u64_batch_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, const 
   NttPlan* p;
   int rc = ctx->plan(modulus, omega, n, inverse, &p);
   if (rc) return rc;
-  return run_plan(*p, d_in, d_out, batch, ctx->scratch0, ctx->scratch1, ctx->pick(stream));
+  PBF_HIP(hipSetDevice(ctx->device));
+  return run_plan(*p, d_in, d_out, batch, ctx->scratch0, ctx->scratch1, ctx->pick(stream), &ctx->fork);
 }
 
 // fft.rs:109-132 mul_ntt

@@ -73,11 +73,25 @@ struct NttPlan {
   std::vector<std::shared_ptr<DevBuf>> tc;    // per pass: stage-C tables of ntt_gl_pass_kernel
 };
 
+// Extra streams and events of the multi-stream NTT group schedule (ntt_launch.hip
+// run_gl_passes). Owned by one context (created lazily on its device, destroyed with it),
+// so distinct contexts never share or race on them (include/pbf.h "Streams").
+constexpr int GL_MAX_STREAMS = 8;
+struct ForkSet {
+  int device = 0;
+  hipStream_t aux[GL_MAX_STREAMS] = {};  // aux[0] unused: slot 0 is the caller's stream
+  hipEvent_t fork = nullptr, join[GL_MAX_STREAMS] = {};
+  int ensure(int streams);               // streams 1..streams-1 and the event pair exist
+  ~ForkSet();
+};
+
 // Build a plan (validates omega's order and n^-1). Returns PBF status.
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p);
 // Enqueue a batched transform of a planned size on `stream` (d_in may equal d_out).
+// `fork` (the context's ForkSet) allows the multi-stream group schedule for large
+// Goldilocks batches; null keeps every launch on `stream`.
 int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
-             hipStream_t stream);
+             hipStream_t stream, ForkSet* fork = nullptr);
 // Kernel launchers (ntt_launch.hip)
 int launch_pointwise_mul(FieldKind k, const FieldArgs& fa, const uint64_t* a, const uint64_t* b, uint64_t* c,
                          uint64_t count, hipStream_t s);
@@ -99,6 +113,9 @@ int launch_shard_unsplit(const uint64_t* recv, uint64_t* out, uint64_t nl, uint3
 int launch_fill_random(const FieldArgs& fa, FieldKind k, uint64_t seed, uint64_t* d_out, uint64_t count,
                        hipStream_t s);
 
+// Plonk::verify's KZG pairing check on a given stream (pairing.hip)
+int pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, int* ok, hipStream_t s);
+
 }  // namespace pbf
 
 struct pbf_ctx {
@@ -107,6 +124,7 @@ struct pbf_ctx {
   hipStream_t user_stream = nullptr;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, int>, std::unique_ptr<pbf::NttPlan>> plans;
   pbf::DevBuf scratch0, scratch1, scratch2, io0, io1, io2, partial;
+  pbf::ForkSet fork;  // aux streams of the NTT group schedule (this context only)
   std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::unique_ptr<pbf::TwoLevel>> two_level;
   int roots(uint64_t m, uint64_t root, uint64_t n, pbf::TwoLevel** out);
   // `_dev` entry points enqueue on exactly the stream they are given (NULL = the

@@ -318,7 +318,9 @@ static MsmWork msm_work(pbf_ctx* ctx) {
 // Enqueue the device part; window sums land in w.sums (MSM_NW Xyzz, Montgomery).
 static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc, uint64_t n, hipStream_t s,
                       MsmWork& w) {
-  if (n > 0xFFFFFFFFull / MSM_NW) return fail(PBF_EINVAL, "too many points");
+  // the sort counts n * MSM_NW pairs in an int; scalars must be canonical Fr (< r < 2^254),
+  // so the 16-bit signed-digit recoding never carries out of the top window
+  if (n > 0x7FFFFFFFull / MSM_NW) return fail(PBF_EINVAL, "too many points (n * 16 must fit an int)");
   const uint64_t m = n * MSM_NW;
   int rc;
   if ((rc = w.pts.ensure(n * sizeof(Affine))) || (rc = w.inf.ensure(n)) || (rc = w.keys.ensure(m * 4)) ||

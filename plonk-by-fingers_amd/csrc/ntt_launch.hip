@@ -246,11 +246,11 @@ static PassFn pass_fn(FieldKind k, int e64, int logr, PassCfg c) {
 }
 
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                         DevBuf& s1, hipStream_t stream, uint32_t split_log);
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork = nullptr);
 
 int run_plan(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
-             hipStream_t stream) {
-  return run_plan_impl(p, d_in, d_out, batch, s0, s1, stream, 0);
+             hipStream_t stream, ForkSet* fork) {
+  return run_plan_impl(p, d_in, d_out, batch, s0, s1, stream, 0, fork);
 }
 
 // Split a natural-order batch [b][g*S + kk] into the send layout [g][b][kk].
@@ -416,23 +416,30 @@ static GlPassFn gl_fn_blk(int logr, bool first) {
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
 
-// extra streams of the multi-stream group schedule (PBF_NTT_STREAMS), per device
-constexpr int GL_MAX_STREAMS = 8;
-static hipStream_t aux_stream(int i) {
-  static std::map<std::pair<int, int>, hipStream_t> m;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  auto key = std::make_pair(dev, i);
-  auto it = m.find(key);
-  if (it != m.end()) return it->second;
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  m[key] = st;
-  return st;
+int ForkSet::ensure(int streams) {
+  if (streams > GL_MAX_STREAMS) streams = GL_MAX_STREAMS;
+  if (streams > 1 && !fork) PBF_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  for (int i = 1; i < streams; ++i) {
+    if (!aux[i]) PBF_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
+    if (!join[i]) PBF_HIP(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
+  }
+  return 0;
+}
+
+ForkSet::~ForkSet() {
+  (void)hipSetDevice(device);
+  for (int i = 1; i < GL_MAX_STREAMS; ++i) {
+    if (aux[i]) {
+      (void)hipStreamSynchronize(aux[i]);
+      (void)hipStreamDestroy(aux[i]);
+    }
+    if (join[i]) (void)hipEventDestroy(join[i]);
+  }
+  if (fork) (void)hipEventDestroy(fork);
 }
 
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                         DevBuf& s1, hipStream_t stream, uint32_t split_log) {
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
   // default schedule (measured best at 2^20 x 32): groups of 4
   // polynomials alternating over two streams once the batch has at least 8
   size_t G = batch >= 8 ? 4 : batch;
@@ -440,17 +447,18 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   if (split_log != 0 || G == 0 || G >= batch) return run_gl_group(p, d_in, d_out, batch, s0, s1, stream, split_log);
   // PBF_NTT_STREAMS=k: groups round-robin over the caller's stream and k-1 more (disjoint
   // scratch), so the passes of k groups run concurrently and their phases interleave
+  // (the extra streams are the context's own ForkSet; without one everything stays on `stream`)
   int ns = getenv("PBF_NTT_STREAMS") ? atoi(getenv("PBF_NTT_STREAMS")) : 2;
   ns = ns < 1 ? 1 : (ns > GL_MAX_STREAMS ? GL_MAX_STREAMS : ns);
+  if (!fork) ns = 1;
   hipStream_t sts[GL_MAX_STREAMS];
   sts[0] = stream;
-  for (int i = 1; i < ns; ++i)
-    if (!(sts[i] = aux_stream(i))) return fail(1, "stream creation failed");
-  hipEvent_t ev = nullptr;
   if (ns > 1) {
-    PBF_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    PBF_HIP(hipEventRecord(ev, stream));
-    for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], ev, 0));
+    int rc = fork->ensure(ns);
+    if (rc) return rc;
+    for (int i = 1; i < ns; ++i) sts[i] = fork->aux[i];
+    PBF_HIP(hipEventRecord(fork->fork, stream));
+    for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], fork->fork, 0));
   }
   int gi = 0;
   for (size_t g0 = 0; g0 < batch; g0 += G, ++gi) {
@@ -461,10 +469,9 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   }
   if (ns > 1) {
     for (int i = 1; i < ns; ++i) {
-      PBF_HIP(hipEventRecord(ev, sts[i]));
-      PBF_HIP(hipStreamWaitEvent(stream, ev, 0));
+      PBF_HIP(hipEventRecord(fork->join[i], sts[i]));
+      PBF_HIP(hipStreamWaitEvent(stream, fork->join[i], 0));
     }
-    PBF_HIP(hipEventDestroy(ev));
   }
   return 0;
 }
@@ -528,7 +535,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
 }
 
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                         DevBuf& s1, hipStream_t stream, uint32_t split_log) {
+                         DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
   if (batch == 0) return 0;
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * 8, hipMemcpyDeviceToDevice, stream));
@@ -550,7 +557,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   if (!rc && P > 2) rc = s1.ensure(bytes);
   if (rc) return rc;
   uint32_t log_ns = 0;
-  if (p.gl) return run_gl_passes(p, d_in, d_out, batch, s0, s1, stream, split_log);
+  if (p.gl) return run_gl_passes(p, d_in, d_out, batch, s0, s1, stream, split_log, fork);
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
     PassCfg cfg = pass_cfg(lr);

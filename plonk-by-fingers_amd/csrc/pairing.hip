@@ -700,7 +700,11 @@ extern "C" int pbf_pairing_bn254_dev(pbf_ctx* ctx, const uint64_t* d_g1, const u
   return 0;
 }
 
-extern "C" int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, int* ok) {
+// The pairing check on an explicit stream (host g1 / g2, synchronous): used by
+// pbf_pairing_check_bn254 (context host stream) and Plonk::verify's `_dev` entry (its
+// caller's stream).
+int pbf::pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, int* ok,
+                                 hipStream_t s) {
   if (!ctx || !ok || (n && (!g1 || !g2))) return fail(1, "null argument");
   *ok = 0;
   if (n == 0) {
@@ -711,22 +715,26 @@ extern "C" int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const u
   int rc = check_coords(g1, 2 * n);
   if (!rc) rc = check_coords(g2, 4 * n);
   if (rc) return rc;
-  hipStream_t s = ctx->host_stream();
-  if ((rc = ctx->io0.ensure(n * 64)) || (rc = ctx->io1.ensure(n * 128)) || (rc = ctx->io2.ensure(n * 384 + 64)))
-    return rc;
-  PBF_HIP(hipMemcpyAsync(ctx->io0.p, g1, n * 64, hipMemcpyHostToDevice, s));
-  PBF_HIP(hipMemcpyAsync(ctx->io1.p, g2, n * 128, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipSetDevice(ctx->device));
+  DevBuf &b1 = ctx->buf("pc.g1"), &b2 = ctx->buf("pc.g2"), &b3 = ctx->buf("pc.acc");
+  if ((rc = b1.ensure(n * 64)) || (rc = b2.ensure(n * 128)) || (rc = b3.ensure(n * 384 + 64))) return rc;
+  PBF_HIP(hipMemcpyAsync(b1.p, g1, n * 64, hipMemcpyHostToDevice, s));
+  PBF_HIP(hipMemcpyAsync(b2.p, g2, n * 128, hipMemcpyHostToDevice, s));
   const PairingConsts k = make_consts();
-  uint64_t* acc = (uint64_t*)ctx->io2.p;
+  uint64_t* acc = (uint64_t*)b3.p;
   int* d_ok = (int*)(acc + 48 * n);
-  hipLaunchKernelGGL(miller_kernel, dim3(n), dim3(64), 0, s, (const uint64_t*)ctx->io0.p,
-                     (const uint64_t*)ctx->io1.p, n, acc, k);
+  hipLaunchKernelGGL(miller_kernel, dim3(n), dim3(64), 0, s, (const uint64_t*)b1.p, (const uint64_t*)b2.p, n, acc, k);
   PBF_HIP(hipGetLastError());
   hipLaunchKernelGGL(pairing_check_final, dim3(1), dim3(64), 0, s, (const uint64_t*)acc, n, d_ok, k);
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipMemcpyAsync(ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
   return 0;
+}
+
+extern "C" int pbf_pairing_check_bn254(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2, size_t n, int* ok) {
+  if (!ctx) return fail(1, "null argument");
+  return pairing_check_on_stream(ctx, g1, g2, n, ok, ctx->host_stream());
 }
 
 extern "C" int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars, size_t n,

@@ -188,17 +188,17 @@ int pbf_poly_div_u64(pbf_ctx* ctx, uint64_t modulus, uint64_t root, uint32_t roo
   if (root_log > 32 || root >= modulus) return fail(PBF_EINVAL, "bad root of unity");
   nn = normalized_len(num, nn);
   nd = normalized_len(den, nd);
-  uint64_t lead_inv;
-  if (!invmod(den[nd - 1], modulus, &lead_inv))  // zero divisor: the reference panics (poly.rs:238 unwrap)
-    return fail(PBF_ENOINV, "leading coefficient of the divisor has no inverse");
   const bool num_zero = nn == 1 && num[0] == 0;
-  if (num_zero || nn < nd) {  // the reference's loop does not run: q = 0, r = num
-    q[0] = 0;
+  if (num_zero || nn < nd) {  // the reference's loop does not run (poly.rs:234): q = 0, r = num,
+    q[0] = 0;                 // whatever the divisor is, so 0 / 0 = (0, 0) without a panic
     *lq = 1;
     std::memcpy(r, num, nn * 8);
     *lr = nn;
     return PBF_OK;
   }
+  uint64_t lead_inv;
+  if (!invmod(den[nd - 1], modulus, &lead_inv))  // zero divisor: the reference panics (poly.rs:238 unwrap)
+    return fail(PBF_ENOINV, "leading coefficient of the divisor has no inverse");
   PBF_HIP(hipSetDevice(ctx->device));
   PolyCtx P{ctx, modulus, root, root_log, kind, fa, ctx->host_stream()};
   const size_t k = nn - nd + 1;  // quotient length

@@ -515,6 +515,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     return fail(PBF_EINVAL, "null argument");
   if (n < 8 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two >= 8");
   if (mode != 0 && mode != 1) return fail(PBF_EINVAL, "mode must be 0 (reference r_3) or 1 (paper)");
+  PBF_HIP(hipSetDevice(ctx->device));
   uint32_t log_n = 0;
   while ((1ull << log_n) < n) ++log_n;
   if (log_n + 2 > 28) return fail(PBF_EINVAL, "4n exceeds the 2-adicity of Fr");
@@ -871,6 +872,7 @@ extern "C" int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, 
                                      const uint64_t* abc, const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2,
                                      const uint64_t* srs, size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f) {
   if (!ctx || !q || !copies || !abc || !srs) return fail(PBF_EINVAL, "null argument");
+  PBF_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->host_stream();
   DevBuf &dq = ctx->buf("pv.q"), &dc = ctx->buf("pv.copies"), &dabc = ctx->buf("pv.abc"), &dsrs = ctx->buf("pv.srs");
   int rc;
@@ -937,6 +939,7 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   *ok = 0;
   if (n < 8 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two >= 8");
   if (srs_m < n) return fail(PBF_EINVAL, "SRS too short");
+  PBF_HIP(hipSetDevice(ctx->device));
   uint32_t log_n = 0;
   while ((1ull << log_n) < n) ++log_n;
   hipStream_t s = (hipStream_t)stream;
@@ -1063,7 +1066,7 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   h_neg_g1(e2, g1s + 8);
   memcpy(g2s, g2 + 16, 128);  // [s]G2
   memcpy(g2s + 16, g2, 128);  // G2
-  return pbf_pairing_check_bn254(ctx, g1s, g2s, 2, ok);
+  return pairing_check_on_stream(ctx, g1s, g2s, 2, ok, s);
 }
 
 extern "C" int pbf_plonk_verify_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies,
@@ -1071,6 +1074,7 @@ extern "C" int pbf_plonk_verify_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q,
                                       const uint64_t* proof_f, const uint64_t* chal, const uint64_t* u,
                                       const uint64_t* k1k2, int mode, int* ok) {
   if (!ctx || !q || !copies || !srs) return fail(PBF_EINVAL, "null argument");
+  PBF_HIP(hipSetDevice(ctx->device));
   hipStream_t s = ctx->host_stream();
   DevBuf &dq = ctx->buf("vf.q"), &dc = ctx->buf("vf.copies"), &dsrs = ctx->buf("vf.srs");
   int rc;

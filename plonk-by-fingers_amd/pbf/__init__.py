@@ -317,6 +317,20 @@ class Context:
                                                   mode, _ptr(pts), _ptr(fs), stream))
         return pts, fs
 
+    def plonk_verify_bn254_dev(self, n, d_q, d_copies, d_srs, srs_m, g2s, pts, fields, chal, u, k1k2=(2, 3),
+                               mode=0, stream: int = 0) -> bool:
+        """Plonk::verify (plonk.rs:468-650) with the circuit and SRS on the device; pts / fields
+        as plonk_prove_bn254_dev returns them (limb arrays) or as ints / points."""
+        pa = pts if isinstance(pts, np.ndarray) else _g1_limbs(pts)
+        fa = fields if isinstance(fields, np.ndarray) else ints_to_limbs(fields)
+        ok = ctypes.c_int(-1)
+        _check(self.lib.pbf_plonk_verify_bn254_dev(self.h, n, d_q, d_copies, d_srs, srs_m, _ptr(_g2_limbs(g2s)),
+                                                   _ptr(np.ascontiguousarray(pa, dtype=np.uint64)),
+                                                   _ptr(np.ascontiguousarray(fa, dtype=np.uint64)),
+                                                   _ptr(ints_to_limbs(chal)), _ptr(ints_to_limbs([u])),
+                                                   _ptr(ints_to_limbs(k1k2)), mode, ctypes.byref(ok), stream))
+        return ok.value == 1
+
     # ---- plonk-by-hand types (src/pbh/*.rs), batched on the GPU
     def _u32call(self, fn, a, b, width_out, n):
         a = np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))

@@ -107,19 +107,19 @@ REFERENCE_KATS = {
         "eval": [[[1, 2, 1], 2, 9]],
     },
     "g1": {
-        "cite": "src/pbh/g1.rs:357-385",
+        "cite": "src/pbh/g1.rs:233-260",
         "generator": [1, 2],
         "neg_g": [1, 99], "2g": [68, 74], "neg_2g": [68, 27], "4g": [65, 98], "neg_4g": [65, 3],
         "8g": [18, 49], "neg_8g": [18, 52], "16g": [1, 99], "3g": [26, 45], "5g": [12, 32], "9g": [18, 52],
     },
-    "g2": {"cite": "src/pbh/g2.rs:493-505", "generator": [36, 31], "2g": [90, 82]},
+    "g2": {"cite": "src/pbh/g2.rs:108-119", "generator": [36, 31], "2g": [90, 82]},
     "gt": {
-        "cite": "src/pbh/gt.rs:593-603",
+        "cite": "src/pbh/gt.rs:88-97",
         "mul": [[[26, 97], [93, 76], [97, 89]]],
         "pow": [[[42, 49], 6, [97, 89]], [[68, 47], 600, [97, 89]]],
         "pow101_is_conj": [93, 76],
     },
-    "pairing": {"cite": "src/pbh/pairing.rs:659-679", "p_mul": 1, "r_mul": 4, "q_mul": 3, "a": 5},
+    "pairing": {"cite": "src/pbh/pairing.rs:56-75", "p_mul": 1, "r_mul": 4, "q_mul": 3, "a": 5},
     "plonk_by_hand": {
         "cite": "src/pbh/mod.rs:44-124",
         "s": 2, "srs_n": 6, "omega_pows": 4,

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_g1_vectors(ctx, kats):
-    # g1.rs:357-385 through the batched scalar-mul kernel
+    # g1.rs:233-260 through the batched scalar-mul kernel
     k = kats["g1"]
     g = [1, 2, 0]
     got = ctx.pbh_g1_mul([g] * 6, [1, 2, 4, 8, 16, 3])
@@ -31,7 +31,7 @@ def test_g1_mul_exhaustive_vs_oracle(ctx):
 
 
 def test_g2_gt_vectors(ctx, kats):
-    # g2.rs:493-505, gt.rs:593-603
+    # g2.rs:108-119, gt.rs:88-97
     assert ctx.pbh_g2_mul([[36, 31]], [2]) == [tuple(kats["g2"]["2g"])]
     assert ctx.pbh_g2_mul([[36, 31]], [6]) == [oracle.g2_mul((36, 31), 6)]
     for a, e, r in kats["gt"]["pow"]:
@@ -39,7 +39,7 @@ def test_g2_gt_vectors(ctx, kats):
 
 
 def test_pairing_bilinearity_and_oracle(ctx, kats):
-    # pairing.rs:659-679 + every (P, Q) pair of small multiples vs the oracle
+    # pairing.rs:56-75 + every (P, Q) pair of small multiples vs the oracle
     g1s, g2s = [], []
     for a, b in itertools.product(range(1, 17), range(1, 7)):
         g1s.append(list(oracle.g1_mul((1, 2, 0), a)))

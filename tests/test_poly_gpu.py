@@ -64,6 +64,13 @@ def test_poly_div_edge_cases(ctx, m):
     with pytest.raises(pbf.PbfError) as e:
         ctx.poly_div(m, num, np.zeros(4, dtype=np.uint64))
     assert e.value.code == 2
+    # 0 / 0: the reference's loop never runs (poly.rs:234), so no panic: (0, 0)
+    q, r = ctx.poly_div(m, np.zeros(3, dtype=np.uint64), np.zeros(2, dtype=np.uint64))
+    assert list(q) == [0] and list(r) == [0]
+    # a non-zero constant divided by 0 does enter the loop and panics there
+    with pytest.raises(pbf.PbfError) as e:
+        ctx.poly_div(m, np.array([5], dtype=np.uint64), np.zeros(1, dtype=np.uint64))
+    assert e.value.code == 2
 
 
 def test_poly_div_large_identity(ctx):

@@ -1,4 +1,5 @@
-"""The generalised-prover restatement (oracle/plonk_bn254.py) against the committed
+"""The generalised-prover restatement (oracle/plonk_bn254.py = oracle/plonk.py with BN254
+types; the same code reproduces the reference KAT in tests/test_plonk_oracle_pbh.py) against the committed
 fixtures (regenerated for one case) and against the reference's own asserts: the
 paper-mode proof verifies, the reference-mode proof verifies only with alpha = 1
 (SURVEY.md §0.7)."""
@@ -29,3 +30,12 @@ def test_poly_helpers_match_reference_semantics():
     num = [7, 3, 0, 11, 5]
     q, r = P.pdiv(num, [2, 1])
     assert P.padd(P.pmul(q, [2, 1]), r) == P.norm(num)
+
+
+def test_linear_time_checker_matches_fixtures():
+    # oracle/plonk_bn254.py:evaluations_at_z (used by the 2^20-gate GPU test) reproduces the
+    # 7 field elements of every committed literal-oracle proof
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "plonk_bn254.json")))["cases"]
+    for c in gold:
+        q, cp, abc = P.mul_gates_circuit(c["n"], c["circuit_seed"])
+        assert P.evaluations_at_z(c["n"], q, cp, abc, c["chal"], c["rnd"], mode=c["mode"]) == c["fields"]
