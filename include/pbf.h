@@ -185,7 +185,8 @@ int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars,
  *   out_f   7 x 4: a_z b_z c_z s_sigma_1_z s_sigma_2_z r_z z_omega_z   (Proof, plonk.rs:61-95)
  * mode 0 = the reference's formulas (r_3(x) of plonk.rs:414-416; verifier step 7 of
  * plonk.rs:575-581), mode 1 = the paper linearisation the verifier checks (SURVEY §0.7:
- * with mode 0 an honest proof verifies only when alpha = 1, as in the reference).
+ * with mode 0 an honest proof verifies only when (a_z+b*s1_z+g)(b_z+b*s2_z+g)*alpha = 0,
+ * as in the reference's n = 4 KAT).
  * Errors: PBF_EINVAL for an unsatisfied circuit (constraints.rs:198), a zero permutation
  * denominator (plonk.rs:297), a non-divisible quotient (plonk.rs:370), short SRS.       */
 int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies, const uint64_t* abc,

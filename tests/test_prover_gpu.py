@@ -60,7 +60,7 @@ def test_prove_verify_at_scale(ctx, log_n):
     bad = list(fs)
     bad[0] = (bad[0] + 1) % P.R
     assert not ctx.plonk_verify_bn254(q, cp, srs, g2s, pts, bad, chal, 987654321, mode=1)
-    # the reference formulas verify with their own verifier when alpha = 1
+    # rounds 1-4 of the two modes agree (only r_3(x) differs)
     chal1 = [1] + chal[1:]
     srs2 = ctx.srs_create(s, 2 * n + 2)
     pts0, fs0 = ctx.plonk_prove_bn254(q, cp, abc, chal1, rnd, srs2, mode=0)

@@ -1,7 +1,7 @@
 """The generalised-prover restatement (oracle/plonk_bn254.py = oracle/plonk.py with BN254
 types; the same code reproduces the reference KAT in tests/test_plonk_oracle_pbh.py) against the committed
 fixtures (regenerated for one case) and against the reference's own asserts: the
-paper-mode proof verifies, the reference-mode proof verifies only with alpha = 1
+paper-mode proof verifies, the reference-mode proof verifies only when k3 = 0, as in the n = 4 KAT
 (SURVEY.md §0.7)."""
 import json
 import os

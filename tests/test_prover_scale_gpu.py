@@ -9,8 +9,10 @@ not need an O(n^2) oracle:
   3n+6.. of t(x) and the remainders of W_z / W_zw are all zero (plonk.rs:370, 438, 442),
   so a successful return certifies them;
 * the 9 commitments through the verifier: the paper-mode proof verifies, a proof with a
-  changed evaluation or a swapped commitment does not; the reference-mode proof verifies
-  with its own verifier when alpha = 1.
+  changed evaluation or a swapped commitment does not. (The reference-mode proof is
+  checked by its evaluations only: with the reference's r_3(x) an honest proof verifies
+  only when k3 = (a_z + beta s1_z + gamma)(b_z + beta s2_z + gamma) alpha = 0, as in the
+  reference's n = 4 KAT where (b_z + beta s2_z + gamma) = 170 = 0 mod 17)
 """
 import os
 import random
@@ -59,7 +61,7 @@ def test_prove_2p20_gates(ctx, log_n):
 
     pts, fs = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(),
                                         srs_m, mode=1, stream=sp)
-    chal1 = [1] + chal[1:]
+    chal1 = list(chal)
     pts0, fs0 = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal1, rnd,
                                           dsrs.data_ptr(), srs_m, mode=0, stream=sp)
     torch.cuda.synchronize()
@@ -74,7 +76,7 @@ def test_prove_2p20_gates(ctx, log_n):
     bad_p = pts.copy().reshape(9, 8)
     bad_p[[0, 1]] = bad_p[[1, 0]]  # a_s <-> b_s
     assert not verify(bad_p.reshape(-1), fs, chal, 1)
-    assert verify(pts0, fs0, chal1, 0)  # the reference's formulas, alpha = 1
+    assert not verify(pts0, fs0, chal1, 0)  # the reference's r_3: k3 != 0 here
 
     # field elements: O(n) recomputation from the witness
     qv = _ints(dq, 4)
