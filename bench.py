@@ -36,8 +36,11 @@ def root_of_unity(n: int) -> int:
 
 
 def cpu_baseline(log_n: int, budget_s: float) -> dict:
-    """The oracle's recursion-faithful restatement of fft.rs:90-106 on one core,
-    timed on this host over a bounded sample (whole 2^log_n transforms)."""
+    """CPU baselines on this host over bounded samples (whole 2^log_n transforms):
+    (a) the oracle's recursion-faithful restatement of fft.rs:90-106 on one core (the
+        reference is single-threaded) -- the reported `cpu_baseline`;
+    (b) the oracle's optimised iterative NTT (oracle/ntt_par.cpp) on all the cores this
+        job may use (OMP_NUM_THREADS, 16 on the GPU box) -- `all_cores`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker/baseline only (never on the GPU path)
 
@@ -52,9 +55,23 @@ def cpu_baseline(log_n: int, budget_s: float) -> dict:
         el = time.perf_counter() - t0
         if el >= budget_s and runs >= 2:
             break
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    batch = 2 * threads
+    ab = oracle.splitmix_field(GOLD, 0x5EED0002, n * batch)
+    oracle.ntt_gl_par(w, ab, batch=batch, threads=threads)  # warm-up
+    runs2, t0 = 0, time.perf_counter()
+    while True:
+        oracle.ntt_gl_par(w, ab, batch=batch, threads=threads)
+        runs2 += 1
+        el2 = time.perf_counter() - t0
+        if el2 >= budget_s / 2 and runs2 >= 2:
+            break
     return {"value": runs * n / el, "unit": "elements/s", "cores": 1, "kind": "port",
             "sample": f"{runs} x 2^{log_n}-point Goldilocks NTT, oracle ntt_ct (recursion-faithful "
-                      f"restatement of src/fft.rs:90-106, 1 thread), {el:.1f} s"}
+                      f"restatement of src/fft.rs:90-106, 1 thread), {el:.1f} s",
+            "all_cores": {"value": runs2 * batch * n / el2, "unit": "elements/s", "cores": threads, "kind": "port",
+                          "sample": f"{runs2} x {batch} x 2^{log_n}-point Goldilocks NTT, oracle ntt_gl_par "
+                                    f"(iterative radix-2, one polynomial per thread), {el2:.1f} s"}}
 
 
 def load_traffic(log_n: int, batch: int):
@@ -161,7 +178,8 @@ def main() -> int:
                                    "stream; algorithmic bytes 16*n per transform)"},
         }
         if world == 1 and not args.no_extra:
-            out["extra"] = other_configs(ctx, sp)
+            out["extra"] = {"ntt_2p24": ntt_2p24(ctx, sp, max(args.steps, 20))}
+            out["extra"].update(other_configs(ctx, sp))
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
         print(json.dumps(out), flush=True)
@@ -171,14 +189,48 @@ def main() -> int:
     return 0
 
 
-def _time_ms(fn, reps: int) -> float:
-    fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
+def _median_ms(fn, reps: int = 20, warmup: int = 2) -> dict:
+    """Median / min / max of `reps` timed calls after `warmup` untimed ones (BASELINE.md's
+    measurement rule: median of >= 20 after warm-ups). HIP events on torch's current stream
+    (every call here enqueues on it, or synchronises it) bracket each call."""
+    st = torch.cuda.current_stream()
+    for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps * 1e3
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        fn()
+        e1.record(st)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return {"ms": ts[len(ts) // 2], "ms_min": ts[0], "ms_max": ts[-1], "reps": reps}
+
+
+def ntt_2p24(ctx, sp, steps: int) -> dict:
+    """The north-star size: forward Goldilocks NTT of 2 x 2^24 points per step, HBM-resident,
+    timed like the headline (HIP events around `steps` back-to-back steps)."""
+    n, B = 1 << 24, 2
+    step, _ = _single_gpu(ctx, n, B, sp)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        step()
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    achieved = 16.0 * n * B / (ms / 1e3) / 1e9
+    return {"workload": "Goldilocks forward NTT, batch 2 x 2^24", "ms_per_step": ms,
+            "elements_per_s": n * B / (ms / 1e3), "steps": steps,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(24, B),
+                         "kernel": "ntt_gl_pass_kernel, 3 radix-2^8 passes (algorithmic bytes 16*n per transform)"}}
 
 
 def other_configs(ctx, sp) -> dict:
@@ -203,9 +255,9 @@ def other_configs(ctx, sp) -> dict:
     da[: la * 4] = rand_fr(la)
     db[: la * 4] = rand_fr(la)
     dc = torch.empty_like(da)
-    ms = _time_ms(lambda: ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1, stream=sp), 3)
-    res["config3_bn254_polymul_2p22"] = {"ms": ms, "ntt_elements_per_s": 3 * n / (ms / 1e3),
-                                         "note": "2 forward + 1 inverse NTT of 2^23 + pointwise, 256-bit Montgomery"}
+    t = _median_ms(lambda: ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1, stream=sp))
+    res["config3_bn254_polymul_2p22"] = dict(t, ntt_elements_per_s=3 * n / (t["ms"] / 1e3),
+                                             note="2 forward + 1 inverse NTT of 2^23 + pointwise, 256-bit Montgomery")
     del da, db, dc
     # config 4: BN254 G1 MSM of 2^20 points (points = t_i * G from the batch fixed-base kernel)
     m = 1 << 20
@@ -214,9 +266,9 @@ def other_configs(ctx, sp) -> dict:
     pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
     ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m, stream=sp)
     torch.cuda.synchronize()
-    ms = _time_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp), 3)
-    res["config4_bn254_msm_2p20"] = {"ms": ms, "points_per_s": m / (ms / 1e3),
-                                     "note": "Pippenger c=16, includes the 16-window host Horner"}
+    t = _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp))
+    res["config4_bn254_msm_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3),
+                                         note="Pippenger c=16 (bucket accumulation, window sums, combine)")
     # config 4 (cont.): BN254 pairing check (2 Miller loops + 1 final exponentiation, the
     # KZG check of plonk.rs:646-650) and batched pairing throughput (one wave per pairing)
     G1G = (1, 2)
@@ -225,26 +277,24 @@ def other_configs(ctx, sp) -> dict:
            (8495653923123431417604973247489272438418190587263600148770280649306958101930,
             4082367875863433681332203403145435568316851327593401208105741076214120093531))
     negG1 = (1, pbf.BN254_Q - 2)
-    ok = ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])  # e(G,H) e(-G,H) = 1 (warm-up)
-    reps = 5
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        ok = ok and ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])
-    res["config4_pairing_check"] = {"ms": (time.perf_counter() - t0) * 1e3 / reps, "ok": ok,
-                                    "note": "host round trip incl. copies; 2 pairs, one final exponentiation"}
+    oks = []
+    t = _median_ms(lambda: oks.append(ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])))  # e(G,H) e(-G,H) = 1
+    res["config4_pairing_check"] = dict(t, ok=all(oks),
+                                        note="host round trip incl. copies; 2 pairs, one final exponentiation")
     npair = 4096
     g1 = pbf.ints_to_limbs([c for _ in range(npair) for c in G1G])
     g2 = pbf.ints_to_limbs([c for _ in range(npair) for c in (G2G[0][0], G2G[0][1], G2G[1][0], G2G[1][1])])
     d1, d2 = torch.from_numpy(g1.view(np.int64)).cuda(), torch.from_numpy(g2.view(np.int64)).cuda()
     dout = torch.empty(npair * 48, dtype=torch.int64, device="cuda")
-    ms = _time_ms(lambda: ctx.pairing_bn254_dev(d1.data_ptr(), d2.data_ptr(), npair, dout.data_ptr(), stream=sp), 2)
-    res["config4_pairings_batch"] = {"ms": ms, "pairings_per_s": npair / (ms / 1e3), "batch": npair}
+    t = _median_ms(lambda: ctx.pairing_bn254_dev(d1.data_ptr(), d2.data_ptr(), npair, dout.data_ptr(), stream=sp),
+                   reps=5, warmup=1)
+    res["config4_pairings_batch"] = dict(t, pairings_per_s=npair / (t["ms"] / 1e3), batch=npair)
     # config 5: generalised PLONK prove (+ verify) of the synthetic mul circuit, 2^20 gates on
     # one GPU (scripts/bench_prover.py; 2^24 gates: profiles/r01/session2/prover_2p22_2p24.log)
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import bench_prover  # noqa: E402
 
-    res["config5_prove_2p20"] = bench_prover.run(ctx, 20, reps=2)
+    res["config5_prove_2p20"] = bench_prover.run(ctx, 20, reps=20)
     # config 1: plonk-by-hand proof + verify (pbh/mod.rs:44-124) through the GPU path
     with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
         k = json.load(f)["plonk_by_hand"]

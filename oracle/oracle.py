@@ -31,6 +31,7 @@ _SIG = [
     ("oracle_f_from_i64", _u64, [_u64, ctypes.c_int64]),
     ("oracle_f_inv", ctypes.c_int, [_u64, _u64, _p64]),
     ("oracle_ntt_ct", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("oracle_ntt_gl_par", ctypes.c_int, [_u64, _p64, _p64, _sz, _sz, ctypes.c_int, ctypes.c_int]),
     ("oracle_ntt_vandermonde", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
     ("oracle_ntt_iter", ctypes.c_int, [_u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
     ("oracle_mul_ntt", ctypes.c_int, [_u64, _u64, _p64, _sz, _p64, _sz, _p64]),
@@ -105,6 +106,20 @@ def ntt_iter(m: int, omega: int, values, inverse: bool = False) -> np.ndarray:
     rc = lib().oracle_ntt_iter(m, omega, _p(a), _p(out), a.size, int(inverse))
     if rc:
         raise ValueError(f"oracle_ntt_iter rc={rc}")
+    return out
+
+
+def ntt_gl_par(omega: int, values, batch: int = 1, inverse: bool = False, threads: int = 0) -> np.ndarray:
+    """Goldilocks NTT of `batch` polynomials, optimised iterative form on `threads` host
+    threads (0 = os.cpu_count()): the all-core CPU baseline (ntt_par.cpp)."""
+    import os
+
+    a = _a(values)
+    out = np.empty_like(a)
+    n = a.size // batch
+    t = threads or (os.cpu_count() or 1)
+    if lib().oracle_ntt_gl_par(omega, _p(a), _p(out), n, batch, int(inverse), t):
+        raise ValueError("oracle_ntt_gl_par failed")
     return out
 
 

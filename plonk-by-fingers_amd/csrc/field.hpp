@@ -32,9 +32,19 @@ struct Goldilocks {
     return s + ((wrap || s >= P) ? EPS : 0);
   }
   __host__ __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
+#ifdef __HIP_DEVICE_COMPILE__
+    // 32-bit borrow chain: the borrow comes straight out of v_subb_co_u32 (the 64-bit
+    // __builtin_sub_overflow form re-derived it with a v_cmp_gt_u64: one VALU more)
+    unsigned c1, c2;
+    const unsigned lo = __builtin_subc((unsigned)a, (unsigned)b, 0u, &c1);
+    const unsigned hi = __builtin_subc((unsigned)(a >> 32), (unsigned)(b >> 32), c1, &c2);
+    const uint64_t d = ((uint64_t)hi << 32) | lo;
+    return d - (c2 ? EPS : 0);  // d + p (mod 2^64); d > EPS when borrowing
+#else
     uint64_t d;
     const bool borrow = __builtin_sub_overflow(a, b, &d);
-    return d - (borrow ? EPS : 0);  // d + p (mod 2^64); d > EPS when borrowing
+    return d - (borrow ? EPS : 0);
+#endif
   }
   // 128-bit value lo + hi*2^64 reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
   __host__ __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {

@@ -42,3 +42,21 @@ def test_large_digest_2p16(vectors):
     assert c["n"] == 1 << 16
     a = oracle.splitmix_field(c["modulus"], c["seed"], c["n"])
     assert sha(oracle.ntt_iter(c["modulus"], c["omega"], a)) == c["sha256_fwd"]
+
+
+def test_parallel_cpu_ntt_matches_oracle():
+    # the all-core CPU baseline (oracle/ntt_par.cpp) computes the same transform as the
+    # recursion-faithful restatement of fft.rs:90-106 (and its inverse)
+    import numpy as np
+
+    import oracle
+
+    G = 0xFFFFFFFF00000001
+    for logn in (1, 3, 11):
+        n = 1 << logn
+        w = pow(7, (G - 1) // n, G)
+        a = oracle.splitmix_field(G, 9 + logn, 3 * n)
+        got = oracle.ntt_gl_par(w, a, batch=3, threads=2)
+        ref = np.concatenate([oracle.ntt_ct(G, w, a[i * n:(i + 1) * n]) for i in range(3)])
+        assert np.array_equal(got, ref)
+        assert np.array_equal(oracle.ntt_gl_par(w, got, batch=3, inverse=True, threads=2), a)
