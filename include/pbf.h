@@ -121,6 +121,11 @@ int pbf_ntt_shard_combine_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t omega, ui
                               uint32_t rank, const uint64_t* d_in, uint64_t* d_out, size_t nl,
                               size_t batch, int inverse, void* stream);
 
+/* c[i] = a[i] * b[i] for `count` elements (the pointwise step of mul_ntt, fft.rs:125-129;
+ * the sharded mul_ntt multiplies its blocks with it)                                  */
+int pbf_pointwise_mul_u64_dev(pbf_ctx* ctx, uint64_t modulus, const uint64_t* d_a, const uint64_t* d_b,
+                              uint64_t* d_c, size_t count, void* stream);
+
 /* ---- BN254 scalar field (BASELINE config 3) ----------------------------------
  * r = 21888242871839275222246405745257275088548364400416034343698204186575808495617,
  * elements 4 x uint64_t little-endian, canonical; n a power of two <= 2^28.
@@ -135,6 +140,17 @@ int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, si
 /* batched device mul_ntt: a, b already zero-padded to n = la + lb; out = batch x n  */
 int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d_a, const uint64_t* d_b,
                           uint64_t* d_out, size_t n, size_t batch, void* stream);
+
+/* Stride-sharded Fr NTT across G GPUs: pbf_ntt_shard_local_dev / _combine_dev (above) for
+ * 256-bit elements (omega: 4 x u64, order G*nl). Same layouts, 4 x u64 per element.     */
+int pbf_ntt_fr256_shard_local_dev(pbf_ctx* ctx, const uint64_t* omega, uint32_t world, const uint64_t* d_in,
+                                  uint64_t* d_out, size_t nl, size_t batch, int inverse, void* stream);
+int pbf_ntt_fr256_shard_combine_dev(pbf_ctx* ctx, const uint64_t* omega, uint32_t world, uint32_t rank,
+                                    const uint64_t* d_in, uint64_t* d_out, size_t nl, size_t batch, int inverse,
+                                    void* stream);
+/* c[i] = a[i] * b[i] over Fr (canonical in and out)                                      */
+int pbf_pointwise_mul_fr256_dev(pbf_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, uint64_t* d_c,
+                                size_t count, void* stream);
 
 /* ---- BN254 G1 MSM / SRS (BASELINE config 4) -----------------------------------
  * Points: affine, 8 x uint64_t (x then y, each 4 little-endian limbs, canonical in Fq);
@@ -203,6 +219,34 @@ int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, cons
                                const uint64_t* d_srs, size_t srs_m, const uint64_t* g2, const uint64_t* proof_pts,
                                const uint64_t* proof_f, const uint64_t* chal, const uint64_t* u, const uint64_t* k1k2,
                                int mode, int* ok, void* stream);
+
+/* Config 5 across G GPUs ("NTT sharded across 8xMI355X"): one process (or thread) per GPU
+ * calls pbf_plonk_prove_bn254_sharded_dev with the same inputs (circuit, SRS, challenges,
+ * blinders) and its rank. The library computes nothing collective itself: it calls back
+ * into the caller's communicator (RCCL via torch.distributed in multigpu.py), always for
+ * buffers it names in `comm` and stream-ordered on `stream`:
+ *   all_to_all(user, b, stream):  send[g*b .. (g+1)*b) goes to rank g, recv[g*b ..) comes from g
+ *   all_gather(user, b, stream):  send[0 .. b) of rank g lands in recv[g*b .. (g+1)*b)
+ * Work split: the 14 coset NTTs of size 4n of round 3 and the 4n-point
+ * transforms of round 5 run as stride-sharded NTTs (one all-to-all each way), the quotient
+ * and the opening divisions on this rank's evaluation blocks, t / W_z / W_zw coefficients
+ * are all-gathered; every commitment is a point-range MSM whose partial sums are
+ * all-gathered (64 B per rank); the O(n) steps (interpolation, accumulator, evaluations) are
+ * replicated. Outputs are identical on every rank and bit-identical to the single-GPU
+ * proof. send / recv: device buffers of `capacity` >= 16 * (4n / world) * 32 bytes each.   */
+typedef struct pbf_comm {
+  uint32_t world, rank;
+  void* user;
+  void* send;
+  void* recv;
+  size_t capacity;
+  int (*all_to_all)(void* user, size_t bytes_per_peer, void* stream);
+  int (*all_gather)(void* user, size_t bytes_per_rank, void* stream);
+} pbf_comm;
+int pbf_plonk_prove_bn254_sharded_dev(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64_t* d_q,
+                                      const uint64_t* d_copies, const uint64_t* d_abc, const uint64_t* chal,
+                                      const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* d_srs,
+                                      size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f, void* stream);
 
 /* synthetic config-5 circuit on the device (bench / tests): every gate a*b = c, a, b
  * uniform (splitmix64 of seed), every 4th gate's c copied into the next gate's a       */

@@ -20,6 +20,7 @@ static bool all_canonical(const uint64_t* v, size_t n, uint64_t m) {
 
 using namespace pbf;
 void pbf_internal_drop_plans256(const void* ctx);  // ntt256.hip
+void pbf_internal_drop_tl256(const void* ctx);     // ntt256.hip
 
 int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan** out) {
   auto key = std::make_tuple(m, omega, n, inverse ? 1 : 0);
@@ -83,6 +84,7 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
 void pbf_ctx_destroy(pbf_ctx* ctx) {
   if (!ctx) return;
   pbf_internal_drop_plans256(ctx);
+  pbf_internal_drop_tl256(ctx);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamDestroy(ctx->stream);
@@ -176,6 +178,17 @@ int pbf_poly_eval_u64(pbf_ctx* ctx, uint64_t modulus, const uint64_t* coeffs, si
   PBF_HIP(hipMemcpyAsync(ys, ctx->io2.p, nx * 8, hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
   return PBF_OK;
+}
+
+// c[i] = a[i] * b[i] (the pointwise step of mul_ntt, fft.rs:125-129), device pointers
+int pbf_pointwise_mul_u64_dev(pbf_ctx* ctx, uint64_t modulus, const uint64_t* d_a, const uint64_t* d_b, uint64_t* d_c,
+                              size_t count, void* stream) {
+  if (!ctx || (count && (!d_a || !d_b || !d_c))) return fail(PBF_EINVAL, "null argument");
+  FieldKind k;
+  FieldArgs fa;
+  if (!field_for(modulus, &k, &fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
+  PBF_HIP(hipSetDevice(ctx->device));
+  return launch_pointwise_mul(k, fa, d_a, d_b, d_c, count, ctx->pick(stream));
 }
 
 int pbf_fill_random_u64_dev(pbf_ctx* ctx, uint64_t modulus, uint64_t seed, uint64_t* d_out, size_t count,

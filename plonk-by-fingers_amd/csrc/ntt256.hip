@@ -413,6 +413,100 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
   return 0;
 }
 
+// ---------------------------------------------------------------- multi-GPU
+// Stride-sharded Fr transform of N = G * nl points, the 256-bit twin of the u64 shard
+// kernels in ntt_kernels.hpp: rank g holds a[g + G*m]; local nl-point NTT (root w^G) stored
+// as the send layout [dst][b][kk] (S = nl / G); all-to-all; combine:
+//   out[b][q*S + kk] = X[q*nl + r*S + kk] = sum_g w_G^(g q) w^(g k) Y_g[k],  k = r*S + kk.
+// The inverse runs it backwards (split_inv applies G^-1 and w^(-g k), the local INTT nl^-1).
+// Elements canonical at rest; Montgomery inside the kernels; twiddles Montgomery.
+struct Shard256Args {
+  const U256* in;
+  U256* out;
+  const U256* tw0;  // two-level table of the global root (forward w, inverse w^-1), Montgomery
+  const U256* tw1;
+  uint32_t tw_bits;
+  uint64_t nl, s, rank, n_mask, batch;
+  U256 wg[8];       // w_G^m (forward) / w_G^-m (inverse), Montgomery
+  U256 scale;       // G^-1 (inverse) or 1, Montgomery
+};
+
+__device__ __forceinline__ U256 tw256(const Shard256Args& a, uint64_t e) {
+  return Fr::mul(a.tw0[e & ((1ull << a.tw_bits) - 1)], a.tw1[e >> a.tw_bits]);
+}
+
+// [b][g*S + kk] -> [g][b][kk]
+__global__ void shard_split256_kernel(const U256* in, U256* out, uint64_t s, uint64_t nl, uint64_t batch) {
+  const uint64_t total = nl * batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / nl, k = id % nl;
+    out[((k / s) * batch + b) * s + (k % s)] = in[id];
+  }
+}
+// [g][b][kk] -> [b][g*S + kk]
+__global__ void shard_unsplit256_kernel(const U256* in, U256* out, uint64_t s, uint64_t nl, uint64_t batch) {
+  const uint64_t total = nl * batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / nl, k = id % nl;
+    out[id] = in[((k / s) * batch + b) * s + (k % s)];
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) shard_combine256_kernel(Shard256Args a) {
+  const uint64_t total = a.s * a.batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / a.s, kk = id % a.s;
+    const uint64_t k = a.rank * a.s + kk;
+    U256 t[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const U256 y = Fr::to_mont(a.in[((uint64_t)g * a.batch + b) * a.s + kk]);
+      const uint64_t e = ((uint64_t)g * k) & a.n_mask;
+      t[g] = (g == 0 || e == 0) ? y : Fr::mul(y, tw256(a, e));
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      U256 acc = t[0];
+#pragma unroll
+      for (int g = 1; g < G; ++g) acc = Fr::add(acc, Fr::mul(t[g], a.wg[(g * q) % G]));
+      a.out[b * a.nl + (uint64_t)q * a.s + kk] = Fr::from_mont(acc);
+    }
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) shard_split_inv256_kernel(Shard256Args a) {
+  const uint64_t total = a.s * a.batch;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total; id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = id / a.s, kk = id % a.s;
+    const uint64_t k = a.rank * a.s + kk;
+    U256 x[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) x[q] = Fr::to_mont(a.in[b * a.nl + (uint64_t)q * a.s + kk]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      U256 acc = x[0];
+#pragma unroll
+      for (int q = 1; q < G; ++q) acc = Fr::add(acc, Fr::mul(x[q], a.wg[(g * q) % G]));
+      const uint64_t e = ((uint64_t)g * k) & a.n_mask;
+      if (g != 0 && e != 0) acc = Fr::mul(acc, tw256(a, e));
+      acc = Fr::mul(acc, a.scale);
+      a.out[((uint64_t)g * a.batch + b) * a.s + kk] = Fr::from_mont(acc);
+    }
+  }
+}
+
+struct TwoLevel256 {
+  DevBuf t0, t1;
+  uint32_t bits = 0;
+};
+
+static uint32_t grid256(uint64_t count) {
+  const uint64_t b = (count + 255) / 256;
+  return (uint32_t)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
 static bool canonical_vec(const uint64_t* v, size_t n) {
   for (size_t i = 0; i < n; ++i)
     if (!h_canonical(h_from64(v + 4 * i))) return false;
@@ -540,6 +634,150 @@ int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d
                      (uint64_t)(batch * n));
   PBF_HIP(hipGetLastError());
   return run256(*iv, (const U256*)d_out, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s);
+}
+
+
+}  // extern "C"
+
+namespace {
+// per-(context, root, N) two-level tables of the global root for the shard combine
+std::map<std::tuple<const void*, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>, std::unique_ptr<TwoLevel256>>&
+tl256() {
+  static std::map<std::tuple<const void*, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t>, std::unique_ptr<TwoLevel256>> m;
+  return m;
+}
+int get_tl256(pbf_ctx* ctx, const U256& wm, uint64_t N, TwoLevel256** out) {
+  uint64_t w4[4];
+  u256_to_u64(wm, w4);
+  auto k = std::make_tuple((const void*)ctx, w4[0], w4[1], w4[2], w4[3], N);
+  std::lock_guard<std::mutex> g(plans256_mu());
+  auto it = tl256().find(k);
+  if (it != tl256().end()) { *out = it->second.get(); return 0; }
+  std::unique_ptr<TwoLevel256> t(new TwoLevel256());
+  PBF_HIP(hipSetDevice(ctx->device));
+  uint32_t log_n = 0;
+  while ((1ull << log_n) < N) ++log_n;
+  t->bits = (log_n + 1) / 2;
+  int rc = up256(t->t0, h_powers(wm, 1ull << t->bits));
+  if (!rc) rc = up256(t->t1, h_powers(h_pow(wm, 1ull << t->bits), (N >> t->bits) ? (N >> t->bits) : 1));
+  if (rc) return rc;
+  *out = t.get();
+  tl256()[k] = std::move(t);
+  return 0;
+}
+// (omega of order G*nl) checks shared by the two shard entry points; wm = Montgomery omega
+int shard256_check(const uint64_t* omega, uint32_t G, size_t nl, U256* wm) {
+  if (G != 2 && G != 4 && G != 8) return fail(PBF_EINVAL, "world size must be 2, 4 or 8");
+  if (nl < G || (nl & (nl - 1))) return fail(PBF_EINVAL, "per-rank size must be a power of two >= G");
+  const U256 w = h_from64(omega);
+  if (!h_canonical(w)) return fail(PBF_EINVAL, "omega not canonical");
+  *wm = Fr::to_mont(w);
+  const uint64_t N = (uint64_t)G * nl;
+  const U256 one_m = Fr::to_mont(Fr::one_plain());
+  if (!Fr::eq(h_pow(*wm, N), one_m) || Fr::eq(h_pow(*wm, N / 2), one_m))
+    return fail(PBF_EINVAL, "omega does not have order G*nl");
+  return 0;
+}
+}  // namespace
+
+void pbf_internal_drop_tl256(const void* ctx) {
+  std::lock_guard<std::mutex> g(plans256_mu());
+  auto& m = tl256();
+  for (auto it = m.begin(); it != m.end();) it = (std::get<0>(it->first) == ctx) ? m.erase(it) : std::next(it);
+}
+
+extern "C" {
+
+// Multi-GPU stride-sharded Fr NTT, local step (the u64 pbf_ntt_shard_local_dev for 256-bit
+// elements): forward [b][m] stride shard -> send [dst][b][kk]; inverse recv [src][b][kk] ->
+// [b][m]. Same ABI layout as the u64 entry point, 4 x u64 per element.
+int pbf_ntt_fr256_shard_local_dev(pbf_ctx* ctx, const uint64_t* omega, uint32_t world, const uint64_t* d_in,
+                                  uint64_t* d_out, size_t nl, size_t batch, int inverse, void* stream) {
+  if (!ctx || !omega || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  U256 wm;
+  int rc = shard256_check(omega, world, nl, &wm);
+  if (rc) return rc;
+  PBF_HIP(hipSetDevice(ctx->device));
+  uint64_t wl[4];
+  u256_to_u64(Fr::from_mont(h_pow(wm, world)), wl);  // local root w^G, order nl
+  Plan256* p;
+  if ((rc = get_plan256(ctx, wl, nl, inverse, &p))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = ctx->scratch2.ensure(batch * nl * 32))) return rc;
+  U256* tmp = (U256*)ctx->scratch2.p;
+  const uint64_t S = nl / world;
+  if (!inverse) {
+    if ((rc = run256(*p, (const U256*)d_in, tmp, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
+    hipLaunchKernelGGL(shard_split256_kernel, dim3(grid256(nl * batch)), dim3(256), 0, s, (const U256*)tmp,
+                       (U256*)d_out, S, (uint64_t)nl, (uint64_t)batch);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  hipLaunchKernelGGL(shard_unsplit256_kernel, dim3(grid256(nl * batch)), dim3(256), 0, s, (const U256*)d_in, tmp, S,
+                     (uint64_t)nl, (uint64_t)batch);
+  PBF_HIP(hipGetLastError());
+  return run256(*p, tmp, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s);
+}
+
+// Multi-GPU stride-sharded Fr NTT, combine step (forward: recv -> out[b][q*S + kk]);
+// inverse: the blocked layout -> send [dst][b][kk] (twiddle w^-(g k), radix-G, G^-1).
+int pbf_ntt_fr256_shard_combine_dev(pbf_ctx* ctx, const uint64_t* omega, uint32_t world, uint32_t rank,
+                                    const uint64_t* d_in, uint64_t* d_out, size_t nl, size_t batch, int inverse,
+                                    void* stream) {
+  if (!ctx || !omega || !d_in || !d_out) return fail(PBF_EINVAL, "null argument");
+  if (d_in == d_out) return fail(PBF_EINVAL, "combine is out-of-place");
+  U256 wm;
+  int rc = shard256_check(omega, world, nl, &wm);
+  if (rc) return rc;
+  if (rank >= world) return fail(PBF_EINVAL, "rank out of range");
+  PBF_HIP(hipSetDevice(ctx->device));
+  const uint64_t N = (uint64_t)world * nl;
+  const U256 root = inverse ? h_inv(wm) : wm;
+  TwoLevel256* tl;
+  if ((rc = get_tl256(ctx, root, N, &tl))) return rc;
+  Shard256Args a;
+  a.in = (const U256*)d_in;
+  a.out = (U256*)d_out;
+  a.tw0 = (const U256*)tl->t0.p;
+  a.tw1 = (const U256*)tl->t1.p;
+  a.tw_bits = tl->bits;
+  a.nl = nl;
+  a.s = nl / world;
+  a.rank = rank;
+  a.n_mask = N - 1;
+  a.batch = batch;
+  const U256 wG = h_pow(root, nl);  // primitive G-th root (direction-specific)
+  U256 x = Fr::to_mont(Fr::one_plain());
+  for (uint32_t i = 0; i < 8; ++i) {
+    a.wg[i] = x;
+    if (i + 1 < world) x = Fr::mul(x, wG);
+  }
+  {
+    U256 gg = Fr::one_plain();
+    gg.w[0] = world;
+    a.scale = inverse ? h_inv(Fr::to_mont(gg)) : Fr::to_mont(Fr::one_plain());
+  }
+  void (*fn)(Shard256Args) = nullptr;
+  switch (world) {
+    case 2: fn = inverse ? shard_split_inv256_kernel<2> : shard_combine256_kernel<2>; break;
+    case 4: fn = inverse ? shard_split_inv256_kernel<4> : shard_combine256_kernel<4>; break;
+    default: fn = inverse ? shard_split_inv256_kernel<8> : shard_combine256_kernel<8>; break;
+  }
+  hipLaunchKernelGGL(fn, dim3(grid256(a.s * batch)), dim3(256), 0, (hipStream_t)stream, a);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+// c[i] = a[i] * b[i] over `count` Fr elements (the pointwise step of mul_ntt, fft.rs:125-129)
+int pbf_pointwise_mul_fr256_dev(pbf_ctx* ctx, const uint64_t* d_a, const uint64_t* d_b, uint64_t* d_c, size_t count,
+                                void* stream) {
+  if (!ctx || (count && (!d_a || !d_b || !d_c))) return fail(PBF_EINVAL, "null argument");
+  if (count == 0) return 0;
+  PBF_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(pointwise_mul256_kernel, dim3(grid256(count)), dim3(256), 0, (hipStream_t)stream,
+                     (const U256*)d_a, (const U256*)d_b, (U256*)d_c, (uint64_t)count);
+  PBF_HIP(hipGetLastError());
+  return 0;
 }
 
 }  // extern "C"

@@ -79,20 +79,48 @@ __device__ __forceinline__ U256 pow64(U256 b) {
   return b;
 }
 
-// out[i] = i < len ? in[i] * base^(i + off) : 0, i < count (coset scaling, zero padding).
-// The product of a canonical value and a Montgomery-form power is the canonical product
-// (a * xR * R^-1), so the element needs no conversions.
-__global__ void k_scale_pow(const uint64_t* in, uint64_t len, uint64_t* out, uint64_t count, U256 base, uint64_t off) {
+// out[m] = (j = in_off + in_stride m) < len ? in[j] * base^(e_off + e_mult m) : 0, m < count
+// (coset scaling with zero padding; with in_stride = e_mult = G, in_off = e_off = rank it
+// extracts rank's stride shard of the scaled vector). The product of a canonical value and
+// a Montgomery-form power is the canonical product (a * xR * R^-1): no conversions.
+__global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out,
+                            uint64_t count, U256 base, uint64_t e_off, uint64_t e_mult) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
-  U256 x = fr_pow(base, i0 + off);
-  const U256 step = pow64(base);
+  U256 x = fr_pow(base, e_off + e_mult * i0);
+  const U256 step = fr_pow(base, 64 * e_mult);
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
-    if (i < len) u256_to_u64(Fr::mul(u256_from_u64(in + 4 * i), x), out + 4 * i);
-    else for (int j = 0; j < 4; ++j) out[4 * i + j] = 0;
+    const uint64_t j = in_off + in_stride * i;
+    if (j < len) u256_to_u64(Fr::mul(u256_from_u64(in + 4 * j), x), out + 4 * i);
+    else for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
     x = Fr::mul(x, step);
   }
+}
+
+// Evaluation-domain layout of a rank's blocks in the stride-sharded NTT (multigpu, SURVEY.md
+// §8e): local position p = q*S + kk holds global index q*nl + rank*S + kk. G = 1: p itself.
+struct Blk {
+  uint64_t nl, S, rank;
+  uint32_t G;
+};
+__device__ __forceinline__ uint64_t blk_index(const Blk& b, uint64_t p) {
+  return b.G == 1 ? p : (p / b.S) * b.nl + b.rank * b.S + (p % b.S);
+}
+// x_{i(p)} = g w^{i(p)} for the chunked kernels: advance the running point by w^64 inside a
+// block, recompute it where p + 64 starts a new block
+__device__ __forceinline__ U256 blk_next_x(const Blk& b, uint64_t p, const U256& x, const U256& step, const U256& g,
+                                           const U256& w) {
+  if (b.G == 1 || (p + 64) / b.S == p / b.S) return Fr::mul(x, step);
+  return Fr::mul(g, fr_pow(w, blk_index(b, p + 64)));
+}
+
+// out[g + G m] = in[g][m] (the all-gathered stride shards of one vector, back in order)
+__global__ void k_interleave(const uint64_t* in, uint64_t* out, uint64_t nl, uint32_t G) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= nl * G) return;
+  const uint64_t g = id / nl, m = id % nl;
+  for (int q = 0; q < 4; ++q) out[4 * (g + G * m) + q] = in[4 * id + q];
 }
 
 // out[i] = start * base^i
@@ -298,7 +326,10 @@ __global__ void k_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, uint6
 // divided by Z_H(x_i) = g^n w_4^(i mod 4) - 1 (inverses zh_inv[0..3] from the host)
 struct QuotArgs {
   const uint64_t *a, *b, *c, *z, *ql, *qr, *qo, *qm, *qc, *s1, *s2, *s3, *l1;
-  uint64_t N;
+  const uint64_t* zw;  // z(w x) evaluations (sharded layout), or null: z at index i + 4
+  uint64_t N;          // evaluations held here (N, or nl on a rank of a sharded prove)
+  uint64_t N_all;      // 4n
+  Blk blk;
   U256 alpha, beta, gamma, k1, k2, alpha2, g, wN;
   U256 zh_inv[4];
 };
@@ -306,12 +337,13 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= q.N) return;
-  U256 x = Fr::mul(q.g, fr_pow(q.wN, i0));
+  U256 x = Fr::mul(q.g, fr_pow(q.wN, blk_index(q.blk, i0)));
   const U256 step = pow64(q.wN);
-  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < q.N; ++k, i += 64, x = Fr::mul(x, step)) {
-    const uint64_t o = 4 * i;
+  for (uint64_t p = i0, k = 0; k < PV_CHUNK && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
+    const uint64_t o = 4 * p;
+    const uint64_t i = blk_index(q.blk, p);
     const U256 a = ldr(q.a + o), b = ldr(q.b + o), c = ldr(q.c + o), z = ldr(q.z + o);
-    const U256 zw = ldr(q.z + 4 * ((i + 4) % q.N));  // z(w x_i): w = w_N^4
+    const U256 zw = q.zw ? ldr(q.zw + o) : ldr(q.z + 4 * ((i + 4) % q.N_all));  // z(w x_i): w = w_N^4
     // t1: a b q_m + a q_l + b q_r + c q_o + q_c
     U256 t1 = Fr::mul(Fr::mul(a, b), ldr(q.qm + o));
     t1 = Fr::add(t1, Fr::mul(a, ldr(q.ql + o)));
@@ -337,13 +369,13 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out) {
 }
 
 // out[i] = (P(x_i) - y) / (x_i - z) on the coset, inv_xz[i] = 1/(x_i - z) precomputed
-__global__ void k_coset_minus(uint64_t* out, uint64_t N, U256 g, U256 wN, U256 zpt) {
+__global__ void k_coset_minus(uint64_t* out, uint64_t N, U256 g, U256 wN, U256 zpt, Blk blk) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= N) return;
-  U256 x = Fr::mul(g, fr_pow(wN, i0));
+  U256 x = Fr::mul(g, fr_pow(wN, blk_index(blk, i0)));
   const U256 step = pow64(wN);
-  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < N; ++k, i += 64, x = Fr::mul(x, step))
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < N; ++k, x = blk_next_x(blk, i, x, step, g, wN), i += 64)
     str(out + 4 * i, Fr::sub(x, zpt));
 }
 __global__ void k_sub_mul(const uint64_t* p, U256 y, const uint64_t* inv, uint64_t* out, uint64_t N) {
@@ -484,33 +516,113 @@ struct Prover {
   int ntt(const uint64_t* w, uint64_t* in, uint64_t* out, uint64_t size, uint64_t batch, int inverse) {
     return pbf_ntt_fr256_batch_dev(ctx, w, in, out, size, batch, inverse, s);
   }
+
+  // ---- multi-GPU split (pbf_plonk_prove_bn254_sharded_dev; G = 1: the single-GPU prover)
+  const pbf_comm* comm = nullptr;
+  uint32_t G = 1, rank = 0;
+  uint64_t nl = 0, S = 0;    // 4n / G evaluations per rank, in G blocks of S
+  DevBuf* shard = nullptr;   // stride-shard staging (16 nl elements)
+  uint64_t count() const { return G > 1 ? nl : N; }  // coset evaluations held by this rank
+  Blk blk() const {
+    Blk b;
+    b.nl = nl; b.S = S; b.rank = rank; b.G = G;
+    return b;
+  }
+  int a2a(size_t bytes) {
+    if (comm->all_to_all(comm->user, bytes, (void*)s)) return fail(PBF_ECOMM, "all_to_all callback failed");
+    return 0;
+  }
+  int ag(size_t bytes) {
+    if (comm->all_gather(comm->user, bytes, (void*)s)) return fail(PBF_ECOMM, "all_gather callback failed");
+    return 0;
+  }
+  void scale(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out, uint64_t cnt,
+             const U256& base, uint64_t e_off, uint64_t e_mult) {
+    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
+                       in_stride, len, out, cnt, base, e_off, e_mult);
+  }
+  // k coset NTTs of size N: slot i = evaluations of sum_j srcs[i][j] (bases[i] x)^j at g w_N^e
+  // (this rank's blocks when sharded), slots count() apart in `out`
+  int coset_ntt_batch(int k, const uint64_t* const* srcs, const uint64_t* lens, const U256* bases, uint64_t* out) {
+    if (G == 1) {
+      for (int i = 0; i < k; ++i) scale(srcs[i], 0, 1, lens[i], out + 4 * N * i, N, bases[i], 0, 1);
+      PBF_HIP(hipGetLastError());
+      return ntt(wN_plain, out, out, N, k, 0);  // one batched NTT (fuller GPU, one plan lookup)
+    }
+    uint64_t* sh = (uint64_t*)shard->p;
+    for (int i = 0; i < k; ++i) scale(srcs[i], rank, G, lens[i], sh + 4 * nl * i, nl, bases[i], rank, G);
+    PBF_HIP(hipGetLastError());
+    int rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, sh, (uint64_t*)comm->send, nl, k, 0, s);
+    if (!rc) rc = a2a((size_t)k * S * 32);
+    if (!rc) rc = pbf_ntt_fr256_shard_combine_dev(ctx, wN_plain, G, rank, (const uint64_t*)comm->recv, out, nl, k, 0, s);
+    return rc;
+  }
   // coset NTT of `len` coefficients into N evaluations at g w_N^i
   int coset_ntt(const uint64_t* coeff, uint64_t len, uint64_t* out) {
-    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, coeff, len, out, N,
-                       g, (uint64_t)0);
-    PBF_HIP(hipGetLastError());
-    return ntt(wN_plain, out, out, N, 1, 0);
+    return coset_ntt_batch(1, &coeff, &len, &g, out);
   }
-  // coefficients of the degree < N polynomial with evaluations `ev` on the coset
+  // coefficients (all N of them, on every rank) of the polynomial whose coset evaluations
+  // are `ev` (this rank's blocks when sharded)
   int coset_intt(uint64_t* ev, uint64_t* out) {
-    int rc = ntt(wN_plain, ev, ev, N, 1, 1);
+    if (G == 1) {
+      int rc = ntt(wN_plain, ev, ev, N, 1, 1);
+      if (rc) return rc;
+      scale(ev, 0, 1, N, out, N, g_inv, 0, 1);
+      PBF_HIP(hipGetLastError());
+      return 0;
+    }
+    uint64_t* sh = (uint64_t*)shard->p;
+    int rc = pbf_ntt_fr256_shard_combine_dev(ctx, wN_plain, G, rank, ev, (uint64_t*)comm->send, nl, 1, 1, s);
+    if (!rc) rc = a2a(S * 32);
+    if (!rc) rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, (const uint64_t*)comm->recv, sh, nl, 1, 1, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, ev, N, out, N,
-                       g_inv, (uint64_t)0);
+    scale(sh, 0, 1, nl, (uint64_t*)comm->send, nl, g_inv, rank, G);  // u_j g^-j, j = rank + G m
+    PBF_HIP(hipGetLastError());
+    if ((rc = ag(nl * 32))) return rc;
+    hipLaunchKernelGGL(k_interleave, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)comm->recv, out, nl, G);
     PBF_HIP(hipGetLastError());
     return 0;
   }
+  // SRS::eval_at_s (plonk.rs:51-58); sharded: this rank's point range, partial sums
+  // all-gathered (64 B per rank) and added on the host
   int commit(const uint64_t* d_srs, const uint64_t* coeff, uint64_t len, uint64_t* out) {
-    return pbf_msm_g1_bn254_dev(ctx, d_srs, coeff, len, out, s);
+    if (G == 1) return pbf_msm_g1_bn254_dev(ctx, d_srs, coeff, len, out, s);
+    const uint64_t base = len / G, extra = len % G;
+    const uint64_t start = rank * base + (rank < extra ? rank : extra);
+    const uint64_t cnt = base + (rank < extra ? 1 : 0);
+    uint64_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int rc;
+    if (cnt && (rc = pbf_msm_g1_bn254_dev(ctx, d_srs + 8 * start, coeff + 4 * start, cnt, part, s))) return rc;
+    PBF_HIP(hipMemcpyAsync(comm->send, part, 64, hipMemcpyHostToDevice, s));
+    if ((rc = ag(64))) return rc;
+    std::vector<uint64_t> all(8 * G);
+    PBF_HIP(hipMemcpyAsync(all.data(), comm->recv, 64 * G, hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    Xyzz acc = G1::identity();
+    for (uint32_t r = 0; r < G; ++r) {
+      const uint64_t* q = all.data() + 8 * r;
+      if (!(q[0] | q[1] | q[2] | q[3] | q[4] | q[5] | q[6] | q[7])) continue;  // identity
+      Affine a;
+      a.x = Fq::to_mont(u256_from_u64(q));
+      a.y = Fq::to_mont(u256_from_u64(q + 4));
+      acc = G1::add(acc, G1::from_affine(a));
+    }
+    U256 x, y;
+    G1::to_affine_plain(acc, &x, &y);
+    u256_to_u64(x, out);
+    u256_to_u64(y, out + 4);
+    return 0;
   }
 };
 
 }  // namespace
 
-extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
-                                         const uint64_t* d_abc, const uint64_t* chal, const uint64_t* rnd,
-                                         const uint64_t* k1k2, const uint64_t* d_srs, size_t srs_m, int mode,
-                                         uint64_t* out_pts, uint64_t* out_f, void* stream) {
+// Plonk::prove; comm == null (or world 1): one GPU; else this rank's part of the multi-GPU
+// split (pbf.h pbf_plonk_prove_bn254_sharded_dev)
+static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                      const uint64_t* d_abc, const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2,
+                      const uint64_t* d_srs, size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f,
+                      void* stream) {
   if (!ctx || !d_q || !d_copies || !d_abc || !chal || !rnd || !k1k2 || !d_srs || !out_pts || !out_f)
     return fail(PBF_EINVAL, "null argument");
   if (n < 8 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two >= 8");
@@ -540,6 +652,22 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   P.g_inv = hinvm(P.g);
   hout(P.w_plain, P.omega);
   hout(P.wN_plain, P.omegaN);
+  if (comm && comm->world > 1) {
+    const uint32_t G = comm->world;
+    if (G != 2 && G != 4 && G != 8) return fail(PBF_EINVAL, "world size must be 2, 4 or 8");
+    if (comm->rank >= G) return fail(PBF_EINVAL, "rank out of range");
+    if (!comm->send || !comm->recv || !comm->all_to_all || !comm->all_gather) return fail(PBF_EINVAL, "incomplete comm");
+    if (4 * (uint64_t)n < (uint64_t)G * G) return fail(PBF_EINVAL, "4n must be at least world^2");
+    P.comm = comm;
+    P.G = G;
+    P.rank = comm->rank;
+    P.nl = 4 * (uint64_t)n / G;
+    P.S = P.nl / G;
+    if (comm->capacity < 16 * P.nl * 32) return fail(PBF_EINVAL, "comm buffers below 16 * (4n / world) * 32 bytes");
+    P.shard = &ctx->buf("pv.shard");
+    int rc0 = P.shard->ensure(16 * P.nl * 32);
+    if (rc0) return rc0;
+  }
   const hipStream_t s = P.s;
   const uint64_t N = P.N;
   const U256 one = fr_one_m();
@@ -557,7 +685,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   int rc;
   if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure(3 * n * E)) || (rc = B.coef.ensure(11 * (n + 8) * E)) ||
       (rc = B.acc.ensure((n + 8) * E)) || (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure(n * E)) ||
-      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure(13 * N * E)) ||
+      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure(14 * P.count() * E)) ||
       (rc = B.t.ensure(N * E)) || (rc = B.work.ensure(3 * N * E)) || (rc = B.flag.ensure(64)) ||
       (rc = B.evals.ensure(16 * E)))
     return rc;
@@ -570,8 +698,9 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   auto C = [&](int k) { return coef + 4 * CS * k; };
   // slots: 0 a, 1 b, 2 c, 3 q_l, 4 q_r, 5 q_o, 6 q_m, 7 q_c, 8 s1, 9 s2, 10 s3
   uint64_t* coset = (uint64_t*)B.coset.p;
-  auto CE = [&](int k) { return coset + 4 * N * k; };
-  // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1
+  const uint64_t NE = P.count();  // coset evaluations held here (N; nl = N / G when sharded)
+  auto CE = [&](int k) { return coset + 4 * NE * k; };
+  // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1 [13 z(w x), sharded]
   uint64_t* work = (uint64_t*)B.work.p;
   uint64_t* W0 = work;
   uint64_t* W1 = work + 4 * N;
@@ -667,23 +796,29 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
                        one, ninv);
     PBF_HIP(hipGetLastError());
   }
-  for (int k = 0; k < 13; ++k) {
-    const uint64_t* src;
-    uint64_t len;
-    if (cmap[k] == -1) { src = zx; len = n + 3; }
-    else if (cmap[k] == -2) { src = (const uint64_t*)B.tmp0.p; len = n; }
-    else { src = C(cmap[k]); len = cmap[k] < 3 ? n + 2 : n; }
-    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, src, len,
-                       CE(k), N, P.g, (uint64_t)0);
-    PBF_HIP(hipGetLastError());
+  {
+    const uint64_t* srcs[14];
+    uint64_t lens[14];
+    U256 bases[14];
+    for (int k = 0; k < 13; ++k) {
+      if (cmap[k] == -1) { srcs[k] = zx; lens[k] = n + 3; }
+      else if (cmap[k] == -2) { srcs[k] = (const uint64_t*)B.tmp0.p; lens[k] = n; }
+      else { srcs[k] = C(cmap[k]); lens[k] = cmap[k] < 3 ? n + 2 : n; }
+      bases[k] = P.g;
+    }
+    // sharded: z(w x) gets its own slot (coefficients z_j w^j) instead of reading z at index i+4,
+    // which may sit in another rank's block
+    srcs[13] = zx; lens[13] = n + 3; bases[13] = Fr::mul(P.g, P.omega);
+    if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0)))) return rc;
   }
-  // the 13 coset slots are contiguous: one batched NTT (fuller GPU, one plan lookup)
-  if ((rc = P.ntt(P.wN_plain, CE(0), CE(0), N, 13, 0))) return rc;
   P.mark("round 3 coset NTTs (13)");
   QuotArgs qa;
   qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
   qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);
-  qa.N = N;
+  qa.zw = P.G > 1 ? CE(13) : nullptr;
+  qa.N = NE;
+  qa.N_all = N;
+  qa.blk = P.blk();
   qa.alpha = alpha; qa.beta = beta; qa.gamma = gamma; qa.k1 = k1; qa.k2 = k2;
   qa.alpha2 = Fr::mul(alpha, alpha);
   qa.g = P.g; qa.wN = P.omegaN;
@@ -699,7 +834,7 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     }
   }
   uint64_t* tq = (uint64_t*)B.t.p;
-  hipLaunchKernelGGL(k_quotient, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, qa, W0);
+  hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, qa, W0);
   PBF_HIP(hipGetLastError());
   if ((rc = P.coset_intt(W0, tq))) return rc;
   const uint64_t m = n + 2;  // coefficients per t part
@@ -775,8 +910,8 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
     PBF_HIP(hipGetLastError());
     if (mode == 0) {
       // r_3(x) = z(x) s_sigma_3(x) (beta z_w(z)) K3 (plonk.rs:414-416): the product on the coset
-      hipLaunchKernelGGL(k_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)CE(3), (const uint64_t*)CE(11),
-                         W2, N);
+      hipLaunchKernelGGL(k_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)CE(3), (const uint64_t*)CE(11),
+                         W2, NE);
       PBF_HIP(hipGetLastError());
       if ((rc = P.coset_intt(W2, W0))) return rc;
       LinComb L2;
@@ -829,15 +964,15 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   }
   // division by (x - z) on the coset: W(x_i) = P(x_i) / (x_i - z)
   uint64_t* inv = W0;
-  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, N, P.g, P.omegaN,
-                     zc);
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((N + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, N, P.d_bad);
+  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, NE, P.g,
+                     P.omegaN, zc, P.blk());
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((NE + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, NE, P.d_bad);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("z lies on the evaluation coset"))) return rc;
   if ((rc = P.coset_ntt(W2, N, W1))) return rc;  // numerator evaluations (rx no longer needed)
-  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)W1, u256_zero(),
-                     (const uint64_t*)inv, W2, N);
+  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)W1, u256_zero(),
+                     (const uint64_t*)inv, W2, NE);
   PBF_HIP(hipGetLastError());
   if ((rc = P.coset_intt(W2, W1))) return rc;  // W_z coefficients
   const uint64_t wlen = rlen - 1 > m ? rlen - 1 : m;
@@ -846,12 +981,12 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   if ((rc = P.check_bad("W_z division left a remainder (plonk.rs:438)"))) return rc;
   if ((rc = P.commit(d_srs, W1, wlen, pts[7]))) return rc;
   // W_zw = (z(x) - z_w(z)) / (x - z w)   (plonk.rs:441-442), z's coset evaluations reused
-  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((N + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, N, P.g, P.omegaN,
-                     zw);
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((N + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, N, P.d_bad);
-  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)CE(3), zw_z,
-                     (const uint64_t*)inv, W2, N);
+  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, NE, P.g,
+                     P.omegaN, zw, P.blk());
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((NE + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, NE, P.d_bad);
+  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)CE(3), zw_z,
+                     (const uint64_t*)inv, W2, NE);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("z w lies on the evaluation coset"))) return rc;
   if ((rc = P.coset_intt(W2, W1))) return rc;
@@ -865,6 +1000,22 @@ extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t*
   const U256 fo[7] = {a_z, b_z, c_z, s1_z, s2_z, r_z, zw_z};
   for (int i = 0; i < 7; ++i) hout(out_f + 4 * i, fo[i]);
   return 0;
+}
+
+extern "C" int pbf_plonk_prove_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, const uint64_t* d_copies,
+                                         const uint64_t* d_abc, const uint64_t* chal, const uint64_t* rnd,
+                                         const uint64_t* k1k2, const uint64_t* d_srs, size_t srs_m, int mode,
+                                         uint64_t* out_pts, uint64_t* out_f, void* stream) {
+  return prove_impl(ctx, nullptr, n, d_q, d_copies, d_abc, chal, rnd, k1k2, d_srs, srs_m, mode, out_pts, out_f, stream);
+}
+
+extern "C" int pbf_plonk_prove_bn254_sharded_dev(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64_t* d_q,
+                                                 const uint64_t* d_copies, const uint64_t* d_abc, const uint64_t* chal,
+                                                 const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* d_srs,
+                                                 size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f,
+                                                 void* stream) {
+  if (!comm) return fail(PBF_EINVAL, "null comm");
+  return prove_impl(ctx, comm, n, d_q, d_copies, d_abc, chal, rnd, k1k2, d_srs, srs_m, mode, out_pts, out_f, stream);
 }
 
 // host-pointer wrapper: uploads q / copies / abc / SRS, proves, returns (pts, fields)

@@ -28,7 +28,10 @@ GOLD = 0xFFFFFFFF00000001
 
 
 class GpuShardOps:
-    """The HIP kernels of libpbf.so, enqueued on `stream` (torch's stream)."""
+    """The HIP kernels of libpbf.so, enqueued on `stream` (torch's stream): u64 elements
+    (Goldilocks or a 32-bit modulus), one int64 word each."""
+
+    words = 1
 
     def __init__(self, ctx, stream: int):
         self.ctx = ctx
@@ -41,6 +44,27 @@ class GpuShardOps:
     def combine(self, modulus, omega, world, rank, src: torch.Tensor, dst: torch.Tensor, nl, batch, inverse):
         self.ctx.shard_combine_dev(modulus, omega, world, rank, src.data_ptr(), dst.data_ptr(), nl, batch, inverse,
                                    stream=self.stream)
+
+    def pointwise(self, modulus, a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, count: int):
+        self.ctx.pointwise_mul_dev(modulus, a.data_ptr(), b.data_ptr(), c.data_ptr(), count, stream=self.stream)
+
+
+class GpuFrShardOps(GpuShardOps):
+    """The same steps over BN254 Fr (4 int64 words per element; the modulus argument is
+    ignored, omega is an int below r)."""
+
+    words = 4
+
+    def local(self, modulus, omega, world, src, dst, nl, batch, inverse):
+        self.ctx.fr_shard_local_dev(omega, world, src.data_ptr(), dst.data_ptr(), nl, batch, inverse,
+                                    stream=self.stream)
+
+    def combine(self, modulus, omega, world, rank, src, dst, nl, batch, inverse):
+        self.ctx.fr_shard_combine_dev(omega, world, rank, src.data_ptr(), dst.data_ptr(), nl, batch, inverse,
+                                      stream=self.stream)
+
+    def pointwise(self, modulus, a, b, c, count):
+        self.ctx.fr_pointwise_mul_dev(a.data_ptr(), b.data_ptr(), c.data_ptr(), count, stream=self.stream)
 
 
 class ShardedNtt:
@@ -55,7 +79,8 @@ class ShardedNtt:
         self.modulus = modulus
         self.n_global = world * nl
         self.omega = omega if omega is not None else pow(7, (modulus - 1) // self.n_global, modulus)
-        shape = (batch * nl,)
+        self.words = getattr(ops, "words", 1)  # int64 words per element
+        shape = (batch * nl * self.words,)
         self.send = torch.empty(shape, dtype=torch.int64, device=device)
         self.recv = torch.empty(shape, dtype=torch.int64, device=device)
         if chunks is None:
@@ -71,7 +96,7 @@ class ShardedNtt:
         return self.comm.all_to_all_single(self.recv[sl], self.send[sl], async_op=True)
 
     def _slice(self, c: int) -> slice:
-        L = (self.batch // self.chunks) * self.nl
+        L = (self.batch // self.chunks) * self.nl * self.words
         return slice(c * L, (c + 1) * L)
 
     def _pipeline(self, first, second):
@@ -112,6 +137,32 @@ class ShardedNtt:
         """Global output index held at out[q*S + kk] on `rank`."""
         s = nl // world
         return [q * nl + rank * s + kk for q in range(world) for kk in range(s)]
+
+
+class ShardedMulNtt:
+    """mul_ntt (src/fft.rs:109-132) with every polynomial stride-sharded over the ranks
+    ("same stride layout end-to-end, no gather between NTT and
+    pointwise"). The product domain has N = la + lb = world * nl points (a power of two,
+    fft.rs:114-118); rank g holds a[g + G m] and b[g + G m] (zero-padded), and gets back the
+    stride shard c[g + G m] of the un-normalised product INTT(NTT(a) * NTT(b)). Steps: one
+    forward sharded NTT of the pair (batch 2), the pointwise product of this rank's blocks
+    (pointwise needs no exchange: both spectra have the same blocked layout), one inverse
+    sharded NTT. Two all-to-alls in total."""
+
+    def __init__(self, ops, comm, rank: int, world: int, nl: int, modulus: int = GOLD, omega: int | None = None,
+                 device: str | torch.device = "cuda"):
+        self.fwd = ShardedNtt(ops, comm, rank, world, nl, 2, modulus, omega, device, chunks=1)
+        self.inv = ShardedNtt(ops, comm, rank, world, nl, 1, modulus, self.fwd.omega, device, chunks=1)
+        self.ops, self.nl, self.modulus, self.words = ops, nl, modulus, self.fwd.words
+        self.spec = torch.empty(2 * nl * self.words, dtype=torch.int64, device=device)
+
+    def mul(self, a_shard: torch.Tensor, b_shard: torch.Tensor, c_shard: torch.Tensor) -> torch.Tensor:
+        L = self.nl * self.words
+        pair = torch.cat([a_shard.reshape(-1), b_shard.reshape(-1)])
+        self.fwd.forward(pair, self.spec)
+        prod = torch.empty(L, dtype=torch.int64, device=self.spec.device)
+        self.ops.pointwise(self.modulus, self.spec[:L], self.spec[L:], prod, self.nl)
+        return self.inv.inverse(prod, c_shard)
 
 
 class BenchSharded:
@@ -172,3 +223,137 @@ class ShardedMsm:
             u = [int(v) & m for v in p.cpu().tolist()]
             pts.append((sum(u[k] << (64 * k) for k in range(4)), sum(u[4 + k] << (64 * k) for k in range(4))))
         return self.ops.combine(pts)
+
+
+# ---------------------------------------------------------------- communicators
+class _Done:
+    def wait(self):
+        return True
+
+
+class LocalGroup:
+    """World of `world` virtual ranks in one process, one host thread each (tests and
+    single-GPU rehearsals of the multi-GPU paths): collectives meet at a barrier and move
+    data with device (or host) copies."""
+
+    def __init__(self, world: int):
+        import threading
+
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.slots = [None] * world
+
+
+class LocalComm:
+    """The torch.distributed calls the sharded paths use, for one virtual rank of a
+    LocalGroup (same signatures: all_to_all_single, all_gather, all_gather_into_tensor)."""
+
+    def __init__(self, group: LocalGroup, rank: int):
+        self.group, self.rank = group, rank
+
+    def _sync(self, t):
+        if t.is_cuda:
+            torch.cuda.current_stream().synchronize()
+
+    def _exchange(self, out, inp, pick):
+        g = self.group
+        self._sync(inp)
+        g.slots[self.rank] = inp
+        g.barrier.wait()
+        parts = out.view(g.world, -1)
+        for src in range(g.world):
+            parts[src].copy_(pick(g.slots[src]))
+        self._sync(out)
+        g.barrier.wait()  # every rank has read every slot before any input is reused
+        return _Done()
+
+    def all_to_all_single(self, out, inp, async_op=False):
+        return self._exchange(out, inp, lambda t: t.view(self.group.world, -1)[self.rank])
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        return self._exchange(out, inp, lambda t: t)
+
+    def all_gather(self, outs, inp, async_op=False):
+        flat = torch.empty(self.group.world * inp.numel(), dtype=inp.dtype, device=inp.device)
+        self._exchange(flat, inp.reshape(-1), lambda t: t.reshape(-1))
+        for k, o in enumerate(outs):
+            o.copy_(flat.view(self.group.world, -1)[k].view_as(o))
+        return _Done()
+
+
+class DistComm:
+    """torch.distributed with equal-split collectives on flat tensors; a gloo group (CPU
+    only) gets device tensors staged through the host."""
+
+    def __init__(self, dist, world: int):
+        self.dist, self.world = dist, world
+        self.staged = dist.get_backend() == "gloo"
+
+    def all_to_all_single(self, out, inp, async_op=False):
+        if self.staged and inp.is_cuda:
+            o = torch.empty(out.numel(), dtype=out.dtype)
+            self.dist.all_to_all_single(o, inp.cpu())
+            out.copy_(o.view_as(out))
+        else:
+            self.dist.all_to_all_single(out, inp)
+        return _Done()
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        src = inp.cpu() if self.staged and inp.is_cuda else inp
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        self.dist.all_gather(parts, src)
+        out.view(self.world, -1).copy_(torch.stack([p.reshape(-1) for p in parts]))
+        return _Done()
+
+    def all_gather(self, outs, inp, async_op=False):
+        return self.dist.all_gather(outs, inp)
+
+
+# ---------------------------------------------------------------- config 5 across GPUs
+class ShardedProver:
+    """Plonk::prove (src/plonk.rs:191-466) for BASELINE config 5 with its NTTs sharded across
+    the ranks (pbf_plonk_prove_bn254_sharded_dev): every rank calls prove()
+    with the same circuit, SRS, challenges and blinders on its own GPU; the library calls back
+    here for the all-to-alls of the stride-sharded 4n-point transforms and the all-gathers
+    (t / W_z / W_zw coefficients, commitment partial sums). `comm` is torch.distributed
+    (RCCL), a DistComm or a LocalComm. Returns the proof (9 points, 7 field elements as
+    limb arrays), identical on every rank and to the single-GPU prover's."""
+
+    def __init__(self, ctx, comm, rank: int, world: int, n: int, stream: int = 0, device="cuda"):
+        import ctypes
+
+        import pbf
+
+        self.ctx, self.comm, self.rank, self.world, self.n = ctx, comm, rank, world, n
+        self.stream = stream
+        nl = 4 * n // world
+        self.words = 16 * nl * 4  # 16 * nl Fr elements of 4 int64 words
+        self.send = torch.empty(self.words, dtype=torch.int64, device=device)
+        self.recv = torch.empty(self.words, dtype=torch.int64, device=device)
+        cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+        def a2a(_user, nbytes, _stream):
+            try:
+                k = nbytes // 8
+                self.comm.all_to_all_single(self.recv[:world * k], self.send[:world * k])
+                return 0
+            except Exception as e:  # surfaces as PBF_ECOMM
+                self.error = e
+                return 1
+
+        def ag(_user, nbytes, _stream):
+            try:
+                k = nbytes // 8
+                self.comm.all_gather_into_tensor(self.recv[:world * k], self.send[:k])
+                return 0
+            except Exception as e:
+                self.error = e
+                return 1
+
+        self._cbs = (cb(a2a), cb(ag))  # keep the ctypes thunks alive
+        self.error = None
+        self.c = pbf.Comm(world, rank, self.send.data_ptr(), self.recv.data_ptr(), self.words * 8, *self._cbs)
+
+    def prove(self, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m, k1k2=(2, 3), mode=1):
+        return self.ctx.plonk_prove_bn254_sharded_dev(self.c, self.n, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m,
+                                                      k1k2=k1k2, mode=mode, stream=self.stream)

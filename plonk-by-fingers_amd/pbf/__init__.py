@@ -52,6 +52,12 @@ SIGNATURES = [
     ("pbf_poly_div_u64", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, _p64, _sz, _p64, _sz, _p64,
                                         ctypes.POINTER(_sz), _p64, ctypes.POINTER(_sz)]),
     ("pbf_fill_random_u64_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _sz, _vp]),
+    ("pbf_pointwise_mul_u64_dev", ctypes.c_int, [_vp, _u64, _vp, _vp, _vp, _sz, _vp]),
+    ("pbf_ntt_fr256_shard_local_dev", ctypes.c_int, [_vp, _p64, ctypes.c_uint32, _vp, _vp, _sz, _sz, ctypes.c_int,
+                                                     _vp]),
+    ("pbf_ntt_fr256_shard_combine_dev", ctypes.c_int, [_vp, _p64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
+                                                       _sz, ctypes.c_int, _vp]),
+    ("pbf_pointwise_mul_fr256_dev", ctypes.c_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
     ("pbf_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _p64, _sz, ctypes.c_int]),
     ("pbf_ntt_fr256_batch_dev", ctypes.c_int, [_vp, _p64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
     ("pbf_mul_ntt_fr256", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64, _sz, _p64]),
@@ -72,6 +78,8 @@ SIGNATURES = [
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("pbf_plonk_verify_bn254_dev", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _sz, _p64, _p64, _p64, _p64, _p64, _p64,
                                                   ctypes.c_int, ctypes.POINTER(ctypes.c_int), _vp]),
+    ("pbf_plonk_prove_bn254_sharded_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _vp, _vp, _p64, _p64, _p64, _vp, _sz,
+                                                         ctypes.c_int, _p64, _p64, _vp]),
     ("pbf_plonk_synth_circuit_bn254_dev", ctypes.c_int, [_vp, _sz, _u64, _vp, _vp, _vp, _vp]),
     ("pbf_srs_create_bn254_dev", ctypes.c_int, [_vp, _p64, _sz, _vp, _vp]),
     ("pbf_pbh_g1_mul", ctypes.c_int, [_vp, _p32, _p32, _sz, _p32]),
@@ -219,6 +227,26 @@ class Context:
         _check(self.lib.pbf_ntt_shard_combine_dev(self.h, modulus, omega, world, rank, _vp(d_in), _vp(d_out), nl,
                                                   batch, int(inverse), _vp(stream) if stream else None))
 
+    def pointwise_mul_dev(self, modulus: int, d_a: int, d_b: int, d_c: int, count: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_pointwise_mul_u64_dev(self.h, modulus, _vp(d_a), _vp(d_b), _vp(d_c), count,
+                                                  _vp(stream) if stream else None))
+
+    def fr_shard_local_dev(self, omega: int, world: int, d_in: int, d_out: int, nl: int, batch: int,
+                           inverse: bool = False, stream: int = 0) -> None:
+        _check(self.lib.pbf_ntt_fr256_shard_local_dev(self.h, _ptr(ints_to_limbs([omega])), world, _vp(d_in),
+                                                      _vp(d_out), nl, batch, int(inverse),
+                                                      _vp(stream) if stream else None))
+
+    def fr_shard_combine_dev(self, omega: int, world: int, rank: int, d_in: int, d_out: int, nl: int, batch: int,
+                             inverse: bool = False, stream: int = 0) -> None:
+        _check(self.lib.pbf_ntt_fr256_shard_combine_dev(self.h, _ptr(ints_to_limbs([omega])), world, rank,
+                                                        _vp(d_in), _vp(d_out), nl, batch, int(inverse),
+                                                        _vp(stream) if stream else None))
+
+    def fr_pointwise_mul_dev(self, d_a: int, d_b: int, d_c: int, count: int, stream: int = 0) -> None:
+        _check(self.lib.pbf_pointwise_mul_fr256_dev(self.h, _vp(d_a), _vp(d_b), _vp(d_c), count,
+                                                    _vp(stream) if stream else None))
+
     # ---- BN254 Fr (elements as Python ints <-> 4 x u64 little-endian)
     def ntt_fr(self, omega: int, values, inverse: bool = False) -> list:
         a = ints_to_limbs(values)
@@ -331,6 +359,17 @@ class Context:
                                                    _ptr(ints_to_limbs(k1k2)), mode, ctypes.byref(ok), stream))
         return ok.value == 1
 
+    def plonk_prove_bn254_sharded_dev(self, comm: "Comm", n, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m,
+                                      k1k2=(2, 3), mode=0, stream: int = 0):
+        """This rank's part of the multi-GPU prove (include/pbf.h); comm: a Comm struct."""
+        pts = np.zeros(72, dtype=np.uint64)
+        fs = np.zeros(28, dtype=np.uint64)
+        _check(self.lib.pbf_plonk_prove_bn254_sharded_dev(self.h, ctypes.addressof(comm), n, d_q, d_copies, d_abc,
+                                                          _ptr(ints_to_limbs(chal)), _ptr(ints_to_limbs(rnd)),
+                                                          _ptr(ints_to_limbs(k1k2)), d_srs, srs_m, mode, _ptr(pts),
+                                                          _ptr(fs), stream))
+        return pts, fs
+
     # ---- plonk-by-hand types (src/pbh/*.rs), batched on the GPU
     def _u32call(self, fn, a, b, width_out, n):
         a = np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))
@@ -405,6 +444,19 @@ class Context:
 
 
 Q32 = 3221225473  # 3 * 2^30 + 1 (the reference-literal cross-check prime)
+
+
+class Comm(ctypes.Structure):
+    """struct pbf_comm (include/pbf.h): world, rank, user, send, recv, capacity and the
+    all_to_all / all_gather callbacks (CFUNCTYPE(c_int, c_void_p, c_size_t, c_void_p))."""
+
+    _fields_ = [("world", ctypes.c_uint32), ("rank", ctypes.c_uint32), ("user", ctypes.c_void_p),
+                ("send", ctypes.c_void_p), ("recv", ctypes.c_void_p), ("capacity", ctypes.c_size_t),
+                ("all_to_all", ctypes.c_void_p), ("all_gather", ctypes.c_void_p)]
+
+    def __init__(self, world, rank, send, recv, capacity, a2a, ag):
+        super().__init__(world, rank, None, send, recv, capacity, ctypes.cast(a2a, ctypes.c_void_p),
+                         ctypes.cast(ag, ctypes.c_void_p))
 
 
 def default_root(modulus: int):

@@ -125,3 +125,109 @@ def test_sharded_msm_ranges_gpu(ctx, G):
         parts.append(ops.partial(dp[8 * a:].data_ptr(), ds[4 * a:].data_ptr(), b - a))
     full = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n, stream=st)
     assert ops.combine(parts) == full
+
+
+def _fr_rand(count, seed):
+    import bn254
+
+    return bn254.limbs_to_ints(bn254.random_limbs(count, seed))
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+@pytest.mark.parametrize("nl", [1 << 4, 1 << 9, 1 << 12])
+def test_sharded_ntt_fr256(ctx, G, nl):
+    """pbf_ntt_fr256_shard_local_dev / _combine_dev: G virtual ranks, device-copy all-to-all,
+    assembled output == the single-GPU Fr NTT of the whole vector; the inverse returns the shards."""
+    import bn254
+
+    N, batch = G * nl, 2
+    w = bn254.root_of_unity(N)
+    glob = [_fr_rand(N, 31 * G + b) for b in range(batch)]
+    stream = torch.cuda.current_stream().cuda_stream
+    enc = lambda v: torch.from_numpy(bn254.ints_to_limbs(v).view(np.int64)).cuda()  # noqa: E731
+    shards = [enc([x for b in range(batch) for x in glob[b][g::G]]) for g in range(G)]
+    sends = [torch.empty_like(shards[0]) for _ in range(G)]
+    for g in range(G):
+        ctx.fr_shard_local_dev(w, G, shards[g].data_ptr(), sends[g].data_ptr(), nl, batch, stream=stream)
+    recvs = [torch.cat([sends[g].view(G, -1)[r] for g in range(G)]) for r in range(G)]
+    outs = [torch.empty_like(shards[0]) for _ in range(G)]
+    for r in range(G):
+        ctx.fr_shard_combine_dev(w, G, r, recvs[r].data_ptr(), outs[r].data_ptr(), nl, batch, stream=stream)
+    ref = torch.cat([enc(g) for g in glob])
+    ctx.ntt_fr_batch_dev(w, ref.data_ptr(), ref.data_ptr(), N, batch, stream=stream)
+    torch.cuda.synchronize()
+    refv = bn254.limbs_to_ints(ref.cpu().numpy().view(np.uint64))
+    for r in range(G):
+        got = bn254.limbs_to_ints(outs[r].cpu().numpy().view(np.uint64))
+        idx = ShardedNtt.output_indices(r, G, nl)
+        for b in range(batch):
+            assert got[b * nl:(b + 1) * nl] == [refv[b * N + i] for i in idx], (G, nl, r, b)
+    sends2 = [torch.empty_like(shards[0]) for _ in range(G)]
+    for r in range(G):
+        ctx.fr_shard_combine_dev(w, G, r, outs[r].data_ptr(), sends2[r].data_ptr(), nl, batch, inverse=True,
+                                 stream=stream)
+    recvs2 = [torch.cat([sends2[g].view(G, -1)[r] for g in range(G)]) for r in range(G)]
+    for g in range(G):
+        back = torch.empty_like(shards[0])
+        ctx.fr_shard_local_dev(w, G, recvs2[g].data_ptr(), back.data_ptr(), nl, batch, inverse=True, stream=stream)
+        torch.cuda.synchronize()
+        assert torch.equal(back, shards[g]), (G, nl, g)
+
+
+@pytest.mark.parametrize("field,G,nl", [("gold", 2, 1 << 12), ("gold", 8, 1 << 14), ("fr", 4, 1 << 10),
+                                         ("fr", 8, 1 << 8)])
+def test_sharded_mul_ntt_virtual_ranks(field, G, nl):
+    """multigpu.ShardedMulNtt (mul_ntt, fft.rs:109-132, stride-sharded end to end) with G
+    threads on this GPU: each rank's product shard equals the single-GPU mul_ntt's."""
+    import threading
+
+    import bn254
+    from multigpu import GpuFrShardOps, GpuShardOps, LocalComm, LocalGroup, ShardedMulNtt
+
+    N = G * nl
+    la = N // 2 + 5
+    lb = N - la
+    if field == "gold":
+        M, w = GOLD, pow(7, (GOLD - 1) // N, GOLD)
+        a = oracle.splitmix_field(GOLD, 61, la)
+        b = oracle.splitmix_field(GOLD, 62, lb)
+        ref = [int(x) for x in pbf.default_context().mul_ntt(GOLD, w, a, b)]
+        pad = lambda v: np.concatenate([np.asarray(v, dtype=np.uint64), np.zeros(N - len(v), dtype=np.uint64)])  # noqa
+        A, Bv = pad(a), pad(b)
+        enc = lambda v: torch.from_numpy(np.ascontiguousarray(v).view(np.int64)).cuda()  # noqa: E731
+        dec = lambda t: [int(x) for x in t.cpu().numpy().view(np.uint64)]  # noqa: E731
+        Ops = GpuShardOps
+    else:
+        M, w = bn254.R, bn254.root_of_unity(N)
+        a, b = _fr_rand(la, 63), _fr_rand(lb, 64)
+        ref = pbf.default_context().mul_ntt_fr(w, a, b)
+        A, Bv = a + [0] * (N - la), b + [0] * (N - lb)
+        enc = lambda v: torch.from_numpy(bn254.ints_to_limbs(list(v)).view(np.int64)).cuda()  # noqa: E731
+        dec = lambda t: bn254.limbs_to_ints(t.cpu().numpy().view(np.uint64))  # noqa: E731
+        Ops = GpuFrShardOps
+    group = LocalGroup(G)
+    out, errs = [None] * G, []
+
+    def rank_main(r):
+        try:
+            c = pbf.Context(0)
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                sm = ShardedMulNtt(Ops(c, st.cuda_stream), LocalComm(group, r), r, G, nl, modulus=M, omega=w)
+                cs = torch.empty(nl * Ops.words, dtype=torch.int64, device="cuda")
+                sm.mul(enc(A[r::G]), enc(Bv[r::G]), cs)
+                st.synchronize()
+                out[r] = dec(cs)
+            c.close()
+        except Exception as e:
+            errs.append(f"rank {r}: {e!r}")
+            group.barrier.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not errs, errs
+    for r in range(G):
+        assert out[r] == list(ref[r::G]), (field, G, r)
