@@ -160,6 +160,13 @@ int pbf_msm_g1_bn254(pbf_ctx* ctx, const uint64_t* points, const uint64_t* scala
                      uint64_t* out);
 int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t* d_scalars, size_t n,
                          uint64_t* out, void* stream);
+/* The same sum against a FIXED base set (KZG commitments: the SRS): out = sum_{i<n}
+ * scalars[i] * points[i], n <= n_points. The first call for a base set precomputes its
+ * window table 2^(16w) P_i (16 x n_points affine points, cached in the context and
+ * revalidated by a device fingerprint of the points on every call, so rewriting the points
+ * in place is safe); then every (point, window) digit shares one set of 2^15 buckets.     */
+int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
+                               size_t n, uint64_t* out, void* stream);
 /* out_i = scalars_i * G (G = (1, 2)), device pointers                               */
 int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t* d_out, size_t n,
                               void* stream);

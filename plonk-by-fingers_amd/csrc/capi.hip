@@ -72,6 +72,7 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
   pbf_ctx* c = new pbf_ctx();
   c->device = device;
   c->fork.device = device;
+  c->msm_tail.device = device;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;

@@ -85,6 +85,21 @@ struct ForkSet {
   ~ForkSet();
 };
 
+// The asynchronous tail of the fixed-base MSM (msm.hip msm_fixed_device): after the
+// accumulation, the latency-bound bucket join and reduction run on a context-owned side
+// stream while the caller's stream goes on; MSM_TAIL_SLOTS workspaces rotate between the
+// MSMs in flight. msm_fixed_wait orders a stream after every tail enqueued so far.
+constexpr int MSM_TAIL_SLOTS = 3;
+struct MsmTail {
+  int device = 0;
+  hipStream_t aux = nullptr;
+  hipEvent_t ready[MSM_TAIL_SLOTS] = {}, done[MSM_TAIL_SLOTS] = {};
+  bool used[MSM_TAIL_SLOTS] = {};
+  int next = 0, last = -1;
+  int ensure();
+  ~MsmTail();  // waits for the side stream (declared after the buffers it uses)
+};
+
 // Build a plan (validates omega's order and n^-1). Returns PBF status.
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p);
 // Enqueue a batched transform of a planned size on `stream` (d_in may equal d_out).
@@ -125,6 +140,12 @@ struct pbf_ctx {
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, int>, std::unique_ptr<pbf::NttPlan>> plans;
   pbf::DevBuf scratch0, scratch1, scratch2, io0, io1, io2, partial;
   pbf::ForkSet fork;  // aux streams of the NTT group schedule (this context only)
+  // fixed-base MSM window table (msm.hip msm_fixed_table): the points it was built from
+  struct FixedBase {
+    const void* ptr = nullptr;
+    uint64_t n = 0, fingerprint = 0;
+    pbf::DevBuf table;
+  } fixed_base;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::unique_ptr<pbf::TwoLevel>> two_level;
   int roots(uint64_t m, uint64_t root, uint64_t n, pbf::TwoLevel** out);
   // `_dev` entry points enqueue on exactly the stream they are given (NULL = the
@@ -139,4 +160,5 @@ struct pbf_ctx {
     if (!b) b.reset(new pbf::DevBuf());
     return *b;
   }
+  pbf::MsmTail msm_tail;  // destroyed before `named`: its stream drains first
 };

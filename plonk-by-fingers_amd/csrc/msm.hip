@@ -20,8 +20,7 @@
 #include <hipcub/hipcub.hpp>
 #include <vector>
 #include "../../include/pbf.h"
-#include "ec_bn254.hpp"
-#include "internal.hpp"
+#include "msm.hpp"
 
 namespace pbf {
 
@@ -82,10 +81,10 @@ __global__ void msm_digits(const uint64_t* scalars, const uint8_t* inf, uint32_t
   }
 }
 
-__global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* start, uint32_t* end) {
+__global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* start, uint32_t* end, uint32_t sent) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t k = keys[j];
-    if (k == MSM_SENTINEL) continue;
+    if (k == sent) continue;
     if (j == 0 || keys[j - 1] != k) start[k] = (uint32_t)j;
     if (j == m - 1 || keys[j + 1] != k) end[k] = (uint32_t)(j + 1);
   }
@@ -104,7 +103,7 @@ constexpr uint32_t MSM_CH = PBF_MSM_CH;  // sorted entries per accumulation thre
 
 struct ChunkPart {
   Xyzz acc;
-  uint32_t key;  // MSM_SENTINEL: no partial
+  uint32_t key;  // the sentinel key: no partial
   uint32_t pad[3];
 };
 
@@ -114,16 +113,16 @@ struct ChunkPart {
 // this chunk and ends in a later one. Buckets with no entry stay zero (ZZ = 0: identity).
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE))) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
                                                      const uint32_t* start, const uint32_t* end, uint32_t m,
-                                                     Xyzz* buckets, ChunkPart* head, ChunkPart* tail) {
+                                                     Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c0 = t * MSM_CH;
   if (c0 >= m) return;
   const uint32_t c1 = c0 + MSM_CH < m ? c0 + MSM_CH : m;
   uint32_t cur = keys[c0], rs = c0;
   Xyzz acc = G1::identity();
-  head[t].key = MSM_SENTINEL;
-  tail[t].key = MSM_SENTINEL;
-  if (cur == MSM_SENTINEL) return;  // past the valid prefix (zero digits sort last)
+  head[t].key = sent;
+  tail[t].key = sent;
+  if (cur == sent) return;  // past the valid prefix (zero digits sort last)
   auto flush = [&](uint32_t re) {
     const uint32_t bs = start[cur], be = end[cur];
     if (bs < rs) {  // continues a bucket of an earlier chunk (possibly spanning this one)
@@ -150,7 +149,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
     }
     if (k != cur) {
       flush(j);
-      if (k == MSM_SENTINEL) return;
+      if (k == sent) return;
       cur = k;
       rs = j;
       acc = G1::identity();
@@ -164,11 +163,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
 // one thread per chunk owning a boundary-crossing bucket: its tail plus the heads of the
 // following chunks the bucket covers
 __global__ void __launch_bounds__(256) msm_chunk_join(const ChunkPart* head, const ChunkPart* tail,
-                                                      const uint32_t* end, uint32_t nchunks, Xyzz* buckets) {
+                                                      const uint32_t* end, uint32_t nchunks, Xyzz* buckets,
+                                                      uint32_t sent) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nchunks) return;
   const uint32_t k = tail[t].key;
-  if (k == MSM_SENTINEL) return;
+  if (k == sent) return;
   Xyzz acc = tail[t].acc;
   const uint32_t be = end[k];
   for (uint32_t u = t + 1; u < nchunks && u * MSM_CH < be; ++u) acc = G1::add(acc, head[u].acc);
@@ -191,9 +191,9 @@ __device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
 constexpr uint32_t MSM_SEG = PBF_MSM_SEG;
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_SEG_WPE))) msm_segments(const Xyzz* buckets, Xyzz* shares) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_SEG_WPE))) msm_segments(const Xyzz* buckets, Xyzz* shares, uint32_t nw) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= MSM_NW * MSM_NSEG) return;
+  if (id >= nw * MSM_NSEG) return;
   const uint32_t w = id / MSM_NSEG, seg = id % MSM_NSEG;
   const uint32_t a = seg * MSM_SEG;
   const Xyzz* B = buckets + (uint64_t)w * MSM_NB;
@@ -227,6 +227,164 @@ __global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz*
 // workgroup w: the window sum from its MSM_NPART partial sums
 __global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* parts, Xyzz* sums) {
   msm_tree_sum(parts + (uint64_t)blockIdx.x * MSM_NPART, MSM_NPART, sums + blockIdx.x);
+}
+
+// ---------------------------------------------------------------- fixed-base MSM
+// KZG commitments are MSMs against the fixed SRS (plonk.rs:51-58), so the SRS points can be
+// precomputed once per window: table[w][i] = 2^(16 w) P_i (affine, Montgomery). Every
+// (point, window) digit then goes to ONE set of 2^15 buckets (bucket |d| - 1 of entry
+// table[w][i], negated for d < 0): the same 16 n mixed additions as the windowed form, but
+// one bucket reduction instead of 16, no Horner over windows, 16-bit sort keys, and no
+// per-call conversion of the points. 16 n x 64 B of table (1 GiB per 2^20 points).
+
+// table window w from window w-1: 16 doublings in XYZZ, then affine through a
+// block-wide batch inversion of the ZZZ (prefix and suffix products in LDS, one Fermat
+// inversion per block); the identity (0, 0) stays (0, 0)
+__global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affine* next, uint64_t n) {
+  __shared__ U256 pre[256], suf[256];
+  __shared__ U256 tinv;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + t;
+  const U256 one = G1::one_m();
+  bool id = true;
+  Xyzz acc = G1::identity();
+  if (i < n) {
+    const Affine a = prev[i];
+    id = Fq::is_zero(a.x) && Fq::is_zero(a.y);
+    if (!id) {
+      acc = G1::mdbl(a);
+      for (int k = 1; k < MSM_C; ++k) acc = G1::dbl(acc);
+    }
+  }
+  const U256 z = id ? one : acc.ZZZ;
+  pre[t] = z;
+  suf[t] = z;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {  // inclusive prefix / suffix products
+    U256 p = pre[t], q = suf[t];
+    if (t >= off) p = Fq::mul(pre[t - off], p);
+    if (t + off < 256) q = Fq::mul(q, suf[t + off]);
+    __syncthreads();
+    pre[t] = p;
+    suf[t] = q;
+    __syncthreads();
+  }
+  if (t == 0) tinv = G1::inv(pre[255]);
+  __syncthreads();
+  if (i >= n) return;
+  Affine r;
+  if (id) {
+    r.x = u256_zero();
+    r.y = u256_zero();
+  } else {
+    U256 izzz = tinv;  // 1 / ZZZ_t = tinv * prod_{u<t} * prod_{u>t}
+    if (t > 0) izzz = Fq::mul(izzz, pre[t - 1]);
+    if (t < 255) izzz = Fq::mul(izzz, suf[t + 1]);
+    const U256 q = Fq::mul(acc.ZZ, izzz);
+    const U256 izz = Fq::mul(q, q);
+    r.x = Fq::mul(acc.X, izz);
+    r.y = Fq::mul(acc.Y, izzz);
+  }
+  next[i] = r;
+}
+
+// one (key, value) per (point, window): key = |d| - 1 (MSM_NB: zero digit or identity point),
+// value = index of table[w][first + i] | sign
+__global__ void msm_fixed_digits(const uint64_t* scalars, const Affine* table, uint64_t n_table, uint64_t first,
+                                 uint32_t* keys, uint32_t* vals, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = scalars + 4 * i;
+    const Affine p = table[first + i];
+    const bool skip = Fq::is_zero(p.x) && Fq::is_zero(p.y);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < MSM_NW; ++w) {
+      uint32_t d = (uint32_t)((s[w / 4] >> (16 * (w % 4))) & 0xFFFF) + carry;
+      bool neg = false;
+      if (d > MSM_NB) {
+        d = (1u << MSM_C) - d;
+        neg = true;
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? MSM_NB : (d - 1);
+      vals[(uint64_t)w * n + i] = (uint32_t)((uint64_t)w * n_table + first + i) | (neg ? MSM_NEG : 0u);
+    }
+  }
+}
+
+// Boundary join for large buckets (the fixed-base form: ~16 n / 2^15 entries per bucket, 512
+// at 2^20 points, so a bucket crossing chunks spans ~16 of them). Tree over each bucket's
+// continuation partials head[o+1 .. e] (o = chunk of the bucket's first entry, e = chunk of
+// its last): at step s, the continuation at o + 1 + 2 s j adds head[o + 1 + 2 s j + s] when
+// that is <= e. After ceil(log2(span)) steps head[o+1] holds their sum; msm_join_final adds
+// it to the owner's tail partial. One work item per (bucket, j) -- not per chunk, so the
+// waves of a step hold only adding lanes (a per-chunk grid kept every wave busy at every
+// step for a shrinking share of active lanes).
+// the largest number of chunks a bucket spans (bounds the tree steps that do any work)
+__global__ void __launch_bounds__(256) msm_max_span(const uint32_t* start, const uint32_t* end, uint32_t nb,
+                                                    uint32_t* span) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nb || end[k] <= start[k]) return;
+  atomicMax(span, (end[k] - 1) / MSM_CH - start[k] / MSM_CH);
+}
+__global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint32_t* start, const uint32_t* end,
+                                                     uint32_t nb, uint32_t step, const uint32_t* span) {
+  const uint32_t sp = *span;
+  if (step >= sp) return;  // every bucket's continuations already summed
+  const uint32_t per = (sp + 2 * step - 1) / (2 * step);  // pair slots per bucket
+  const uint64_t items = (uint64_t)nb * per;
+  for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < items;
+       id += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = (uint32_t)(id / per), j = (uint32_t)(id % per);
+    const uint32_t bs = start[k], be = end[k];
+    if (be <= bs) continue;
+    const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+    const uint32_t u = o + 1 + 2 * step * j;
+    if (u + step <= e) head[u].acc = G1::add(head[u].acc, head[u + step].acc);
+  }
+}
+__global__ void __launch_bounds__(256) msm_join_final(const ChunkPart* head, const ChunkPart* tail, uint32_t nchunks,
+                                                      Xyzz* buckets, uint32_t sent) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nchunks) return;
+  const uint32_t k = tail[t].key;
+  if (k == sent) return;
+  buckets[k] = G1::add(tail[t].acc, head[t + 1].acc);  // a tail always has a continuation
+}
+
+// 64-bit fingerprint of n canonical affine points (8 u64 each): block XORs of a position-
+// mixed hash, then one block folds them (validates a cached table against the points)
+__device__ __forceinline__ uint64_t fp_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(256) msm_fingerprint(const uint64_t* pts, uint64_t words, uint64_t* partial) {
+  __shared__ uint64_t red[256];
+  uint64_t h = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < words; j += (uint64_t)gridDim.x * 256)
+    h ^= fp_mix(pts[j] + 0x9E3779B97F4A7C15ull * (j + 1));
+  red[threadIdx.x] = h;
+  __syncthreads();
+  for (uint32_t st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] ^= red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+__global__ void __launch_bounds__(256) msm_fingerprint_fold(const uint64_t* partial, uint32_t count, uint64_t* out) {
+  __shared__ uint64_t red[256];
+  uint64_t h = 0;
+  for (uint32_t j = threadIdx.x; j < count; j += 256) h ^= partial[j];
+  red[threadIdx.x] = h;
+  __syncthreads();
+  for (uint32_t st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) red[threadIdx.x] ^= red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
 }
 
 // Fixed-base comb for s * G (SRS::create): table[w][d-1] = d * 2^(8w) * G (affine,
@@ -347,7 +505,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   PBF_HIP(hipMemsetAsync(w.start.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
-                     (uint32_t*)w.start.p, (uint32_t*)w.end.p);
+                     (uint32_t*)w.start.p, (uint32_t*)w.end.p, MSM_SENTINEL);
   // the valid (non-sentinel) prefix of the sorted list: the sentinel sorts last; its
   // length is known only on the device, so chunks past it return at once
   PBF_HIP(hipMemsetAsync(w.buckets.p, 0, (uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz), s));
@@ -355,11 +513,11 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
                      (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
-                     (ChunkPart*)w.tail.p);
+                     (ChunkPart*)w.tail.p, MSM_SENTINEL);
   hipLaunchKernelGGL(msm_chunk_join, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const ChunkPart*)w.head.p,
-                     (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p);
+                     (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p, MSM_SENTINEL);
   hipLaunchKernelGGL(msm_segments, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
-                     (Xyzz*)w.shares.p);
+                     (Xyzz*)w.shares.p, (uint32_t)MSM_NW);
   hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW * MSM_NPART), dim3(MSM_SEG_THREADS), 0, s,
                      (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
   hipLaunchKernelGGL(msm_window_final, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.parts.p,
@@ -380,6 +538,160 @@ static void msm_finish_host(const Xyzz* sums, uint64_t* out) {
     out[i] = (uint64_t)x.w[2 * i] | ((uint64_t)x.w[2 * i + 1] << 32);
     out[4 + i] = (uint64_t)y.w[2 * i] | ((uint64_t)y.w[2 * i + 1] << 32);
   }
+}
+
+// ---- fixed-base tables: cached per context, validated by a fingerprint of the points
+constexpr uint32_t FP_BLOCKS = 1024;
+
+static int msm_fingerprint_host(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, uint64_t* out) {
+  DevBuf& fp = ctx->buf("msm.fp");
+  int rc = fp.ensure((FP_BLOCKS + 1) * 8);
+  if (rc) return rc;
+  uint64_t* part = (uint64_t*)fp.p;
+  hipLaunchKernelGGL(msm_fingerprint, dim3(FP_BLOCKS), dim3(256), 0, s, d_pts, 8 * n, part);
+  hipLaunchKernelGGL(msm_fingerprint_fold, dim3(1), dim3(256), 0, s, (const uint64_t*)part, FP_BLOCKS, part + FP_BLOCKS);
+  PBF_HIP(hipGetLastError());
+  PBF_HIP(hipMemcpyAsync(out, part + FP_BLOCKS, 8, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+// the window table of the n points at d_pts (built on first use; rebuilt when the points at
+// that address changed)
+int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
+  if (n == 0 || n > 0x7FFFFFFFull / MSM_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
+  uint64_t fp = 0;
+  int rc = msm_fingerprint_host(ctx, d_pts, n, s, &fp);
+  if (rc) return rc;
+  auto& fb = ctx->fixed_base;
+  if (fb.ptr == (const void*)d_pts && fb.n == n && fb.fingerprint == fp && fb.table.p) {
+    *out = (const Affine*)fb.table.p;
+    return 0;
+  }
+  if ((rc = fb.table.ensure((uint64_t)MSM_NW * n * sizeof(Affine)))) return rc;
+  Affine* tbl = (Affine*)fb.table.p;
+  DevBuf& inf = ctx->buf("msm.inf");
+  if ((rc = inf.ensure(n))) return rc;
+  hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, tbl, (uint8_t*)inf.p, n);
+  for (int w = 1; w < MSM_NW; ++w)
+    hipLaunchKernelGGL(msm_table_window, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       (const Affine*)(tbl + (uint64_t)(w - 1) * n), tbl + (uint64_t)w * n, n);
+  PBF_HIP(hipGetLastError());
+  fb.ptr = d_pts;
+  fb.n = n;
+  fb.fingerprint = fp;
+  *out = tbl;
+  return 0;
+}
+
+int MsmTail::ensure() {
+  if (aux) return 0;
+  PBF_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+  for (int i = 0; i < MSM_TAIL_SLOTS; ++i) {
+    PBF_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
+    PBF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  }
+  return 0;
+}
+MsmTail::~MsmTail() {
+  if (!aux) return;
+  (void)hipSetDevice(device);
+  (void)hipStreamSynchronize(aux);
+  (void)hipStreamDestroy(aux);
+  for (int i = 0; i < MSM_TAIL_SLOTS; ++i) {
+    if (ready[i]) (void)hipEventDestroy(ready[i]);
+    if (done[i]) (void)hipEventDestroy(done[i]);
+  }
+}
+
+int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s) {
+  MsmTail& t = ctx->msm_tail;
+  if (t.last >= 0) PBF_HIP(hipStreamWaitEvent(s, t.done[t.last], 0));  // the side stream is in order
+  return 0;
+}
+
+// sum_i scalars[i] * P_(first + i), i < n, against a window table of n_table points; the
+// result (XYZZ, Montgomery) is written to *d_result on the device (nothing waits for it).
+// On `s`: digits, sort, bucket bounds, accumulation (throughput-bound, the whole chip).
+// On the context's side stream: the boundary join and the bucket reduction (latency-bound
+// chains of a few hundred waves), overlapping whatever the caller enqueues next on `s`.
+int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64_t first, const uint64_t* d_sc,
+                     uint64_t n, hipStream_t s, Xyzz* d_result) {
+  if (first + n > n_table) return fail(PBF_EINVAL, "fixed-base MSM: range beyond the table");
+  const uint64_t m = n * MSM_NW;
+  MsmTail& tl = ctx->msm_tail;
+  int rc;
+  if ((rc = tl.ensure())) return rc;
+  const int slot = tl.next;
+  const std::string pre = "msm.f" + std::to_string(slot) + ".";
+  DevBuf &keys = ctx->buf("msm.keys"), &vals = ctx->buf("msm.vals"), &keys2 = ctx->buf("msm.keys2"),
+         &vals2 = ctx->buf("msm.vals2"), &temp = ctx->buf("msm.temp");
+  DevBuf &start = ctx->buf(pre + "start"), &end = ctx->buf(pre + "end"), &buckets = ctx->buf(pre + "buckets"),
+         &shares = ctx->buf(pre + "shares"), &parts = ctx->buf(pre + "parts"), &head = ctx->buf(pre + "head"),
+         &tail = ctx->buf(pre + "tail"), &spb = ctx->buf(pre + "span");
+  // a slot's buffers may still be read by its previous tail: reallocation waits for it
+  if (tl.used[slot]) PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
+  const uint64_t hbytes = (m / MSM_CH + 1) * sizeof(ChunkPart);
+  if ((head.bytes < hbytes || tail.bytes < hbytes) && tl.used[slot]) PBF_HIP(hipEventSynchronize(tl.done[slot]));
+  if ((rc = keys.ensure(m * 4)) || (rc = vals.ensure(m * 4)) || (rc = keys2.ensure(m * 4)) ||
+      (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)MSM_NB * 4)) ||
+      (rc = end.ensure((uint64_t)MSM_NB * 4)) || (rc = buckets.ensure((uint64_t)MSM_NB * sizeof(Xyzz))) ||
+      (rc = shares.ensure((uint64_t)MSM_NSEG * sizeof(Xyzz))) || (rc = parts.ensure(MSM_NPART * sizeof(Xyzz))) ||
+      (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) || (rc = spb.ensure(4)))
+    return rc;
+  hipLaunchKernelGGL(msm_fixed_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, table, n_table, first,
+                     (uint32_t*)keys.p, (uint32_t*)vals.p, n);
+  size_t temp_bytes = 0;
+  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
+                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, MSM_BB + 1, s));
+  if ((rc = temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
+  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
+                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, MSM_BB + 1, s));
+  PBF_HIP(hipMemsetAsync(start.p, 0, (uint64_t)MSM_NB * 4, s));
+  PBF_HIP(hipMemsetAsync(end.p, 0, (uint64_t)MSM_NB * 4, s));
+  hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
+                     (uint32_t*)start.p, (uint32_t*)end.p, MSM_NB);
+  PBF_HIP(hipMemsetAsync(buckets.p, 0, (uint64_t)MSM_NB * sizeof(Xyzz), s));
+  PBF_HIP(hipMemsetAsync(spb.p, 0, 4, s));
+  const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
+  hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
+                     (const uint32_t*)vals2.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)m,
+                     (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p, MSM_NB);
+  hipLaunchKernelGGL(msm_max_span, dim3(MSM_NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
+                     (const uint32_t*)end.p, MSM_NB, (uint32_t*)spb.p);
+  PBF_HIP(hipGetLastError());
+  // ---- the tail, on the side stream
+  hipStream_t a = tl.aux;
+  PBF_HIP(hipEventRecord(tl.ready[slot], s));
+  PBF_HIP(hipStreamWaitEvent(a, tl.ready[slot], 0));
+  // ceil(log2(nchunks)) steps bound any span; steps past the largest span exit at once. The
+  // grid covers the mean span's pair slots (the kernel strides over the rest).
+  const uint64_t mean_span = m / ((uint64_t)MSM_NB * MSM_CH) + 2;
+  for (uint32_t step = 1; step < nchunks; step <<= 1) {
+    const uint64_t items = (uint64_t)MSM_NB * ((mean_span + 2 * step - 1) / (2 * step));
+    hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
+                       (const uint32_t*)start.p, (const uint32_t*)end.p, MSM_NB, step, (const uint32_t*)spb.p);
+  }
+  hipLaunchKernelGGL(msm_join_final, dim3((nchunks + 255) / 256), dim3(256), 0, a, (const ChunkPart*)head.p,
+                     (const ChunkPart*)tail.p, nchunks, (Xyzz*)buckets.p, MSM_NB);
+  hipLaunchKernelGGL(msm_segments, dim3((MSM_NSEG + 255) / 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
+                     (Xyzz*)shares.p, 1u);
+  hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NPART), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)shares.p,
+                     (Xyzz*)parts.p);
+  hipLaunchKernelGGL(msm_window_final, dim3(1), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)parts.p, d_result);
+  PBF_HIP(hipGetLastError());
+  PBF_HIP(hipEventRecord(tl.done[slot], a));
+  tl.used[slot] = true;
+  tl.last = slot;
+  tl.next = (slot + 1) % MSM_TAIL_SLOTS;
+  return 0;
+}
+
+void xyzz_to_affine_u64(const Xyzz& p, uint64_t* out) {
+  U256 x, y;
+  G1::to_affine_plain(p, &x, &y);
+  u256_to_u64(x, out);
+  u256_to_u64(y, out + 4);
 }
 
 static bool host_fq_canonical(const uint64_t* v) {
@@ -435,6 +747,29 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
   PBF_HIP(hipMemcpyAsync(sums.data(), w.sums.p, MSM_NW * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
   msm_finish_host(sums.data(), out);
+  return PBF_OK;
+}
+
+// SRS::eval_at_s against a fixed base set (KZG commitments): the first call for a base set
+// builds its window table (cached in the context, revalidated by a fingerprint each call)
+int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
+                               size_t n, uint64_t* out, void* stream) {
+  if (!ctx || !out || (n && (!d_points || !d_scalars))) return fail(PBF_EINVAL, "null argument");
+  if (n > n_points) return fail(PBF_EINVAL, "more scalars than base points");
+  if (n == 0) { for (int i = 0; i < 8; ++i) out[i] = 0; return PBF_OK; }
+  PBF_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  const Affine* tbl;
+  int rc = msm_fixed_table(ctx, d_points, n_points, s, &tbl);
+  if (rc) return rc;
+  DevBuf& res = ctx->buf("msm.fixed_result");
+  if ((rc = res.ensure(sizeof(Xyzz)))) return rc;
+  if ((rc = msm_fixed_device(ctx, tbl, n_points, 0, d_scalars, n, s, (Xyzz*)res.p))) return rc;
+  if ((rc = msm_fixed_wait(ctx, s))) return rc;
+  Xyzz r;
+  PBF_HIP(hipMemcpyAsync(&r, res.p, sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  xyzz_to_affine_u64(r, out);
   return PBF_OK;
 }
 

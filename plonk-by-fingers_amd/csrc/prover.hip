@@ -28,8 +28,7 @@
 #include <ctime>
 #include <vector>
 #include "../../include/pbf.h"
-#include "ec_bn254.hpp"
-#include "internal.hpp"
+#include "msm.hpp"
 
 namespace pbf {
 
@@ -583,34 +582,41 @@ struct Prover {
     PBF_HIP(hipGetLastError());
     return 0;
   }
-  // SRS::eval_at_s (plonk.rs:51-58); sharded: this rank's point range, partial sums
-  // all-gathered (64 B per rank) and added on the host
-  int commit(const uint64_t* d_srs, const uint64_t* coeff, uint64_t len, uint64_t* out) {
-    if (G == 1) return pbf_msm_g1_bn254_dev(ctx, d_srs, coeff, len, out, s);
+  // SRS::eval_at_s (plonk.rs:51-58) as a fixed-base MSM against the SRS window table
+  // (msm.hpp), its XYZZ result left in device slot `slot` (finish_commits collects all of
+  // them with one copy: the challenges are inputs, nothing waits on a commitment). Sharded:
+  // this rank's point range; the G partial sums are all-gathered into the slot's G entries.
+  const Affine* srs_tbl = nullptr;
+  uint64_t srs_n = 0;
+  Xyzz* slots = nullptr;  // 9 x G
+  int commit(const uint64_t* coeff, uint64_t len, int slot) {
+    if (G == 1) return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot);
     const uint64_t base = len / G, extra = len % G;
     const uint64_t start = rank * base + (rank < extra ? rank : extra);
     const uint64_t cnt = base + (rank < extra ? 1 : 0);
-    uint64_t part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int rc;
-    if (cnt && (rc = pbf_msm_g1_bn254_dev(ctx, d_srs + 8 * start, coeff + 4 * start, cnt, part, s))) return rc;
-    PBF_HIP(hipMemcpyAsync(comm->send, part, 64, hipMemcpyHostToDevice, s));
-    if ((rc = ag(64))) return rc;
-    std::vector<uint64_t> all(8 * G);
-    PBF_HIP(hipMemcpyAsync(all.data(), comm->recv, 64 * G, hipMemcpyDeviceToHost, s));
-    PBF_HIP(hipStreamSynchronize(s));
-    Xyzz acc = G1::identity();
-    for (uint32_t r = 0; r < G; ++r) {
-      const uint64_t* q = all.data() + 8 * r;
-      if (!(q[0] | q[1] | q[2] | q[3] | q[4] | q[5] | q[6] | q[7])) continue;  // identity
-      Affine a;
-      a.x = Fq::to_mont(u256_from_u64(q));
-      a.y = Fq::to_mont(u256_from_u64(q + 4));
-      acc = G1::add(acc, G1::from_affine(a));
+    if (cnt) {
+      if ((rc = msm_fixed_device(ctx, srs_tbl, srs_n, start, coeff + 4 * start, cnt, s, (Xyzz*)comm->send)) ||
+          (rc = msm_fixed_wait(ctx, s)))
+        return rc;
+    } else {
+      PBF_HIP(hipMemsetAsync(comm->send, 0, sizeof(Xyzz), s));  // ZZ = 0: the identity
     }
-    U256 x, y;
-    G1::to_affine_plain(acc, &x, &y);
-    u256_to_u64(x, out);
-    u256_to_u64(y, out + 4);
+    if ((rc = ag(sizeof(Xyzz)))) return rc;
+    PBF_HIP(hipMemcpyAsync(slots + (uint64_t)slot * G, comm->recv, G * sizeof(Xyzz), hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
+  int finish_commits(int count, uint64_t (*out)[8]) {
+    std::vector<Xyzz> h((size_t)count * G);
+    int rc = msm_fixed_wait(ctx, s);
+    if (rc) return rc;
+    PBF_HIP(hipMemcpyAsync(h.data(), slots, h.size() * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < count; ++k) {
+      Xyzz acc = h[(size_t)k * G];
+      for (uint32_t r = 1; r < G; ++r) acc = G1::add(acc, h[(size_t)k * G + r]);
+      xyzz_to_affine_u64(acc, out[k]);
+    }
     return 0;
   }
 };
@@ -691,6 +697,13 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     return rc;
   P.d_bad = (int*)B.flag.p;
   PBF_HIP(hipMemsetAsync(P.d_bad, 0, sizeof(int), s));
+  {
+    DevBuf& sl = ctx->buf("pv.commits");
+    if ((rc = sl.ensure(9 * (uint64_t)P.G * sizeof(Xyzz)))) return rc;
+    P.slots = (Xyzz*)sl.p;
+    P.srs_n = srs_m;
+    if ((rc = msm_fixed_table(ctx, d_srs, srs_m, s, &P.srs_tbl))) return rc;  // built once per SRS
+  }
   uint64_t* hpow = (uint64_t*)B.hpow.p;
   uint64_t* sigma = (uint64_t*)B.sigma.p;
   const uint64_t CS = n + 8;  // coefficient slot (room for blinding terms up to x^(n+2))
@@ -743,7 +756,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   PBF_HIP(hipGetLastError());
   uint64_t pts[9][8];
   for (int k = 0; k < 3; ++k)
-    if ((rc = P.commit(d_srs, C(k), n + 2, pts[k]))) return rc;
+    if ((rc = P.commit(C(k), n + 2, k))) return rc;
   P.mark("round 1 commits (3 MSM)");
 
   // ---- round 2: accumulator (plonk.rs:278-313)
@@ -783,7 +796,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   }
   uint64_t* zx = acc;  // length n+3
   P.mark("round 2 accumulator");
-  if ((rc = P.commit(d_srs, zx, n + 3, pts[3]))) return rc;
+  if ((rc = P.commit(zx, n + 3, 3))) return rc;
   P.mark("round 2 commit (MSM)");
 
   // ---- round 3: quotient on the coset g H_4n (plonk.rs:326-382)
@@ -842,10 +855,10 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)")))
     return rc;
-  if ((rc = P.commit(d_srs, tq, m, pts[4]))) return rc;            // t_lo
+  if ((rc = P.commit(tq, m, 4))) return rc;            // t_lo
   P.mark("round 3 quotient + INTT");
-  if ((rc = P.commit(d_srs, tq + 4 * m, m, pts[5]))) return rc;    // t_mid
-  if ((rc = P.commit(d_srs, tq + 8 * m, m, pts[6]))) return rc;    // t_hi
+  if ((rc = P.commit(tq + 4 * m, m, 5))) return rc;    // t_mid
+  if ((rc = P.commit(tq + 8 * m, m, 6))) return rc;    // t_hi
   P.mark("round 3 commits (3 MSM)");
 
   // ---- round 4: evaluations at z (plonk.rs:393-399), linearisation r(x) (:401-422)
@@ -979,7 +992,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - wlen)), dim3(256), 0, s, (const uint64_t*)W1, wlen, N, P.d_bad);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("W_z division left a remainder (plonk.rs:438)"))) return rc;
-  if ((rc = P.commit(d_srs, W1, wlen, pts[7]))) return rc;
+  if ((rc = P.commit(W1, wlen, 7))) return rc;
   // W_zw = (z(x) - z_w(z)) / (x - z w)   (plonk.rs:441-442), z's coset evaluations reused
   hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, NE, P.g,
                      P.omegaN, zw, P.blk());
@@ -993,7 +1006,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - (n + 2))), dim3(256), 0, s, (const uint64_t*)W1, n + 2, N, P.d_bad);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("W_zw division left a remainder (plonk.rs:442)"))) return rc;
-  if ((rc = P.commit(d_srs, W1, n + 2, pts[8]))) return rc;
+  if ((rc = P.commit(W1, n + 2, 8))) return rc;
+  if ((rc = P.finish_commits(9, pts))) return rc;
   P.mark("round 5 openings + 2 MSM");
 
   for (int i = 0; i < 9; ++i) memcpy(out_pts + 8 * i, pts[i], 64);

@@ -65,6 +65,7 @@ SIGNATURES = [
     ("pbf_msm_g1_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
     ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
     ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    ("pbf_msm_g1_bn254_fixed_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, _p64, _vp]),
     ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
     ("pbf_pairing_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
     ("pbf_pairing_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
@@ -288,6 +289,14 @@ class Context:
                                              _vp(stream) if stream else None))
         x, y = limbs_to_ints(out)
         return (x, y)
+
+    def msm_g1_fixed_dev(self, d_points: int, n_points: int, d_scalars: int, n: int, stream: int = 0) -> tuple:
+        """sum_{i<n} s_i P_i against the fixed base set of n_points points (KZG commit)."""
+        out = np.zeros(8, dtype=np.uint64)
+        _check(self.lib.pbf_msm_g1_bn254_fixed_dev(self.h, _vp(d_points), n_points, _vp(d_scalars), n, _ptr(out),
+                                                   _vp(stream) if stream else None))
+        v = limbs_to_ints(out)
+        return v[0], v[1]
 
     def g1_mul_base_dev(self, d_scalars: int, d_out: int, n: int, stream: int = 0) -> None:
         _check(self.lib.pbf_g1_bn254_mul_base_dev(self.h, _vp(d_scalars), _vp(d_out), n,

@@ -150,3 +150,70 @@ def test_fixed_base_comb_matches_double_and_add(ctx, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert a[:8].tolist() == [0] * 8  # 0 * G = identity
+
+
+def _dev_points(pts):
+    import torch
+
+    return torch.from_numpy(pbf._g1_limbs(pts).view(np.int64)).cuda()
+
+
+def _dev_scalars(sc):
+    import torch
+
+    return torch.from_numpy(pbf.ints_to_limbs(sc).view(np.int64)).cuda()
+
+
+@pytest.mark.parametrize("n_points,n", [(1, 1), (7, 7), (300, 300), (300, 17), (4096, 4000)])
+def test_fixed_base_msm_vs_naive_fold(ctx, n_points, n):
+    """pbf_msm_g1_bn254_fixed_dev (window table 2^(16w) P_i, one bucket set) == the oracle's
+    naive fold of SRS::eval_at_s (plonk.rs:51-58) over the first n base points."""
+    rnd = random.Random(n_points * 7 + n)
+    pts = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(min(n_points, 64))]
+    pts = (pts * (n_points // len(pts) + 1))[:n_points]  # repeats: P + P in one bucket
+    sc = [rnd.randrange(R) for _ in range(n)]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    got = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n)
+    ref = bn254.msm_naive(pts[:n], sc) if n <= 300 else None
+    if ref is not None:
+        assert got == enc(ref)
+    assert got == ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n)  # the windowed Pippenger agrees
+
+
+def test_fixed_base_msm_edges_and_cache(ctx):
+    import torch
+
+    g = bn254.G1_GEN
+    neg = (g[0], Q - g[1])
+    pts = [g, neg, (0, 0), bn254.g1_mul(g, 2), g]
+    sc = [5, 5, 9, 0, R - 1]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    ref = bn254.msm_naive([None if p == (0, 0) else p for p in pts], sc)
+    assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), ds.data_ptr(), len(pts)) == enc(ref)
+    # the cached table is rebuilt when the points at the same address change
+    pts2 = [bn254.g1_mul(g, 3 + i) for i in range(len(pts))]
+    dp.copy_(_dev_points(pts2))
+    torch.cuda.synchronize()
+    assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), ds.data_ptr(), len(pts)) == enc(bn254.msm_naive(pts2, sc))
+    # all-zero scalars: the identity
+    dz = _dev_scalars([0] * len(pts))
+    assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), dz.data_ptr(), len(pts)) == (0, 0)
+
+
+def test_fixed_base_msm_2p20_discrete_log(ctx):
+    """Config-4 size through the fixed-base path: P_i = t_i G, result (sum s_i t_i) G."""
+    import torch
+
+    m = 1 << 20
+    rng = np.random.default_rng(44)
+    t = bn254.random_limbs(m, 45)
+    s = bn254.random_limbs(m, 46)
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    dsc = torch.from_numpy(s.view(np.int64)).cuda()
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(dt.data_ptr(), pts.data_ptr(), m)
+    got = ctx.msm_g1_fixed_dev(pts.data_ptr(), m, dsc.data_ptr(), m)
+    tv, sv = bn254.limbs_to_ints(t), bn254.limbs_to_ints(s)
+    k = sum(a * b for a, b in zip(tv, sv)) % R
+    assert got == enc(bn254.g1_mul(bn254.G1_GEN, k))
+    del rng
