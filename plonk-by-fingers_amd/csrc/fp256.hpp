@@ -56,6 +56,144 @@ struct Fp256 {
     }
     return r;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Device add / sub / reduce_once as explicit 32-bit carry chains: one chain carries through
+  // an SGPR pair (VOP3), the other through VCC, p's limbs in VGPRs (an instruction with a
+  // carry-in may read no other SGPR or literal on gfx950: one constant-bus read). Written in C++ the compiler rebuilds every limb's
+  // carry from 64-bit adds and moves (~70 instructions, ~340 cycles for one add on a lone
+  // wave); these are 24 VALU. A VALU carry write read by a VALU needs 2 wait states on gfx950:
+  // the two chains are interleaved so each carry has one independent instruction and one
+  // s_nop behind it (the compiler does not see inside the asm, so the pads are explicit).
+  __device__ __forceinline__ static U256 add(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    // s = a + b (< 2p < 2^256: no carry out), t = s - p; s where that borrowed (VCC), else t
+    U256 s = a, t;
+    uint64_t m;
+    asm(
+        "v_add_co_u32_e64 %0, %16, %0, %17\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32_e64 %1, %16, %1, %18, %16\n\t"
+        "v_subrev_co_u32_e32 %8, vcc, %25, %0\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %2, %16, %2, %19, %16\n\t"
+        "v_subbrev_co_u32_e32 %9, vcc, %26, %1, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %3, %16, %3, %20, %16\n\t"
+        "v_subbrev_co_u32_e32 %10, vcc, %27, %2, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %4, %16, %4, %21, %16\n\t"
+        "v_subbrev_co_u32_e32 %11, vcc, %28, %3, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %5, %16, %5, %22, %16\n\t"
+        "v_subbrev_co_u32_e32 %12, vcc, %29, %4, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %6, %16, %6, %23, %16\n\t"
+        "v_subbrev_co_u32_e32 %13, vcc, %30, %5, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %7, %16, %7, %24, %16\n\t"
+        "v_subbrev_co_u32_e32 %14, vcc, %31, %6, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %15, vcc, %32, %7, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e32 %0, %8, %0, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %9, %1, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %10, %2, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %11, %3, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %12, %4, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %13, %5, vcc\n\t"
+        "v_cndmask_b32_e32 %6, %14, %6, vcc\n\t"
+        "v_cndmask_b32_e32 %7, %15, %7, vcc"
+        : "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]), "+v"(s.w[3]), "+v"(s.w[4]), "+v"(s.w[5]), "+v"(s.w[6]),
+          "+v"(s.w[7]), "=&v"(t.w[0]), "=&v"(t.w[1]), "=&v"(t.w[2]), "=&v"(t.w[3]), "=&v"(t.w[4]),
+          "=&v"(t.w[5]), "=&v"(t.w[6]), "=&v"(t.w[7]), "=&s"(m)
+        : "v"(b.w[0]), "v"(b.w[1]), "v"(b.w[2]), "v"(b.w[3]), "v"(b.w[4]), "v"(b.w[5]), "v"(b.w[6]),
+          "v"(b.w[7]), "v"(Prm::P[0]), "v"(Prm::P[1]), "v"(Prm::P[2]), "v"(Prm::P[3]), "v"(Prm::P[4]),
+          "v"(Prm::P[5]), "v"(Prm::P[6]), "v"(Prm::P[7])
+        : "vcc");
+    return s;
+  }
+  __device__ __forceinline__ static U256 sub(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
+    // s = a - b (mod 2^256), t = s + p; t where the subtraction borrowed (m), else s
+    U256 s = a, t;
+    uint64_t m;
+    asm(
+        "v_sub_co_u32_e64 %0, %16, %0, %17\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32_e64 %1, %16, %1, %18, %16\n\t"
+        "v_add_co_u32_e32 %8, vcc, %25, %0\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %2, %16, %2, %19, %16\n\t"
+        "v_addc_co_u32_e32 %9, vcc, %26, %1, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %3, %16, %3, %20, %16\n\t"
+        "v_addc_co_u32_e32 %10, vcc, %27, %2, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %4, %16, %4, %21, %16\n\t"
+        "v_addc_co_u32_e32 %11, vcc, %28, %3, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %5, %16, %5, %22, %16\n\t"
+        "v_addc_co_u32_e32 %12, vcc, %29, %4, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %6, %16, %6, %23, %16\n\t"
+        "v_addc_co_u32_e32 %13, vcc, %30, %5, vcc\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %7, %16, %7, %24, %16\n\t"
+        "v_addc_co_u32_e32 %14, vcc, %31, %6, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_addc_co_u32_e32 %15, vcc, %32, %7, vcc\n\t"
+        "v_cndmask_b32_e64 %0, %0, %8, %16\n\t"
+        "v_cndmask_b32_e64 %1, %1, %9, %16\n\t"
+        "v_cndmask_b32_e64 %2, %2, %10, %16\n\t"
+        "v_cndmask_b32_e64 %3, %3, %11, %16\n\t"
+        "v_cndmask_b32_e64 %4, %4, %12, %16\n\t"
+        "v_cndmask_b32_e64 %5, %5, %13, %16\n\t"
+        "v_cndmask_b32_e64 %6, %6, %14, %16\n\t"
+        "v_cndmask_b32_e64 %7, %7, %15, %16"
+        : "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]), "+v"(s.w[3]), "+v"(s.w[4]), "+v"(s.w[5]), "+v"(s.w[6]),
+          "+v"(s.w[7]), "=&v"(t.w[0]), "=&v"(t.w[1]), "=&v"(t.w[2]), "=&v"(t.w[3]), "=&v"(t.w[4]),
+          "=&v"(t.w[5]), "=&v"(t.w[6]), "=&v"(t.w[7]), "=&s"(m)
+        : "v"(b.w[0]), "v"(b.w[1]), "v"(b.w[2]), "v"(b.w[3]), "v"(b.w[4]), "v"(b.w[5]), "v"(b.w[6]),
+          "v"(b.w[7]), "v"(Prm::P[0]), "v"(Prm::P[1]), "v"(Prm::P[2]), "v"(Prm::P[3]), "v"(Prm::P[4]),
+          "v"(Prm::P[5]), "v"(Prm::P[6]), "v"(Prm::P[7])
+        : "vcc");
+    return s;
+  }
+  __device__ __forceinline__ static U256 reduce_once(const U256& a) {
+    // a - p unless that borrows (a < 2p)
+    U256 d;
+    asm(
+        "v_subrev_co_u32_e32 %0, vcc, %16, %8\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %1, vcc, %17, %9, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %2, vcc, %18, %10, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %3, vcc, %19, %11, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %4, vcc, %20, %12, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %5, vcc, %21, %13, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %6, vcc, %22, %14, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_subbrev_co_u32_e32 %7, vcc, %23, %15, vcc\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e32 %0, %0, %8, vcc\n\t"
+        "v_cndmask_b32_e32 %1, %1, %9, vcc\n\t"
+        "v_cndmask_b32_e32 %2, %2, %10, vcc\n\t"
+        "v_cndmask_b32_e32 %3, %3, %11, vcc\n\t"
+        "v_cndmask_b32_e32 %4, %4, %12, vcc\n\t"
+        "v_cndmask_b32_e32 %5, %5, %13, vcc\n\t"
+        "v_cndmask_b32_e32 %6, %6, %14, vcc\n\t"
+        "v_cndmask_b32_e32 %7, %7, %15, vcc"
+        : "=&v"(d.w[0]), "=&v"(d.w[1]), "=&v"(d.w[2]), "=&v"(d.w[3]), "=&v"(d.w[4]), "=&v"(d.w[5]),
+          "=&v"(d.w[6]), "=&v"(d.w[7])
+        : "v"(a.w[0]), "v"(a.w[1]), "v"(a.w[2]), "v"(a.w[3]), "v"(a.w[4]), "v"(a.w[5]), "v"(a.w[6]),
+          "v"(a.w[7]), "v"(Prm::P[0]), "v"(Prm::P[1]), "v"(Prm::P[2]), "v"(Prm::P[3]), "v"(Prm::P[4]),
+          "v"(Prm::P[5]), "v"(Prm::P[6]), "v"(Prm::P[7])
+        : "vcc");
+    return d;
+  }
+#else
   __host__ __device__ __forceinline__ static U256 add(const U256& a, const U256& b, const FieldArgs& = FieldArgs{}) {
     U256 s;
     uint64_t c = 0;
@@ -103,6 +241,7 @@ struct Fp256 {
     for (int i = 0; i < 8; ++i) r.w[i] = borrow ? a.w[i] : d.w[i];
     return r;
   }
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   // Accumulators are 96-bit: c0 (64) + c1 (32) * 2^64. v_mad_u64_u32 returns the carry out
   // of its 64-bit sum in an SGPR pair, which a v_addc folds into c1. On gfx950 a VALU SGPR

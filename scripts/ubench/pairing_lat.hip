@@ -1,0 +1,108 @@
+// Latency microbenchmark of the pairing kernels' building blocks on one wave (gfx950):
+// cycles per dependent Fq product, Fq2 product, wave-cooperative Fq12 product and Miller
+// doubling step. Build: make -C scripts/ubench; run on the GPU box: scripts/ubench/pairing_lat
+#include "../../plonk-by-fingers_amd/csrc/pairing.hip"
+#include <cstdio>
+
+using namespace pbf;
+
+__global__ void __launch_bounds__(64) k_lat(int what, int iters, const uint64_t* seed, uint64_t* out, PairingConsts k) {
+  __shared__ PairLds L;
+  const int lane = threadIdx.x;
+  load_consts(k, L, lane);
+  U256 x = Fq::to_mont(u256_from_u64(seed)), y = Fq::to_mont(u256_from_u64(seed + 4));
+  Fq2 a{x, y}, b{y, x};
+  if (lane < 6) {
+    L.reg[0][lane] = Fq2{x, y};
+    L.reg[1][lane] = Fq2{y, x};
+  }
+  if (lane < 32) L.sl[lane] = Fq2{x, y};
+  __syncthreads();
+  uint64_t t0 = clock64(), w0 = wall_clock64();
+  switch (what) {
+    case 0: for (int i = 0; i < iters; ++i) x = Fq::mul(x, y); break;
+    case 1: for (int i = 0; i < iters; ++i) a = f2_mul(a, b); break;
+    case 2: for (int i = 0; i < iters; ++i) w12_mul(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
+    case 3: for (int i = 0; i < iters; ++i) run_uops(c_dbl_prog, DBL_LEN, L.reg[0], L, lane); break;
+    case 4: for (int i = 0; i < iters; ++i) run_uops(c_add_prog, ADD_LEN, L.reg[0], L, lane); break;
+    case 5: for (int i = 0; i < iters; ++i) x = Fq::add(x, y); break;
+    case 6: {  // one dependent v_mad_u64_u32 chain
+      uint64_t acc = x.w[0];
+      for (int i = 0; i < iters; ++i) acc = (uint64_t)(uint32_t)acc * y.w[1] + (acc >> 7);
+      x.w[0] = (uint32_t)acc;
+      break;
+    }
+    case 7: {  // four independent chains
+      uint64_t a0 = x.w[0], a1 = x.w[1], a2 = x.w[2], a3 = x.w[3];
+      for (int i = 0; i < iters; i += 4) {
+        a0 = (uint64_t)(uint32_t)a0 * y.w[1] + (a0 >> 7);
+        a1 = (uint64_t)(uint32_t)a1 * y.w[2] + (a1 >> 7);
+        a2 = (uint64_t)(uint32_t)a2 * y.w[3] + (a2 >> 7);
+        a3 = (uint64_t)(uint32_t)a3 * y.w[4] + (a3 >> 7);
+      }
+      x.w[0] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3);
+      break;
+    }
+    default: {  // one dependent 32-bit add-with-carry chain
+      uint32_t c = x.w[0];
+      for (int i = 0; i < iters; ++i) c = c * 3u + y.w[1];
+      x.w[0] = c;
+      break;
+    }
+  }
+  uint64_t t1 = clock64(), w1 = wall_clock64();
+  if (lane == 0) {
+    out[0] = t1 - t0;
+    out[1] = w1 - w0;
+    out[2] = x.w[0] ^ a.c0.w[0] ^ L.reg[0][0].c0.w[0];
+  }
+}
+
+// throughput: every lane of a full grid runs two independent chains of Fq products
+__global__ void __launch_bounds__(256) k_tput(int iters, const uint64_t* seed, uint64_t* out) {
+  U256 x = u256_from_u64(seed), y = u256_from_u64(seed + 4), z = x;
+  x.w[0] ^= threadIdx.x;
+  z.w[1] ^= blockIdx.x;
+  for (int i = 0; i < iters; ++i) {
+    x = Fq::mul(x, y);
+    z = Fq::mul(z, y);
+  }
+  if ((x.w[0] ^ z.w[0]) == 0x12345u) out[3] = 1;  // keeps the chains live
+}
+
+int main() {
+  uint64_t *d_seed, *d_out, h[3];
+  uint64_t seed[8] = {0x1234567, 0x89abcdef, 0x5555, 0x1000, 0x7777, 0x3333, 0x2222, 0x100};
+  hipMalloc(&d_seed, 64);
+  hipMalloc(&d_out, 64);
+  hipMemcpy(d_seed, seed, 64, hipMemcpyHostToDevice);
+  int wclk = 0;
+  hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);  // kHz
+  const char* names[] = {"fq_mul", "fq2_mul", "fq12_mul(wave)", "miller_dbl_step", "miller_add_step", "fq_add", "mad_u64_dep", "mad_u64_x4", "mul_add_u32_dep"};
+  const int iters[] = {4096, 2048, 256, 64, 64, 4096, 65536, 65536, 65536};
+  for (int w = 0; w < 9; ++w) {
+    for (int rep = 0; rep < 2; ++rep) {  // first launch warms the code
+      hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, w, iters[w], d_seed, d_out, make_consts());
+      hipMemcpy(h, d_out, 24, hipMemcpyDeviceToHost);
+    }
+    printf("%-18s %10.1f cycles  %8.3f us   per op\n", names[w], (double)h[0] / iters[w],
+           (double)h[1] / iters[w] * 1e3 / wclk);
+  }
+  {
+    const int blocks = 256 * 8, iters = 256;  // 8 workgroups (32 waves) per CU
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int rep = 0; rep < 3; ++rep) {
+      hipEventRecord(e0, 0);
+      hipLaunchKernelGGL(k_tput, dim3(blocks), dim3(256), 0, 0, iters, d_seed, d_out);
+      hipEventRecord(e1, 0);
+      hipEventSynchronize(e1);
+      float ms = 0;
+      hipEventElapsedTime(&ms, e0, e1);
+      const double muls = 2.0 * iters * blocks * 256;
+      printf("fq_mul throughput   %.3f ms  %.3e Fq products/s\n", ms, muls / (ms * 1e-3));
+    }
+  }
+  return 0;
+}
