@@ -160,5 +160,7 @@ struct pbf_ctx {
     if (!b) b.reset(new pbf::DevBuf());
     return *b;
   }
+  // pairing check: the G2 inputs whose prepared lines sit in buf("pc.lines") (pairing.hip)
+  std::vector<uint64_t> pair_g2_key;
   pbf::MsmTail msm_tail;  // destroyed before `named`: its stream drains first
 };

@@ -6,8 +6,41 @@
 
 using namespace pbf;
 
-__global__ void __launch_bounds__(64) k_lat(int what, int iters, const uint64_t* seed, uint64_t* out, PairingConsts k) {
-  __shared__ PairLds L;
+// the three rounds of w_mul<false> separately
+__device__ __forceinline__ void r1(const Fq2* x, const Fq2* y, PL& L, int tid) {
+  if (tid < 108) {
+    const int q = tid / 3, r = tid - 3 * q, i = q / 6, jj = q - 6 * i;
+    L.t[tid] = Fq::mul(kara_operand(x[i], r), kara_operand(y[jj], r));
+  }
+  bsync();
+}
+__device__ __forceinline__ void r2(PL& L, int tid) {
+  if (tid < 36) {
+    const int i = tid / 6, j = tid - 6 * i;
+    Fq2 p = kara_combine(L.t[3 * tid], L.t[3 * tid + 1], L.t[3 * tid + 2]);
+    if (i + j >= 6) p = f2_mul_xi(p);
+    L.pp[tid] = p;
+  }
+  bsync();
+}
+__device__ __forceinline__ void r3(Fq2* dst, PL& L, int tid) {
+  if (tid < 12) {
+    const int k = tid >> 1, c = tid & 1;
+    U256 s[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int i = k - j < 0 ? k - j + 6 : k - j;
+      const Fq2& p = L.pp[i * 6 + j];
+      s[j] = c ? p.c1 : p.c0;
+    }
+    const U256 v = Fq::add(Fq::add(Fq::add(s[0], s[1]), Fq::add(s[2], s[3])), Fq::add(s[4], s[5]));
+    if (c) dst[k].c1 = v; else dst[k].c0 = v;
+  }
+  bsync();
+}
+
+__global__ void __launch_bounds__(PT) k_lat(int what, int iters, const uint64_t* seed, uint64_t* out, PairingConsts k) {
+  __shared__ PL L;
   const int lane = threadIdx.x;
   load_consts(k, L, lane);
   U256 x = Fq::to_mont(u256_from_u64(seed)), y = Fq::to_mont(u256_from_u64(seed + 4));
@@ -22,10 +55,15 @@ __global__ void __launch_bounds__(64) k_lat(int what, int iters, const uint64_t*
   switch (what) {
     case 0: for (int i = 0; i < iters; ++i) x = Fq::mul(x, y); break;
     case 1: for (int i = 0; i < iters; ++i) a = f2_mul(a, b); break;
-    case 2: for (int i = 0; i < iters; ++i) w12_mul(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
-    case 3: for (int i = 0; i < iters; ++i) run_uops(c_dbl_prog, DBL_LEN, L.reg[0], L, lane); break;
-    case 4: for (int i = 0; i < iters; ++i) run_uops(c_add_prog, ADD_LEN, L.reg[0], L, lane); break;
+    case 2: for (int i = 0; i < iters; ++i) w_mul<false>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
+    case 3: for (int i = 0; i < iters; ++i) w_csqr(L.reg[0], L.reg[0], L, lane); break;
+    case 4: for (int i = 0; i < iters; ++i) w_mul<true>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
     case 5: for (int i = 0; i < iters; ++i) x = Fq::add(x, y); break;
+    case 9: for (int i = 0; i < iters; ++i) r1(L.reg[0], L.reg[1], L, lane); break;
+    case 10: for (int i = 0; i < iters; ++i) r2(L, lane); break;
+    case 11: for (int i = 0; i < iters; ++i) r3(L.reg[0], L, lane); break;
+    case 12: for (int i = 0; i < iters; ++i) bsync(); break;
+    case 13: for (int i = 0; i < iters; ++i) { if (lane < 64) x = Fq::mul(x, y); bsync(); } break;
     case 6: {  // one dependent v_mad_u64_u32 chain
       uint64_t acc = x.w[0];
       for (int i = 0; i < iters; ++i) acc = (uint64_t)(uint32_t)acc * y.w[1] + (acc >> 7);
@@ -78,11 +116,11 @@ int main() {
   hipMemcpy(d_seed, seed, 64, hipMemcpyHostToDevice);
   int wclk = 0;
   hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);  // kHz
-  const char* names[] = {"fq_mul", "fq2_mul", "fq12_mul(wave)", "miller_dbl_step", "miller_add_step", "fq_add", "mad_u64_dep", "mad_u64_x4", "mul_add_u32_dep"};
-  const int iters[] = {4096, 2048, 256, 64, 64, 4096, 65536, 65536, 65536};
-  for (int w = 0; w < 9; ++w) {
+  const char* names[] = {"fq_mul", "fq2_mul", "fq12_mul(lanes)", "fq12_cyc_sqr", "fq12_mul_line", "fq_add", "mad_u64_dep", "mad_u64_x4", "mul_add_u32_dep", "w_mul round1", "w_mul round2", "w_mul round3", "barrier", "fq_mul+barrier"};
+  const int iters[] = {4096, 2048, 256, 256, 256, 4096, 65536, 65536, 65536, 256, 256, 256, 4096, 1024};
+  for (int w = 0; w < 14; ++w) {
     for (int rep = 0; rep < 2; ++rep) {  // first launch warms the code
-      hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, w, iters[w], d_seed, d_out, make_consts());
+      hipLaunchKernelGGL(k_lat, dim3(1), dim3(PT), 0, 0, w, iters[w], d_seed, d_out, make_consts());
       hipMemcpy(h, d_out, 24, hipMemcpyDeviceToHost);
     }
     printf("%-18s %10.1f cycles  %8.3f us   per op\n", names[w], (double)h[0] / iters[w],
