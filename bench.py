@@ -29,6 +29,7 @@ import pbf  # noqa: E402
 
 GOLD = pbf.GOLDILOCKS
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FQ_MUL_PEAK = 1.0e11  # BN254 Fq Montgomery products/s, all CUs (scripts/ubench/pairing_lat.hip k_tput)
 
 
 def root_of_unity(n: int) -> int:
@@ -74,6 +75,50 @@ def cpu_baseline(log_n: int, budget_s: float) -> dict:
                                     f"(iterative radix-2, one polynomial per thread), {el2:.1f} s"}}
 
 
+def live_traffic(log_n: int, batch: int, steps: int = 6) -> dict | None:
+    """HBM bytes per step of the NTT bench workload, measured now: two rocprofv3 PMC passes
+    (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots")
+    over a child bench.py that runs only the NTT steps. Counters are KiB; the NTT kernels load
+    8 B per lane in 64-B runs, which FETCH_SIZE counts exactly on gfx950 (calibrated against
+    scripts/ubench/tile_copy moving a known byte count in the same pattern), so
+    no 2x wide-load correction applies. None if rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+
+    if not shutil.which("rocprofv3"):
+        return None
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="pbf_traffic_", dir="/tmp")
+    child = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", "0", "--no-cpu",
+             "--no-extra", "--no-traffic", "--log-n", str(log_n), "--batch", str(batch)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", tmp, "-o", counter.lower(), "--"] + child
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                             start_new_session=True)
+        try:
+            rc = p.wait(timeout=150)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None
+        path = os.path.join(tmp, counter.lower() + "_counter_collection.csv")
+        if rc != 0 or not os.path.exists(path):
+            return None
+        total = 0.0
+        for r in csv.DictReader(open(path)):
+            if "ntt_" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                total += float(r["Counter_Value"])
+        out[counter] = total * 1024.0 / steps  # bytes per step (the child runs `steps` steps, no warm-up)
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"hbm_bytes_per_step": out["FETCH_SIZE"] + out["WRITE_SIZE"], "fetch_bytes_per_step": out["FETCH_SIZE"],
+            "write_bytes_per_step": out["WRITE_SIZE"], "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+            "separate passes over this bench's NTT steps, run by bench.py"}
+
+
 def load_traffic(log_n: int, batch: int):
     """HBM bytes per NTT from the committed PMC pass (profiles/pmc_ntt_2p{log_n}.json), if any."""
     p = os.path.join(ROOT, "profiles", f"pmc_ntt_2p{log_n}_b{batch}.json")
@@ -93,6 +138,7 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the config 1/3/4 side measurements")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
     ap.add_argument("--prove-log-n", type=str, default="20,24",
                     help="N > 1: gate counts (log2, comma-separated) of the sharded config-5 prove")
     args = ap.parse_args()
@@ -193,6 +239,20 @@ def main() -> int:
             out["extra"].update(other_configs(ctx, sp))
         if world > 1 and sharded_prove is not None:
             out["extra"] = {"config5_prove_sharded": sharded_prove}
+        if world == 1 and not args.no_traffic:
+            tr = live_traffic(args.log_n, B)
+            if tr:
+                out["roofline"]["traffic"] = tr["hbm_bytes_per_step"]
+                out["roofline"]["traffic_detail"] = dict(tr, algorithmic_bytes_per_step=alg_bytes_step)
+            if "extra" in out and "ntt_2p24" in out["extra"]:
+                tr24 = live_traffic(24, 2)
+                if tr24:
+                    r24 = out["extra"]["ntt_2p24"]["roofline"]
+                    r24["traffic"] = tr24["hbm_bytes_per_step"]
+                    r24["traffic_detail"] = dict(tr24, algorithmic_bytes_per_step=16.0 * (1 << 24) * 2,
+                                                 calibration="FETCH_SIZE calibrated for 64-B runs (2^20 plan); "
+                                                             "the 2^24 plan reads 128-B runs, which may be "
+                                                             "tallied at half (MI355X_MICROARCH.md, HBM)")
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
         print(json.dumps(out), flush=True)
@@ -327,8 +387,29 @@ def other_configs(ctx, sp) -> dict:
     ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m, stream=sp)
     torch.cuda.synchronize()
     t = _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp))
-    res["config4_bn254_msm_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3),
-                                         note="Pippenger c=16 (bucket accumulation, window sums, combine)")
+    # compute roofline of the MSM: 16 m mixed XYZZ additions of 10 Fq products each (the
+    # accumulation; the bucket reduction adds < 1 %) against the measured Fq-product
+    # throughput of the chip (scripts/ubench/pairing_lat.hip k_tput: every lane of a full grid
+    # running independent Fq products, 9.7-10.2e10/s on MI355X)
+    fq_products = 16 * m * 10
+
+    def msm_roof(ms):
+        ach = fq_products / (ms / 1e3)
+        return {"bound": "valu (Fq products)", "achieved": ach, "peak": FQ_MUL_PEAK, "unit": "Fq products/s",
+                "frac": ach / FQ_MUL_PEAK, "fq_products": fq_products,
+                "peak_source": "scripts/ubench/pairing_lat.hip k_tput (measured)"}
+
+    res["config4_bn254_msm_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3), roofline=msm_roof(t["ms"]),
+                                         note="Pippenger c=16, 16 windows (bucket accumulation, window sums, "
+                                              "host Horner); points converted every call")
+    # the same MSM against a fixed base set (KZG commit: SRS window table built on first use,
+    # one bucket set, join and reduction on a side stream; the result copied back each call)
+    ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp)  # builds the table
+    torch.cuda.synchronize()
+    t = _median_ms(lambda: ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp))
+    res["config4_kzg_commit_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3), roofline=msm_roof(t["ms"]),
+                                          note="fixed-base window table (16 x 2^20 affine points, 1 GiB, built "
+                                               "once per base set), fingerprint check per call")
     # config 4 (cont.): BN254 pairing check (2 Miller loops + 1 final exponentiation, the
     # KZG check of plonk.rs:646-650) and batched pairing throughput (one wave per pairing)
     G1G = (1, 2)
@@ -338,9 +419,16 @@ def other_configs(ctx, sp) -> dict:
             4082367875863433681332203403145435568316851327593401208105741076214120093531))
     negG1 = (1, pbf.BN254_Q - 2)
     oks = []
+    ctx2 = pbf.Context(ctx.device)  # a fresh context: its first check also builds the G2 lines
+    t0 = time.perf_counter()
+    oks.append(ctx2.pairing_check_bn254([G1G, negG1], [G2G, G2G]))
+    first_ms = (time.perf_counter() - t0) * 1e3
+    ctx2.close()
     t = _median_ms(lambda: oks.append(ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])))  # e(G,H) e(-G,H) = 1
-    res["config4_pairing_check"] = dict(t, ok=all(oks),
-                                        note="host round trip incl. copies; 2 pairs, one final exponentiation")
+    res["config4_pairing_check"] = dict(t, ok=all(oks), first_call_ms=first_ms,
+                                        note="host round trip incl. copies; 2 pairs, one multi-Miller loop and "
+                                             "one final exponentiation; prepared G2 lines reused after the first "
+                                             "call (first_call_ms: fresh context, lines built)")
     npair = 4096
     g1 = pbf.ints_to_limbs([c for _ in range(npair) for c in G1G])
     g2 = pbf.ints_to_limbs([c for _ in range(npair) for c in (G2G[0][0], G2G[0][1], G2G[1][0], G2G[1][1])])

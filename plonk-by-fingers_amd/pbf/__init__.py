@@ -145,6 +145,7 @@ class Context:
         _check(lib.pbf_ctx_create(device, ctypes.byref(h)))
         self.h = h
         self.lib = lib
+        self.device = device
 
     def close(self) -> None:
         if self.h:
