@@ -121,7 +121,7 @@ struct G1 {
     return r;
   }
   // k * p for a small non-negative k (double-and-add, MSB first)
-  __host__ __device__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
+  __host__ __device__ __forceinline__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
     Xyzz r = identity();
     int top = 31;
     while (top >= 0 && !((k >> top) & 1)) --top;  // from the leading one

@@ -56,7 +56,7 @@ struct Fp256 {
     }
     return r;
   }
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(PBF_NO_ASM_ADD)
   // Device add / sub / reduce_once as explicit 32-bit carry chains: one chain carries through
   // an SGPR pair (VOP3), the other through VCC, p's limbs in VGPRs (an instruction with a
   // carry-in may read no other SGPR or literal on gfx950: one constant-bus read). Written in C++ the compiler rebuilds every limb's

@@ -145,6 +145,7 @@ struct pbf_ctx {
     const void* ptr = nullptr;
     uint64_t n = 0, fingerprint = 0;
     pbf::DevBuf table;
+    pbf::DevBuf inf;  // per point: 1 = the identity (contributes nothing)
   } fixed_base;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::unique_ptr<pbf::TwoLevel>> two_level;
   int roots(uint64_t m, uint64_t root, uint64_t n, pbf::TwoLevel** out);

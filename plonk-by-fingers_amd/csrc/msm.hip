@@ -113,15 +113,19 @@ struct ChunkPart {
 // this chunk and ends in a later one. Buckets with no entry stay zero (ZZ = 0: identity).
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE))) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
                                                      const uint32_t* start, const uint32_t* end, uint32_t m,
-                                                     Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent) {
+                                                     Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent,
+                                                     const uint32_t* m_dev) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c0 = t * MSM_CH;
-  if (c0 >= m) return;
-  const uint32_t c1 = c0 + MSM_CH < m ? c0 + MSM_CH : m;
-  uint32_t cur = keys[c0], rs = c0;
-  Xyzz acc = G1::identity();
+  if (c0 >= m) return;  // past the chunks of the m-entry list
   head[t].key = sent;
   tail[t].key = sent;
+  // m_dev: the valid length, known on the device only (counting sort: no sentinel entries)
+  const uint32_t mv = m_dev ? *m_dev : m;
+  if (c0 >= mv) return;
+  const uint32_t c1 = c0 + MSM_CH < mv ? c0 + MSM_CH : mv;
+  uint32_t cur = keys[c0], rs = c0;
+  Xyzz acc = G1::identity();
   if (cur == sent) return;  // past the valid prefix (zero digits sort last)
   auto flush = [&](uint32_t re) {
     const uint32_t bs = start[cur], be = end[cur];
@@ -191,12 +195,14 @@ __device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
 constexpr uint32_t MSM_SEG = PBF_MSM_SEG;
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
 
+template <uint32_t NB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_SEG_WPE))) msm_segments(const Xyzz* buckets, Xyzz* shares, uint32_t nw) {
+  constexpr uint32_t NSEG = NB / MSM_SEG;
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= nw * MSM_NSEG) return;
-  const uint32_t w = id / MSM_NSEG, seg = id % MSM_NSEG;
+  if (id >= nw * NSEG) return;
+  const uint32_t w = id / NSEG, seg = id % NSEG;
   const uint32_t a = seg * MSM_SEG;
-  const Xyzz* B = buckets + (uint64_t)w * MSM_NB;
+  const Xyzz* B = buckets + (uint64_t)w * NB;
   Xyzz running = G1::identity(), wsum = G1::identity();
   for (int k = (int)(a + MSM_SEG - 1); k >= (int)a; --k) {
     running = G1::add(running, B[k]);
@@ -224,20 +230,29 @@ static_assert(MSM_NSEG % MSM_SEG_THREADS == 0 && MSM_NPART <= MSM_SEG_THREADS, "
 __global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz* shares, Xyzz* parts) {
   msm_tree_sum(shares + (uint64_t)blockIdx.x * MSM_SEG_THREADS, MSM_SEG_THREADS, parts + blockIdx.x);
 }
-// workgroup w: the window sum from its MSM_NPART partial sums
-__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* parts, Xyzz* sums) {
-  msm_tree_sum(parts + (uint64_t)blockIdx.x * MSM_NPART, MSM_NPART, sums + blockIdx.x);
+// workgroup w: the window sum from its npart (<= MSM_SEG_THREADS) partial sums
+__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* parts, Xyzz* sums, uint32_t npart) {
+  msm_tree_sum(parts + (uint64_t)blockIdx.x * npart, npart, sums + blockIdx.x);
 }
 
 // ---------------------------------------------------------------- fixed-base MSM
 // KZG commitments are MSMs against the fixed SRS (plonk.rs:51-58), so the SRS points can be
-// precomputed once per window: table[w][i] = 2^(16 w) P_i (affine, Montgomery). Every
-// (point, window) digit then goes to ONE set of 2^15 buckets (bucket |d| - 1 of entry
-// table[w][i], negated for d < 0): the same 16 n mixed additions as the windowed form, but
-// one bucket reduction instead of 16, no Horner over windows, 16-bit sort keys, and no
-// per-call conversion of the points. 16 n x 64 B of table (1 GiB per 2^20 points).
+// precomputed once per window: table[w][i] = 2^(FX_C w) P_i (affine, Montgomery). Every
+// (point, window) digit then goes to ONE set of buckets (bucket |d| - 1 of entry
+// table[w][i], negated for d < 0): one bucket reduction instead of one per window, no
+// Horner over windows, no per-call conversion of the points. The window stays at 16-bit
+// signed digits (16 windows, 2^15 buckets, the table 16 x n x 64 B = 1 GiB per 2^20
+// points). Measured alternatives (2^20-gate proof): 20-bit digits (13 windows: 13 n
+// instead of 16 n mixed additions, 2^19 buckets) 50.8 ms against 48.1 -- the accumulation
+// did not shrink in proportion and the 2^19-bucket reduction (0.84 ms segments, 0.40 ms
+// trees) steals the VALUs; a counting sort by global atomics instead of the radix sort
+// 58.3 ms -- count 0.52 + scatter 0.91 ms per MSM: device-scope atomics on MI355X resolve
+// beyond the per-XCD L2s (~26 G/s).
+constexpr int FX_C = 16, FX_NW = 16;
+constexpr uint32_t FX_NB = 1u << (FX_C - 1);  // buckets (|d| - 1, |d| <= 2^(FX_C-1))
+static_assert(FX_C * FX_NW >= 255, "windows must cover a 254-bit scalar plus the recoding carry");
 
-// table window w from window w-1: 16 doublings in XYZZ, then affine through a
+// table window w from window w-1: FX_C doublings in XYZZ, then affine through a
 // block-wide batch inversion of the ZZZ (prefix and suffix products in LDS, one Fermat
 // inversion per block); the identity (0, 0) stays (0, 0)
 __global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affine* next, uint64_t n) {
@@ -253,7 +268,7 @@ __global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affi
     id = Fq::is_zero(a.x) && Fq::is_zero(a.y);
     if (!id) {
       acc = G1::mdbl(a);
-      for (int k = 1; k < MSM_C; ++k) acc = G1::dbl(acc);
+      for (int k = 1; k < FX_C; ++k) acc = G1::dbl(acc);
     }
   }
   const U256 z = id ? one : acc.ZZZ;
@@ -288,27 +303,37 @@ __global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affi
   next[i] = r;
 }
 
-// one (key, value) per (point, window): key = |d| - 1 (MSM_NB: zero digit or identity point),
-// value = index of table[w][first + i] | sign
-__global__ void msm_fixed_digits(const uint64_t* scalars, const Affine* table, uint64_t n_table, uint64_t first,
-                                 uint32_t* keys, uint32_t* vals, uint64_t n) {
+// window w's signed digit of a scalar (FX_C bits; d > 2^(FX_C-1) -> d - 2^FX_C, carry 1 upward):
+// calls in window order carry through `carry`. Returns |d| (0: no entry), sets neg.
+__device__ __forceinline__ uint32_t fx_digit(const uint64_t* s, int w, uint32_t& carry, bool& neg) {
+  const int bit = FX_C * w, limb = bit >> 6, off = bit & 63;
+  uint64_t v = limb < 4 ? s[limb] >> off : 0;
+  if (off + FX_C > 64 && limb + 1 < 4) v |= s[limb + 1] << (64 - off);
+  uint32_t d = (uint32_t)(v & ((1u << FX_C) - 1)) + carry;
+  neg = false;
+  if (d > FX_NB) {
+    d = (1u << FX_C) - d;
+    neg = true;
+    carry = 1;
+  } else {
+    carry = 0;
+  }
+  return d;
+}
+
+// one (key, value) per (point, window): key = |d| - 1 (FX_NB: zero digit or identity
+// point, sorts last), value = index of table[w][first + i] | sign
+__global__ void __launch_bounds__(256) msm_fx_digits(const uint64_t* scalars, const uint8_t* inf, uint64_t n_table,
+                                                     uint64_t first, uint64_t n, uint32_t* keys, uint32_t* vals) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = scalars + 4 * i;
-    const Affine p = table[first + i];
-    const bool skip = Fq::is_zero(p.x) && Fq::is_zero(p.y);
+    const bool skip = inf[first + i] != 0;
     uint32_t carry = 0;
 #pragma unroll
-    for (int w = 0; w < MSM_NW; ++w) {
-      uint32_t d = (uint32_t)((s[w / 4] >> (16 * (w % 4))) & 0xFFFF) + carry;
-      bool neg = false;
-      if (d > MSM_NB) {
-        d = (1u << MSM_C) - d;
-        neg = true;
-        carry = 1;
-      } else {
-        carry = 0;
-      }
-      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? MSM_NB : (d - 1);
+    for (int w = 0; w < FX_NW; ++w) {
+      bool neg;
+      const uint32_t d = fx_digit(s, w, carry, neg);
+      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? FX_NB : d - 1;
       vals[(uint64_t)w * n + i] = (uint32_t)((uint64_t)w * n_table + first + i) | (neg ? MSM_NEG : 0u);
     }
   }
@@ -513,15 +538,15 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
                      (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
-                     (ChunkPart*)w.tail.p, MSM_SENTINEL);
+                     (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr);
   hipLaunchKernelGGL(msm_chunk_join, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const ChunkPart*)w.head.p,
                      (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p, MSM_SENTINEL);
-  hipLaunchKernelGGL(msm_segments, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
-                     (Xyzz*)w.shares.p, (uint32_t)MSM_NW);
+  hipLaunchKernelGGL(msm_segments<MSM_NB>, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s,
+                     (const Xyzz*)w.buckets.p, (Xyzz*)w.shares.p, (uint32_t)MSM_NW);
   hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW * MSM_NPART), dim3(MSM_SEG_THREADS), 0, s,
                      (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
   hipLaunchKernelGGL(msm_window_final, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.parts.p,
-                     (Xyzz*)w.sums.p);
+                     (Xyzz*)w.sums.p, MSM_NPART);
   PBF_HIP(hipGetLastError());
   return 0;
 }
@@ -557,9 +582,9 @@ static int msm_fingerprint_host(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n,
 }
 
 // the window table of the n points at d_pts (built on first use; rebuilt when the points at
-// that address changed)
+// that address changed); the table's identity flags are kept with it (fixed_base.inf)
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
-  if (n == 0 || n > 0x7FFFFFFFull / MSM_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
+  if (n == 0 || n > 0x7FFFFFFFull / FX_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
   uint64_t fp = 0;
   int rc = msm_fingerprint_host(ctx, d_pts, n, s, &fp);
   if (rc) return rc;
@@ -568,12 +593,10 @@ int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t
     *out = (const Affine*)fb.table.p;
     return 0;
   }
-  if ((rc = fb.table.ensure((uint64_t)MSM_NW * n * sizeof(Affine)))) return rc;
+  if ((rc = fb.table.ensure((uint64_t)FX_NW * n * sizeof(Affine))) || (rc = fb.inf.ensure(n))) return rc;
   Affine* tbl = (Affine*)fb.table.p;
-  DevBuf& inf = ctx->buf("msm.inf");
-  if ((rc = inf.ensure(n))) return rc;
-  hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, tbl, (uint8_t*)inf.p, n);
-  for (int w = 1; w < MSM_NW; ++w)
+  hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, tbl, (uint8_t*)fb.inf.p, n);
+  for (int w = 1; w < FX_NW; ++w)
     hipLaunchKernelGGL(msm_table_window, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                        (const Affine*)(tbl + (uint64_t)(w - 1) * n), tbl + (uint64_t)w * n, n);
   PBF_HIP(hipGetLastError());
@@ -610,15 +633,20 @@ int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s) {
   return 0;
 }
 
-// sum_i scalars[i] * P_(first + i), i < n, against a window table of n_table points; the
-// result (XYZZ, Montgomery) is written to *d_result on the device (nothing waits for it).
-// On `s`: digits, sort, bucket bounds, accumulation (throughput-bound, the whole chip).
-// On the context's side stream: the boundary join and the bucket reduction (latency-bound
-// chains of a few hundred waves), overlapping whatever the caller enqueues next on `s`.
+// sum_i scalars[i] * P_(first + i), i < n, against the context's window table of n_table
+// points; the result (XYZZ, Montgomery) is written to *d_result on the device (nothing waits
+// for it).
+// On `s`: digits, the sort by bucket, bucket bounds and the accumulation
+// (throughput-bound, the whole chip). On the context's side stream: the boundary join and
+// the bucket reduction (latency-bound chains of a few hundred waves), overlapping whatever
+// the caller enqueues next on `s`.
 int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64_t first, const uint64_t* d_sc,
                      uint64_t n, hipStream_t s, Xyzz* d_result) {
   if (first + n > n_table) return fail(PBF_EINVAL, "fixed-base MSM: range beyond the table");
-  const uint64_t m = n * MSM_NW;
+  auto& fb = ctx->fixed_base;
+  if ((const void*)table != fb.table.p || n_table != fb.n || !fb.inf.p)
+    return fail(PBF_EINVAL, "fixed-base MSM: not the context's table");
+  const uint64_t m = n * FX_NW;  // entries at most (zero digits are skipped)
   MsmTail& tl = ctx->msm_tail;
   int rc;
   if ((rc = tl.ensure())) return rc;
@@ -633,32 +661,37 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   if (tl.used[slot]) PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
   const uint64_t hbytes = (m / MSM_CH + 1) * sizeof(ChunkPart);
   if ((head.bytes < hbytes || tail.bytes < hbytes) && tl.used[slot]) PBF_HIP(hipEventSynchronize(tl.done[slot]));
+  constexpr uint32_t NSEG = FX_NB / MSM_SEG, NPART = NSEG / MSM_SEG_THREADS;
+  static_assert(NSEG % MSM_SEG_THREADS == 0 && NPART <= MSM_SEG_THREADS, "reduction shape");
   if ((rc = keys.ensure(m * 4)) || (rc = vals.ensure(m * 4)) || (rc = keys2.ensure(m * 4)) ||
-      (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)MSM_NB * 4)) ||
-      (rc = end.ensure((uint64_t)MSM_NB * 4)) || (rc = buckets.ensure((uint64_t)MSM_NB * sizeof(Xyzz))) ||
-      (rc = shares.ensure((uint64_t)MSM_NSEG * sizeof(Xyzz))) || (rc = parts.ensure(MSM_NPART * sizeof(Xyzz))) ||
-      (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) || (rc = spb.ensure(4)))
+      (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)FX_NB * 4)) || (rc = end.ensure((uint64_t)FX_NB * 4)) ||
+      (rc = buckets.ensure((uint64_t)FX_NB * sizeof(Xyzz))) || (rc = shares.ensure((uint64_t)NSEG * sizeof(Xyzz))) ||
+      (rc = parts.ensure(NPART * sizeof(Xyzz))) || (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) ||
+      (rc = spb.ensure(4)))
     return rc;
-  hipLaunchKernelGGL(msm_fixed_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, table, n_table, first,
-                     (uint32_t*)keys.p, (uint32_t*)vals.p, n);
+  const uint8_t* inf = (const uint8_t*)fb.inf.p;
+  // ---- digits, sort by bucket, bucket bounds
+  hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
+                     (uint32_t*)keys.p, (uint32_t*)vals.p);
   size_t temp_bytes = 0;
   PBF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
-                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, MSM_BB + 1, s));
+                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, FX_C, s));
   if ((rc = temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
   PBF_HIP(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
-                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, MSM_BB + 1, s));
-  PBF_HIP(hipMemsetAsync(start.p, 0, (uint64_t)MSM_NB * 4, s));
-  PBF_HIP(hipMemsetAsync(end.p, 0, (uint64_t)MSM_NB * 4, s));
+                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, FX_C, s));
+  PBF_HIP(hipMemsetAsync(start.p, 0, (uint64_t)FX_NB * 4, s));
+  PBF_HIP(hipMemsetAsync(end.p, 0, (uint64_t)FX_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
-                     (uint32_t*)start.p, (uint32_t*)end.p, MSM_NB);
-  PBF_HIP(hipMemsetAsync(buckets.p, 0, (uint64_t)MSM_NB * sizeof(Xyzz), s));
+                     (uint32_t*)start.p, (uint32_t*)end.p, FX_NB);
+  // ---- accumulation
+  PBF_HIP(hipMemsetAsync(buckets.p, 0, (uint64_t)FX_NB * sizeof(Xyzz), s));
   PBF_HIP(hipMemsetAsync(spb.p, 0, 4, s));
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
   hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
                      (const uint32_t*)vals2.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)m,
-                     (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p, MSM_NB);
-  hipLaunchKernelGGL(msm_max_span, dim3(MSM_NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
-                     (const uint32_t*)end.p, MSM_NB, (uint32_t*)spb.p);
+                     (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p, FX_NB, (const uint32_t*)nullptr);
+  hipLaunchKernelGGL(msm_max_span, dim3(FX_NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
+                     (const uint32_t*)end.p, FX_NB, (uint32_t*)spb.p);
   PBF_HIP(hipGetLastError());
   // ---- the tail, on the side stream
   hipStream_t a = tl.aux;
@@ -666,19 +699,19 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   PBF_HIP(hipStreamWaitEvent(a, tl.ready[slot], 0));
   // ceil(log2(nchunks)) steps bound any span; steps past the largest span exit at once. The
   // grid covers the mean span's pair slots (the kernel strides over the rest).
-  const uint64_t mean_span = m / ((uint64_t)MSM_NB * MSM_CH) + 2;
+  const uint64_t mean_span = m / ((uint64_t)FX_NB * MSM_CH) + 2;
   for (uint32_t step = 1; step < nchunks; step <<= 1) {
-    const uint64_t items = (uint64_t)MSM_NB * ((mean_span + 2 * step - 1) / (2 * step));
+    const uint64_t items = (uint64_t)FX_NB * ((mean_span + 2 * step - 1) / (2 * step));
     hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
-                       (const uint32_t*)start.p, (const uint32_t*)end.p, MSM_NB, step, (const uint32_t*)spb.p);
+                       (const uint32_t*)start.p, (const uint32_t*)end.p, FX_NB, step, (const uint32_t*)spb.p);
   }
   hipLaunchKernelGGL(msm_join_final, dim3((nchunks + 255) / 256), dim3(256), 0, a, (const ChunkPart*)head.p,
-                     (const ChunkPart*)tail.p, nchunks, (Xyzz*)buckets.p, MSM_NB);
-  hipLaunchKernelGGL(msm_segments, dim3((MSM_NSEG + 255) / 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
+                     (const ChunkPart*)tail.p, nchunks, (Xyzz*)buckets.p, FX_NB);
+  hipLaunchKernelGGL(msm_segments<FX_NB>, dim3((NSEG + 255) / 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
                      (Xyzz*)shares.p, 1u);
-  hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NPART), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)shares.p,
+  hipLaunchKernelGGL(msm_window_reduce, dim3(NPART), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)shares.p,
                      (Xyzz*)parts.p);
-  hipLaunchKernelGGL(msm_window_final, dim3(1), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)parts.p, d_result);
+  hipLaunchKernelGGL(msm_window_final, dim3(1), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)parts.p, d_result, NPART);
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipEventRecord(tl.done[slot], a));
   tl.used[slot] = true;

@@ -95,3 +95,53 @@ def test_non_canonical_coordinate_rejected(ctx):
 
     with pytest.raises(pbf.PbfError):
         ctx.pairing_bn254([(B.Q, 2)], [B.G2_GEN])
+
+
+def _balanced_pairs(ctx, rng, npairs):
+    """npairs (a_i G1, b_i G2) with sum a_i b_i = 0 mod r (product of pairings = 1)."""
+    a = [rng.randrange(1, B.R) for _ in range(npairs)]
+    b = [rng.randrange(1, B.R) for _ in range(npairs)]
+    a[-1] = -sum(x * y for x, y in zip(a[:-1], b[:-1])) * pow(b[-1], B.R - 2, B.R) % B.R
+    ps = [B.g1_mul(B.G1_GEN, x) for x in a]
+    qs = ctx.g2_bn254_mul([B.G2_GEN] * npairs, b)
+    return ps, qs
+
+
+@pytest.mark.parametrize("npairs", [2, 3, 5])
+def test_pairing_check_multi_pair(ctx, npairs):
+    """The multi-Miller check (pairs in chunks of two, an odd tail of one, the chunk
+    values multiplied before one final exponentiation) against the oracle's check."""
+    rng = random.Random(100 + npairs)
+    ps, qs = _balanced_pairs(ctx, rng, npairs)
+    assert ctx.pairing_check_bn254(ps, qs)
+    assert B.pairing_check(list(zip(ps, qs)))
+    bad = list(ps)
+    bad[npairs // 2] = B.g1_add(bad[npairs // 2], B.G1_GEN)
+    assert not ctx.pairing_check_bn254(bad, qs)
+    assert not B.pairing_check(list(zip(bad, qs)))
+
+
+def test_pairing_check_identity_pairs(ctx):
+    """Identity pairs contribute 1 anywhere in the product (either side)."""
+    rng = random.Random(7)
+    ps, qs = _balanced_pairs(ctx, rng, 3)
+    assert ctx.pairing_check_bn254([ps[0], None, ps[1], B.G1_GEN, ps[2]], [qs[0], qs[1], qs[1], None, qs[2]])
+    assert ctx.pairing_check_bn254([None], [B.G2_GEN])
+    assert not ctx.pairing_check_bn254([B.G1_GEN], [B.G2_GEN])
+
+
+def test_pairing_check_prepared_lines_cache(ctx):
+    """The context reuses prepared G2 lines only for the same G2 bytes: alternating G2
+    sets and a same-G2 / different-G1 call all give the oracle's answers."""
+    rng = random.Random(11)
+    p1, q1 = _balanced_pairs(ctx, rng, 2)
+    p2, q2 = _balanced_pairs(ctx, rng, 2)
+    assert ctx.pairing_check_bn254(p1, q1)
+    assert ctx.pairing_check_bn254(p2, q2)
+    assert ctx.pairing_check_bn254(p1, q1)
+    assert not ctx.pairing_check_bn254(p2, q1)  # same G2 as the cached set, other G1
+    assert not ctx.pairing_check_bn254(p1, [q1[0], q2[1]])
+
+
+def test_pairing_check_empty(ctx):
+    assert ctx.pairing_check_bn254([], [])
