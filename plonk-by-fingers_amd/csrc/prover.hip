@@ -367,19 +367,110 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out) {
   }
 }
 
-// out[i] = (P(x_i) - y) / (x_i - z) on the coset, inv_xz[i] = 1/(x_i - z) precomputed
-__global__ void k_coset_minus(uint64_t* out, uint64_t N, U256 g, U256 wN, U256 zpt, Blk blk) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = chunk_first(t);
-  if (i0 >= N) return;
-  U256 x = Fr::mul(g, fr_pow(wN, blk_index(blk, i0)));
-  const U256 step = pow64(wN);
-  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < N; ++k, x = blk_next_x(blk, i, x, step, g, wN), i += 64)
-    str(out + 4 * i, Fr::sub(x, zpt));
+// Synthetic division by (x - z), the quotients of the openings (plonk.rs:430-442):
+// q = (p - y) / (x - z) for p of L coefficients (y subtracted from p_0), q_(L-2-k) = s_k with
+//   s_k = p_(L-1-k) + z s_(k-1)   (Horner from the top coefficient, s_(-1) = 0)
+// and s_(L-1) = p(z) - y, the remainder, which must be zero (the reference's `rem == 0`
+// asserts). O(L) work on the coefficients instead of a coset NTT, a pointwise division by
+// (x_i - z) and a coset INTT of 4n points -- and no failure when z happens to lie on the
+// evaluation coset (the reference's long division has no such case).
+// Blocked linear recurrence with the constant multiplier z: (1) every block of HS_BLK
+// consecutive k runs its recurrence from 0 (per thread, then a Hillis-Steele pass over the
+// threads with multipliers z^(HS_PER 2^j)) and leaves its total; (2) one block turns the
+// totals into each block's incoming s (multiplier z^HS_BLK); (3) s_k += z^(k - k_b + 1) s_in.
+constexpr int HS_T = 256, HS_PER = 16, HS_BLK = HS_T * HS_PER, HS_LOG_T = 8;
+struct HsArgs {
+  const uint64_t* p;
+  uint64_t L;
+  U256 y;                 // subtracted from p_0 (Montgomery)
+  U256 z;                 // Montgomery
+  U256 zs[HS_LOG_T];      // z^(HS_PER 2^j)
+};
+// q[L-2-k] <- block-local s_k (k < L-1); the block-local remainder candidate in rem[block]
+__global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* totals, uint64_t* rem) {
+  __shared__ U256 sh[HS_T];
+  const int t = threadIdx.x;
+  const uint64_t k0 = (uint64_t)blockIdx.x * HS_BLK + (uint64_t)t * HS_PER;
+  U256 v[HS_PER];
+  U256 acc = u256_zero();
+#pragma unroll
+  for (int m = 0; m < HS_PER; ++m) {
+    const uint64_t k = k0 + m;
+    U256 u = u256_zero();
+    if (k < a.L) {
+      u = ldr(a.p + 4 * (a.L - 1 - k));
+      if (k == a.L - 1) u = Fr::sub(u, a.y);
+    }
+    acc = Fr::add(u, Fr::mul(a.z, acc));
+    v[m] = acc;
+  }
+  sh[t] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < HS_LOG_T; ++j) {
+    const int off = 1 << j;
+    U256 x = sh[t];
+    if (t >= off) x = Fr::add(x, Fr::mul(a.zs[j], sh[t - off]));
+    __syncthreads();
+    sh[t] = x;
+    __syncthreads();
+  }
+  const U256 carry = t ? sh[t - 1] : u256_zero();
+  U256 zk = a.z;
+#pragma unroll
+  for (int m = 0; m < HS_PER; ++m) {
+    const uint64_t k = k0 + m;
+    const U256 sk = Fr::add(v[m], Fr::mul(zk, carry));
+    zk = Fr::mul(zk, a.z);
+    if (k + 1 < a.L) str(q + 4 * (a.L - 2 - k), sk);
+    else if (k + 1 == a.L) str(rem, sk);
+  }
+  if (t == HS_T - 1) str(totals + 4 * blockIdx.x, sh[t]);
 }
-__global__ void k_sub_mul(const uint64_t* p, U256 y, const uint64_t* inv, uint64_t* out, uint64_t N) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < N) str(out + 4 * i, Fr::mul(Fr::sub(ldr(p + 4 * i), y), ldr(inv + 4 * i)));
+// totals[b] <- s_(b HS_BLK - 1), the s entering block b (0 for b = 0); one block
+__global__ void __launch_bounds__(HS_T) k_hs2(uint64_t* totals, uint64_t nb, U256 zb) {
+  __shared__ U256 sh[HS_T];
+  const int t = threadIdx.x;
+  const uint64_t per = (nb + HS_T - 1) / HS_T;
+  const uint64_t b0 = (uint64_t)t * per;
+  U256 acc = u256_zero();
+  for (uint64_t k = 0; k < per; ++k)
+    if (b0 + k < nb) acc = Fr::add(ldr(totals + 4 * (b0 + k)), Fr::mul(zb, acc));
+  sh[t] = acc;
+  __syncthreads();
+  U256 m = fr_pow(zb, per);  // multiplier across one thread's range
+  for (int off = 1; off < HS_T; off <<= 1) {
+    U256 x = sh[t];
+    if (t >= off) x = Fr::add(x, Fr::mul(m, sh[t - off]));
+    __syncthreads();
+    sh[t] = x;
+    __syncthreads();
+    m = Fr::mul(m, m);
+  }
+  U256 c = t ? sh[t - 1] : u256_zero();
+  for (uint64_t k = 0; k < per; ++k) {
+    if (b0 + k >= nb) break;
+    const U256 x = ldr(totals + 4 * (b0 + k));
+    str(totals + 4 * (b0 + k), c);
+    c = Fr::add(x, Fr::mul(zb, c));
+  }
+}
+// s_k += z^(k - k_b + 1) s_in(b); the remainder likewise
+__global__ void __launch_bounds__(HS_T) k_hs3(uint64_t* q, uint64_t L, U256 z, const uint64_t* totals,
+                                              uint64_t* rem) {
+  const uint64_t b = blockIdx.x;
+  if (b == 0) return;  // block 0 enters with s = 0
+  const U256 cin = ldr(totals + 4 * b);
+  const uint64_t k0 = b * HS_BLK + (uint64_t)threadIdx.x * HS_PER;
+  if (k0 >= L) return;
+  U256 zk = fr_pow(z, (uint64_t)threadIdx.x * HS_PER + 1);
+  for (int m = 0; m < HS_PER; ++m) {
+    const uint64_t k = k0 + m;
+    if (k >= L) break;
+    uint64_t* dst = k + 1 < L ? q + 4 * (L - 2 - k) : rem;
+    str(dst, Fr::add(ldr(dst), Fr::mul(zk, cin)));
+    zk = Fr::mul(zk, z);
+  }
 }
 
 // any nonzero element in [from, to) sets *bad
@@ -605,6 +696,28 @@ struct Prover {
     if ((rc = ag(sizeof(Xyzz)))) return rc;
     PBF_HIP(hipMemcpyAsync(slots + (uint64_t)slot * G, comm->recv, G * sizeof(Xyzz), hipMemcpyDeviceToDevice, s));
     return 0;
+  }
+  // q = (p - y) / (x - z) for p of L coefficients (k_hs1..3); a nonzero remainder fails with `err`
+  int synth_div(const uint64_t* p, uint64_t L, const U256& z, const U256& y, uint64_t* q, const char* err) {
+    if (L < 2) return fail(PBF_EINVAL, "synthetic division of a constant");
+    const uint64_t nb = (L + HS_BLK - 1) / HS_BLK;
+    DevBuf& hb = ctx->buf("pv.hs");
+    int rc = hb.ensure((nb + 1) * 32);
+    if (rc) return rc;
+    uint64_t* totals = (uint64_t*)hb.p;
+    uint64_t* rem = totals + 4 * nb;
+    HsArgs a;
+    a.p = p;
+    a.L = L;
+    a.y = y;
+    a.z = z;
+    for (int j = 0; j < HS_LOG_T; ++j) a.zs[j] = hpow64(z, (uint64_t)HS_PER << j);
+    hipLaunchKernelGGL(k_hs1, dim3((uint32_t)nb), dim3(HS_T), 0, s, a, q, totals, rem);
+    hipLaunchKernelGGL(k_hs2, dim3(1), dim3(HS_T), 0, s, totals, nb, hpow64(z, HS_BLK));
+    hipLaunchKernelGGL(k_hs3, dim3((uint32_t)nb), dim3(HS_T), 0, s, q, L, z, (const uint64_t*)totals, rem);
+    hipLaunchKernelGGL(k_nonzero, dim3(1), dim3(64), 0, s, (const uint64_t*)rem, 0, 1, d_bad);
+    PBF_HIP(hipGetLastError());
+    return check_bad(err);
   }
   int finish_commits(int count, uint64_t (*out)[8]) {
     std::vector<Xyzz> h((size_t)count * G);
@@ -975,38 +1088,15 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L, W2, N);
     PBF_HIP(hipGetLastError());
   }
-  // division by (x - z) on the coset: W(x_i) = P(x_i) / (x_i - z)
-  uint64_t* inv = W0;
-  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, NE, P.g,
-                     P.omegaN, zc, P.blk());
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((NE + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, NE, P.d_bad);
-  PBF_HIP(hipGetLastError());
-  if ((rc = P.check_bad("z lies on the evaluation coset"))) return rc;
-  if ((rc = P.coset_ntt(W2, N, W1))) return rc;  // numerator evaluations (rx no longer needed)
-  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)W1, u256_zero(),
-                     (const uint64_t*)inv, W2, NE);
-  PBF_HIP(hipGetLastError());
-  if ((rc = P.coset_intt(W2, W1))) return rc;  // W_z coefficients
-  const uint64_t wlen = rlen - 1 > m ? rlen - 1 : m;
-  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - wlen)), dim3(256), 0, s, (const uint64_t*)W1, wlen, N, P.d_bad);
-  PBF_HIP(hipGetLastError());
-  if ((rc = P.check_bad("W_z division left a remainder (plonk.rs:438)"))) return rc;
+  // W_z = numerator / (x - z), W_zw = (z(x) - z_w(z)) / (x - z w) (plonk.rs:430-442) by
+  // synthetic division on the coefficients (replicated on every rank of a sharded prove)
+  const uint64_t lnum = rlen > m ? rlen : m;  // numerator coefficients (t parts m, r rlen, a/b/c n+2)
+  const uint64_t wlen = lnum - 1;             // = max(rlen - 1, m)
+  if ((rc = P.synth_div(W2, lnum, zc, u256_zero(), W1, "W_z division left a remainder (plonk.rs:438)"))) return rc;
   if ((rc = P.commit(W1, wlen, 7))) return rc;
-  // W_zw = (z(x) - z_w(z)) / (x - z w)   (plonk.rs:441-442), z's coset evaluations reused
-  hipLaunchKernelGGL(k_coset_minus, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, inv, NE, P.g,
-                     P.omegaN, zw, P.blk());
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((NE + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)nullptr, (const uint64_t*)inv, inv, NE, P.d_bad);
-  hipLaunchKernelGGL(k_sub_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)CE(3), zw_z,
-                     (const uint64_t*)inv, W2, NE);
-  PBF_HIP(hipGetLastError());
-  if ((rc = P.check_bad("z w lies on the evaluation coset"))) return rc;
-  if ((rc = P.coset_intt(W2, W1))) return rc;
-  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(N - (n + 2))), dim3(256), 0, s, (const uint64_t*)W1, n + 2, N, P.d_bad);
-  PBF_HIP(hipGetLastError());
-  if ((rc = P.check_bad("W_zw division left a remainder (plonk.rs:442)"))) return rc;
-  if ((rc = P.commit(W1, n + 2, 8))) return rc;
+  uint64_t* W3 = W0;  // W1 still feeds the W_z commitment's MSM
+  if ((rc = P.synth_div(zx, n + 3, zw, zw_z, W3, "W_zw division left a remainder (plonk.rs:442)"))) return rc;
+  if ((rc = P.commit(W3, n + 2, 8))) return rc;
   if ((rc = P.finish_commits(9, pts))) return rc;
   P.mark("round 5 openings + 2 MSM");
 

@@ -88,3 +88,27 @@ def test_short_srs_rejected(ctx):
     srs = ctx.srs_create(5, n)
     with pytest.raises(pbf.PbfError):
         ctx.plonk_prove_bn254(q, cp, abc, [1, 2, 3, 4, 5], list(range(1, 10)), srs, mode=0)
+
+
+def test_challenge_on_the_evaluation_coset(ctx):
+    """The openings divide by (x - z) and (x - z w) on the coefficients (synthetic
+    division), so a challenge z on the prover's 4n-point coset g H_4n (or with z w there)
+    still gives the reference's proof (its long division, plonk.rs:430-442, has no such
+    case); the proof matches the literal oracle."""
+    import bn254 as F
+
+    n = 8
+    q, cp, abc = P.mul_gates_circuit(n, 3)
+    s = 0x1234567
+    srs_n = n + 3
+    rng = random.Random(8)
+    w4n = F.root_of_unity(4 * n)
+    for z in (5 * pow(w4n, 3, P.R) % P.R, 5 * pow(w4n, 9, P.R) * pow(F.root_of_unity(n), n - 1, P.R) % P.R):
+        chal = [rng.randrange(P.R) for _ in range(3)] + [z, rng.randrange(P.R)]
+        rnd = [rng.randrange(P.R) for _ in range(9)]
+        st = P.Setup(n, s, srs_n)
+        want_pts, want_f, _ = P.prove(st, q, cp, abc, chal, rnd, mode="paper")
+        srs = ctx.srs_create(s, srs_n)
+        pts, fs = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=1)
+        assert fs == [x % P.R for x in want_f]
+        assert [list(p) if p else None for p in pts] == [list(p) if p else None for p in want_pts]
