@@ -607,6 +607,19 @@ int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t
   return 0;
 }
 
+// the context's window table if it was built from exactly these points (fingerprint
+// checked), else null; never builds one
+int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
+  *out = nullptr;
+  auto& fb = ctx->fixed_base;
+  if (fb.ptr != (const void*)d_pts || fb.n != n || !fb.table.p) return 0;
+  uint64_t fp = 0;
+  int rc = msm_fingerprint_host(ctx, d_pts, n, s, &fp);
+  if (rc) return rc;
+  if (fp == fb.fingerprint) *out = (const Affine*)fb.table.p;
+  return 0;
+}
+
 int MsmTail::ensure() {
   if (aux) return 0;
   PBF_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));

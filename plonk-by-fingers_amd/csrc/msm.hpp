@@ -8,6 +8,8 @@ namespace pbf {
 // Window table (16 x n affine points, Montgomery) of the n canonical affine points at d_pts,
 // cached in the context and revalidated by a fingerprint of the points (one stream sync).
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out);
+// The cached table of exactly these points (fingerprint checked), or null (nothing built).
+int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out);
 // sum_{i<n} scalars[i] * P_(first+i) against a table of n_table points; the XYZZ result
 // (Montgomery) is written to *d_result by the context's side stream (see msm_fixed_wait);
 // nothing on the host waits for it.

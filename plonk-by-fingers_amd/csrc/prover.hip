@@ -1227,8 +1227,22 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   PBF_HIP(hipMemcpyAsync(c + 4 * n * 5, sg.p, 3 * n * E, hipMemcpyDeviceToDevice, s));
   if ((rc = pbf_ntt_fr256_batch_dev(ctx, w_plain, c, c, n, 8, 1, s))) return rc;
   uint64_t pre[8][8];
-  for (int k = 0; k < 8; ++k)
-    if ((rc = pbf_msm_g1_bn254_dev(ctx, d_srs, c + 4 * n * k, n, pre[k], s))) return rc;
+  const Affine* tbl = nullptr;  // the SRS window table, when a prove on this context built it
+  if ((rc = msm_fixed_lookup(ctx, d_srs, srs_m, s, &tbl))) return rc;
+  if (tbl) {
+    DevBuf& vs = ctx->buf("vf.commits");
+    if ((rc = vs.ensure(8 * sizeof(Xyzz)))) return rc;
+    for (int k = 0; k < 8; ++k)
+      if ((rc = msm_fixed_device(ctx, tbl, srs_m, 0, c + 4 * n * k, n, s, (Xyzz*)vs.p + k))) return rc;
+    if ((rc = msm_fixed_wait(ctx, s))) return rc;
+    Xyzz h[8];
+    PBF_HIP(hipMemcpyAsync(h, vs.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < 8; ++k) xyzz_to_affine_u64(h[k], pre[k]);
+  } else {
+    for (int k = 0; k < 8; ++k)
+      if ((rc = pbf_msm_g1_bn254_dev(ctx, d_srs, c + 4 * n * k, n, pre[k], s))) return rc;
+  }
   int bad = 0;
   PBF_HIP(hipMemcpyAsync(&bad, fl.p, sizeof(int), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));

@@ -49,7 +49,7 @@ def _inputs(n, seed, mode):
     return ctx, (dq, dc, dabc, dsrs, srs_m, chal, rnd), ref
 
 
-@pytest.mark.parametrize("G,log_n,mode", [(2, 10, 1), (4, 10, 1), (8, 10, 1), (2, 12, 0), (8, 5, 1)])
+@pytest.mark.parametrize("G,log_n,mode", [(2, 10, 1), (4, 10, 1), (8, 10, 1), (2, 12, 0), (8, 5, 1), (8, 17, 1)])
 def test_sharded_prove_virtual_ranks(G, log_n, mode):
     import torch
 
