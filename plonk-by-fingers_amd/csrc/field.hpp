@@ -18,6 +18,71 @@ struct FieldArgs {
   uint64_t mu;  // Mod32 only: floor(2^64 / m)
 };
 
+#ifdef __HIP_DEVICE_COMPILE__
+// ---- carry-exact device primitives for Goldilocks reductions (gfx950) -------------------
+// One instruction per asm statement, register operands only: the compiler allocates, and
+// its hazard recognizer sees the SGPR lane-mask def/use of each statement (it inserts the
+// wait states a VALU-written carry needs before a VALU reads it). What the compiler cannot
+// express by itself is the carry-out of v_mad_u64_u32, so a reduction that would otherwise
+// recompute carries with 64-bit compares uses it directly.
+struct GlMadC {
+  uint64_t v;  // low 64 bits of a*b + c
+  uint64_t c;  // lane mask: a*b + c >= 2^64
+};
+__device__ __forceinline__ GlMadC gl_mad_c(uint32_t a, uint32_t b, uint64_t c) {
+  GlMadC r;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r.v), "=s"(r.c) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t gl_sub_co(uint32_t a, uint32_t b, uint64_t* borrow) {
+  uint32_t r;
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(*borrow) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t gl_subb0(uint32_t a, uint64_t bin, uint64_t* borrow) {
+  uint32_t r;
+  asm("v_subbrev_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(r), "=s"(*borrow) : "v"(a), "s"(bin));
+  return r;
+}
+__device__ __forceinline__ uint64_t gl_ge_p(uint64_t r) {  // lane mask: r >= p
+  uint64_t m;
+  asm("v_cmp_lt_u64_e64 %0, %1, %2" : "=s"(m) : "s"(0xFFFFFFFF00000000ull), "v"(r));
+  return m;
+}
+template <uint32_t K>
+__device__ __forceinline__ uint32_t gl_selk(uint32_t a, uint64_t m) {  // m ? K : a
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %3, %2" : "=v"(r) : "v"(a), "s"(m), "i"(K));
+  return r;
+}
+// lo + h*(2^32-1) (mod p), canonical; lo < 2^64, h < 2^32. With the carry c of the 64-bit
+// sum r, the value is r + c*EPS: c = 1 leaves r < 2^64 - 2^33, so r + EPS is canonical;
+// c = 0 and r >= p gives r - p = r + EPS (mod 2^64). 6 VALU.
+__device__ __forceinline__ uint64_t gl_addmul_eps(uint64_t lo, uint32_t h) {
+  const GlMadC m = gl_mad_c(h, 0xFFFFFFFFu, lo);
+  const uint32_t a0 = gl_selk<0xFFFFFFFFu>(0u, m.c | gl_ge_p(m.v));
+  return m.v + a0;
+}
+// lo + h0*2^64 + h1*2^96 = lo + h0*EPS - h1 (mod p), canonical; lo < 2^64, h0, h1 < 2^32.
+// r = lo + h0*EPS with carry c1 (+EPS), then r -= h1 with borrow c2 (-EPS). c1 without c2
+// leaves r < 2^64 - 2^33 (r + EPS canonical); c2 without c1 leaves r >= 2^64 - 2^32 (r - EPS
+// canonical); both or neither: r, minus p when r >= p. One 64-bit addend per case:
+// +EPS = {2^32-1, 0}, -EPS = {1, 2^32-1} (mod 2^64). 9 VALU against 15-17 for the compiler's
+// compare-derived carries.
+__device__ __forceinline__ uint64_t gl_red96(uint64_t lo, uint32_t h0, uint32_t h1) {
+  const GlMadC m = gl_mad_c(h0, 0xFFFFFFFFu, lo);
+  uint64_t c2;
+  const uint32_t r0 = gl_sub_co((uint32_t)m.v, h1, &c2);
+  const uint32_t r1 = gl_subb0((uint32_t)(m.v >> 32), c2, &c2);
+  const uint64_t r = ((uint64_t)r1 << 32) | r0;
+  const uint64_t plus = (m.c & ~c2) | (gl_ge_p(r) & ~(m.c ^ c2));
+  const uint64_t minus = c2 & ~m.c;
+  const uint32_t a0 = gl_selk<1u>(gl_selk<0xFFFFFFFFu>(0u, plus), minus);
+  const uint32_t a1 = gl_selk<0xFFFFFFFFu>(0u, minus);
+  return r + (((uint64_t)a1 << 32) | a0);
+}
+#endif
+
 struct Goldilocks {
   static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
   static constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p = 2^32 - 1
@@ -48,6 +113,9 @@ struct Goldilocks {
   }
   // 128-bit value lo + hi*2^64 reduced with 2^64 = 2^32 - 1 and 2^96 = -1 (mod p).
   __host__ __device__ __forceinline__ static uint64_t reduce128(uint64_t lo, uint64_t hi) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return gl_red96(lo, (uint32_t)hi, (uint32_t)(hi >> 32));
+#else
     const uint64_t hh = hi >> 32, hl = (uint32_t)hi;
     uint64_t t0;
     const bool br = __builtin_sub_overflow(lo, hh, &t0);
@@ -56,6 +124,7 @@ struct Goldilocks {
     const bool c = __builtin_add_overflow(t0, hl * EPS, &r);
     r += c ? EPS : 0;                     // wrap: + 2^64 = + EPS (cannot wrap again)
     return r >= P ? r - P : r;
+#endif
   }
   // 64x64 -> 128 from four v_mad_u64_u32 (the carries ride in the 64-bit addends).
   __host__ __device__ __forceinline__ static uint64_t mul(uint64_t a, uint64_t b, const FieldArgs&) {
@@ -73,6 +142,14 @@ struct Goldilocks {
     const bool wrap = __builtin_add_overflow(lo, t, &s);
     return s + ((wrap || s >= P) ? EPS : 0);
   }
+  // lo + h*EPS (mod p), canonical, for any lo < 2^64 and h < 2^32.
+  __host__ __device__ __forceinline__ static uint64_t add_mul_eps(uint64_t lo, uint32_t h) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return gl_addmul_eps(lo, h);
+#else
+    return add_small(lo, (uint64_t)h * EPS);
+#endif
+  }
   // x * 2^S (mod p) for a compile-time 0 <= S < 96, x canonical.
   template <int S>
   __host__ __device__ __forceinline__ static uint64_t mul_pow2(uint64_t x) {
@@ -81,9 +158,7 @@ struct Goldilocks {
       return x;
     } else if constexpr (S <= 32) {
       // x*2^S = lo + hi*2^64 with hi < 2^S <= 2^32, and hi*2^64 = hi*EPS (mod p)
-      const uint64_t hi = x >> (64 - S);
-      const uint64_t lo = x << S;
-      return add_small(lo, (hi << 32) - hi);
+      return add_mul_eps(x << S, (uint32_t)(x >> (64 - S)));
     } else if constexpr (S < 64) {
       return reduce128(x << S, x >> (64 - S));
     } else {
@@ -108,7 +183,7 @@ __host__ __device__ __forceinline__ uint64_t gl_div_pow2(uint64_t x) {
   const uint32_t m = (0u - (uint32_t)x) & mask;
   const uint64_t q = (x + m) >> K;
   const uint32_t mp = K == 32 ? m : (m << ((32 - K) & 31));
-  return Goldilocks::add_small(q, (uint64_t)mp * Goldilocks::EPS);
+  return Goldilocks::add_mul_eps(q, mp);
 }
 
 struct Mod32 {

@@ -527,7 +527,10 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
     }
     const uint32_t grid = persist ? persistent_grid((const void*)fn, tile / 16, tiles) : (uint32_t)tiles;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), 0, stream, a);
+    // A/B diagnostic: extra dynamic LDS per workgroup (PBF_NTT_LDSPAD bytes) lowers the
+    // workgroups resident per CU without changing the code
+    const size_t ldspad = getenv("PBF_NTT_LDSPAD") ? (size_t)atoll(getenv("PBF_NTT_LDSPAD")) : 0;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), ldspad, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;
   }

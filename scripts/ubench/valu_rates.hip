@@ -90,6 +90,9 @@
 #define J_LSHL64(r) "v_lshlrev_b64 " r ", 3, " r "\n"
 #define J_MOV64(r) "v_mov_b64 " r ", %8\n"
 #define J_PKADD(r) "v_pk_add_f32 " r ", " r ", %8\n"
+#define J_MADI64(r) "v_mad_i64_i32 " r ", s[40:41], %9, %9, " r "\n"
+#define J_ASHR64(r) "v_ashrrev_i64 " r ", 3, " r "\n"
+#define J_LSHR64(r) "v_lshrrev_b64 " r ", 3, " r "\n"
 #define J_PKMOV(r) "v_pk_mov_b32 " r ", " r ", %8 op_sel:[0,1]\n"
 #define K64(NAME, I)                                                                   \
   __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed) {           \
@@ -148,6 +151,14 @@ K64(k_lshl64, J_LSHL64)
 K64(k_mov64, J_MOV64)
 K64(k_pk_add_f32, J_PKADD)
 K64(k_pk_mov, J_PKMOV)
+K64(k_madi64, J_MADI64)
+K64(k_ashr64, J_ASHR64)
+K64(k_lshr64, J_LSHR64)
+#define I_DPP(r) "v_mov_b32_dpp " r ", %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+#define I_PL32(r) "v_permlane32_swap_b32 " r ", %8\n"
+#define I_SUBCO(r) "v_sub_co_u32 " r ", vcc, " r ", %8\n"
+K(k_dpp, I_DPP)
+K(k_subco, I_SUBCO)
 
 typedef void (*kfn)(uint32_t*, uint32_t);
 int main() {
@@ -162,7 +173,7 @@ int main() {
       {"v_lshrrev_b32", k_lshr}, {"v_lshlrev_b32 vreg", k_lshlv}, {"v_ashrrev_i32", k_ashr}, {"v_add_co_u32_e64 sdst", k_addco3},
       {"v_mul_u32_u24", k_mulu24}, {"v_fma_f32", k_fmaf}, {"v_mul_f32", k_mulf}, {"v_subrev_u32", k_subrev},
       {"v_lshl_add_u64", k_lshl_add64}, {"v_mad_u64_u32", k_mad64}, {"v_cmp_lt_u64", k_cmp64},
-      {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mov_b32", k_pk_mov},
+      {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mov_b32", k_pk_mov}, {"v_mad_i64_i32", k_madi64}, {"v_ashrrev_i64", k_ashr64}, {"v_lshrrev_b64", k_lshr64}, {"v_mov_b32_dpp", k_dpp}, {"v_sub_co_u32", k_subco},
   };
   const int blocks = 256 * 8 * 4;  // 8 workgroups of 256 threads per CU resident = 8 waves/SIMD, x4 rounds
   uint32_t* out;
