@@ -91,7 +91,7 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
 }
 
 #ifndef PBF_MSM_CH
-#define PBF_MSM_CH 32
+#define PBF_MSM_CH 43
 #endif
 #ifndef PBF_MSM_ACC_WPE
 #define PBF_MSM_ACC_WPE 3
@@ -378,6 +378,102 @@ __global__ void __launch_bounds__(256) msm_join_final(const ChunkPart* head, con
   if (k == sent) return;
   buckets[k] = G1::add(tail[t].acc, head[t + 1].acc);  // a tail always has a continuation
 }
+
+// bucket bounds and the span counter of a fixed-base MSM, zeroed in one launch
+__global__ void __launch_bounds__(256) msm_fx_clear(uint32_t* start, uint32_t* end, uint32_t* span) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  start[k] = 0;
+  end[k] = 0;
+  if (k == 0) *span = 0;
+}
+
+// Join steps past FX_JOIN_GROUP / 2 are not launched (a bucket of the random-digit case
+// spans ~16 chunks); this kernel finishes the rare buckets spanning more than FX_JOIN_GROUP
+// continuation chunks (skewed digits): after the steps 1 .. FX_JOIN_GROUP / 2,
+// head[o + 1 + G j] holds the sum of group j, so head[o + 1] += sum_{j >= 1} head[o + 1 + G j].
+constexpr uint32_t FX_JOIN_GROUP = 32;
+__global__ void __launch_bounds__(256) msm_join_rest(ChunkPart* head, const uint32_t* start, const uint32_t* end,
+                                                     uint32_t nb, const uint32_t* span) {
+  if (*span <= FX_JOIN_GROUP) return;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nb || end[k] <= start[k]) return;
+  const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH;
+  if (e - o <= FX_JOIN_GROUP) return;
+  Xyzz acc = head[o + 1].acc;
+  for (uint32_t u = o + 1 + FX_JOIN_GROUP; u <= e; u += FX_JOIN_GROUP) acc = G1::add(acc, head[u].acc);
+  head[o + 1].acc = acc;
+}
+
+// Bucket b's full sum after the join: a bucket spanning chunks o < e is its chunk-o tail run
+// plus the joined continuations head[o + 1]; any other bucket was written whole (or is
+// empty: zero = identity). Fuses what msm_join_final wrote back.
+__device__ __forceinline__ Xyzz fx_bucket(uint32_t k, const Xyzz* buckets, const ChunkPart* head,
+                                          const ChunkPart* tail, const uint32_t* start, const uint32_t* end) {
+  const uint32_t bs = start[k], be = end[k];
+  if (be <= bs) return G1::identity();
+  const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+  return o < e ? G1::add(tail[o].acc, head[o + 1].acc) : buckets[k];
+}
+
+// Workgroup tree sum of one value per thread (blockDim.x a power of two <= 256) -> *out.
+__device__ __forceinline__ void fx_tree(Xyzz v, Xyzz* out) {
+  __shared__ Xyzz red[256];
+  const uint32_t t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (uint32_t st = blockDim.x / 2; st > 0; st >>= 1) {
+    if (t < st) red[t] = G1::add(red[t], red[t + st]);
+    __syncthreads();
+  }
+  if (t == 0) *out = red[0];
+}
+
+// Fixed-base bucket reduction T = sum_{b < 2^15} (b + 1) B_b as short parallel trees instead
+// of running sums (the tail is a latency chain: its depth in point additions is its time).
+// With b = 256 h + l (h < 128, l < 256), C_h = sum_l B_(256h+l), D_l = sum_h B_(256h+l):
+//   T = sum_{k<7} 2^(k+8) Z_k + sum_{k<8} 2^k Y_k + S,
+//   Z_k = sum_{h: bit k of h} C_h,  Y_k = sum_{l: bit k of l} D_l,  S = sum_h C_h
+// (sum_b b B_b = 256 sum_h h C_h + sum_l l D_l; sum_b B_b = S). Depth: 9 additions (C/D
+// trees), 7 (subset trees), <= 14 doublings, 4 (final sum) -- against ~60 for the
+// segment running sums and their tree.
+constexpr uint32_t FX_NH = FX_NB / 256;  // 128 values of h
+static_assert(FX_NH == 128, "2^15 buckets = 128 x 256");
+// workgroup g < 128: C_g (256 buckets); g >= 128: D_(g-128) (128 buckets)
+__global__ void __launch_bounds__(256) msm_fx_cd(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
+                                                 const uint32_t* start, const uint32_t* end, Xyzz* cd) {
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  Xyzz v;
+  if (g < FX_NH)
+    v = fx_bucket(256 * g + t, buckets, head, tail, start, end);
+  else
+    v = t < FX_NH ? fx_bucket(256 * t + (g - FX_NH), buckets, head, tail, start, end) : G1::identity();
+  fx_tree(v, cd + g);
+}
+// workgroup s (128 threads): s < 8: 2^s Y_s; 8 <= s < 15: 2^s Z_(s-8); s = 15: S.
+__global__ void __launch_bounds__(128) msm_fx_subsets(const Xyzz* cd, Xyzz* sub) {
+  const uint32_t s = blockIdx.x, t = threadIdx.x;
+  const Xyzz* C = cd;
+  const Xyzz* D = cd + FX_NH;
+  Xyzz v;
+  if (s < 8) {  // the t-th l with bit s set
+    v = D[((t >> s) << (s + 1)) | (1u << s) | (t & ((1u << s) - 1))];
+  } else if (s < 15) {
+    const uint32_t k = s - 8;
+    v = t < 64 ? C[((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1))] : G1::identity();
+  } else {
+    v = C[t];
+  }
+  __shared__ Xyzz res;
+  fx_tree(v, &res);
+  if (t == 0) {
+    Xyzz r = res;
+    const uint32_t e = s < 15 ? s : 0;  // Y_s weight 2^s; Z_k weight 2^(k+8) = 2^s
+    for (uint32_t i = 0; i < e; ++i) r = G1::dbl(r);
+    sub[s] = r;
+  }
+}
+// one workgroup of 16 threads: the sum of the 16 scaled subset sums
+__global__ void __launch_bounds__(16) msm_fx_total(const Xyzz* sub, Xyzz* out) { fx_tree(sub[threadIdx.x], out); }
 
 // 64-bit fingerprint of n canonical affine points (8 u64 each): block XORs of a position-
 // mixed hash, then one block folds them (validates a cached table against the points)
@@ -674,12 +770,10 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   if (tl.used[slot]) PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
   const uint64_t hbytes = (m / MSM_CH + 1) * sizeof(ChunkPart);
   if ((head.bytes < hbytes || tail.bytes < hbytes) && tl.used[slot]) PBF_HIP(hipEventSynchronize(tl.done[slot]));
-  constexpr uint32_t NSEG = FX_NB / MSM_SEG, NPART = NSEG / MSM_SEG_THREADS;
-  static_assert(NSEG % MSM_SEG_THREADS == 0 && NPART <= MSM_SEG_THREADS, "reduction shape");
   if ((rc = keys.ensure(m * 4)) || (rc = vals.ensure(m * 4)) || (rc = keys2.ensure(m * 4)) ||
       (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)FX_NB * 4)) || (rc = end.ensure((uint64_t)FX_NB * 4)) ||
-      (rc = buckets.ensure((uint64_t)FX_NB * sizeof(Xyzz))) || (rc = shares.ensure((uint64_t)NSEG * sizeof(Xyzz))) ||
-      (rc = parts.ensure(NPART * sizeof(Xyzz))) || (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) ||
+      (rc = buckets.ensure((uint64_t)FX_NB * sizeof(Xyzz))) || (rc = shares.ensure((uint64_t)(FX_NH + 256) * sizeof(Xyzz))) ||
+      (rc = parts.ensure(16 * sizeof(Xyzz))) || (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) ||
       (rc = spb.ensure(4)))
     return rc;
   const uint8_t* inf = (const uint8_t*)fb.inf.p;
@@ -692,13 +786,12 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   if ((rc = temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
   PBF_HIP(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
                                              (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, FX_C, s));
-  PBF_HIP(hipMemsetAsync(start.p, 0, (uint64_t)FX_NB * 4, s));
-  PBF_HIP(hipMemsetAsync(end.p, 0, (uint64_t)FX_NB * 4, s));
+  hipLaunchKernelGGL(msm_fx_clear, dim3(FX_NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
+                     (uint32_t*)spb.p);
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
                      (uint32_t*)start.p, (uint32_t*)end.p, FX_NB);
   // ---- accumulation
-  PBF_HIP(hipMemsetAsync(buckets.p, 0, (uint64_t)FX_NB * sizeof(Xyzz), s));
-  PBF_HIP(hipMemsetAsync(spb.p, 0, 4, s));
+  // no bucket memset: msm_fx_cd reads only the buckets the accumulation wrote (fx_bucket)
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
   hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
                      (const uint32_t*)vals2.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)m,
@@ -710,21 +803,21 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   hipStream_t a = tl.aux;
   PBF_HIP(hipEventRecord(tl.ready[slot], s));
   PBF_HIP(hipStreamWaitEvent(a, tl.ready[slot], 0));
-  // ceil(log2(nchunks)) steps bound any span; steps past the largest span exit at once. The
-  // grid covers the mean span's pair slots (the kernel strides over the rest).
+  // join steps 1 .. FX_JOIN_GROUP / 2 (steps past the largest span exit at once); wider spans
+  // are finished by msm_join_rest. The grid covers the mean span's pair slots (the kernel
+  // strides over the rest).
   const uint64_t mean_span = m / ((uint64_t)FX_NB * MSM_CH) + 2;
-  for (uint32_t step = 1; step < nchunks; step <<= 1) {
+  for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
     const uint64_t items = (uint64_t)FX_NB * ((mean_span + 2 * step - 1) / (2 * step));
     hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
                        (const uint32_t*)start.p, (const uint32_t*)end.p, FX_NB, step, (const uint32_t*)spb.p);
   }
-  hipLaunchKernelGGL(msm_join_final, dim3((nchunks + 255) / 256), dim3(256), 0, a, (const ChunkPart*)head.p,
-                     (const ChunkPart*)tail.p, nchunks, (Xyzz*)buckets.p, FX_NB);
-  hipLaunchKernelGGL(msm_segments<FX_NB>, dim3((NSEG + 255) / 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
-                     (Xyzz*)shares.p, 1u);
-  hipLaunchKernelGGL(msm_window_reduce, dim3(NPART), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)shares.p,
-                     (Xyzz*)parts.p);
-  hipLaunchKernelGGL(msm_window_final, dim3(1), dim3(MSM_SEG_THREADS), 0, a, (const Xyzz*)parts.p, d_result, NPART);
+  hipLaunchKernelGGL(msm_join_rest, dim3(FX_NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
+                     (const uint32_t*)end.p, FX_NB, (const uint32_t*)spb.p);
+  hipLaunchKernelGGL(msm_fx_cd, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p, (const ChunkPart*)head.p,
+                     (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p);
+  hipLaunchKernelGGL(msm_fx_subsets, dim3(16), dim3(128), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
+  hipLaunchKernelGGL(msm_fx_total, dim3(1), dim3(16), 0, a, (const Xyzz*)parts.p, d_result);
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipEventRecord(tl.done[slot], a));
   tl.used[slot] = true;
