@@ -120,6 +120,49 @@ struct G1 {
     r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
     return r;
   }
+  // add / dbl with the independent products paired through F::mul2 (bit-identical results):
+  // 7 product pairs for add-2008-s and 5 steps for dbl-2008-s-1 instead of 14 and 9 single
+  // products. For single-lane latency chains (the MSM's reduction trees); the throughput
+  // kernels keep add / dbl.
+  __host__ __device__ __forceinline__ static Xyzz dbl2(const Xyzz& p) {
+    if (is_identity(p)) return p;
+    const U256 U = dbl_f(p.Y);
+    U256 V, xx, W, S, MM, ZZ3, WY, ZZZ3;
+    F::mul2(U, U, p.X, p.X, &V, &xx);
+    F::mul2(U, V, p.X, V, &W, &S);
+    const U256 M = F::add(dbl_f(xx), xx);
+    F::mul2(M, M, V, p.ZZ, &MM, &ZZ3);
+    F::mul2(W, p.Y, W, p.ZZZ, &WY, &ZZZ3);
+    Xyzz r;
+    r.X = F::sub(MM, dbl_f(S));
+    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), WY);
+    r.ZZ = ZZ3;
+    r.ZZZ = ZZZ3;
+    return r;
+  }
+  __host__ __device__ __forceinline__ static Xyzz add2(const Xyzz& p, const Xyzz& q) {
+    if (is_identity(p)) return q;
+    if (is_identity(q)) return p;
+    U256 U1, U2, S1, S2;
+    F::mul2(p.X, q.ZZ, q.X, p.ZZ, &U1, &U2);
+    F::mul2(p.Y, q.ZZZ, q.Y, p.ZZZ, &S1, &S2);
+    const U256 P = F::sub(U2, U1);
+    const U256 R = F::sub(S2, S1);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return dbl2(p);
+      return identity();
+    }
+    U256 PP, RR, PPP, Q, ZZ12, ZZZ12, S1P, Y3a;
+    F::mul2(P, P, R, R, &PP, &RR);
+    F::mul2(p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, &ZZ12, &ZZZ12);
+    F::mul2(P, PP, U1, PP, &PPP, &Q);
+    Xyzz r;
+    r.X = F::sub(F::sub(RR, PPP), dbl_f(Q));
+    F::mul2(R, F::sub(Q, r.X), S1, PPP, &Y3a, &S1P);
+    r.Y = F::sub(Y3a, S1P);
+    F::mul2(ZZ12, PP, ZZZ12, PPP, &r.ZZ, &r.ZZZ);
+    return r;
+  }
   // k * p for a small non-negative k (double-and-add, MSB first)
   __host__ __device__ __forceinline__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
     Xyzz r = identity();

@@ -307,6 +307,83 @@ struct Fp256 {
     r.w[7] = (uint32_t)c0;  // the result is < 2p < 2^256: nothing above
     return reduce_once(r);
   }
+  // Two chains of each of two products: four independent v_mad_u64_u32, then their four
+  // carry folds -- each carry is read three instructions after its write, so no wait-state
+  // pad (mac2 needs one s_nop per pair, mac1 two).
+  __device__ __forceinline__ static void mac4(uint64_t& a0, uint32_t& a1, uint32_t xa, uint32_t ya, uint64_t& b0,
+                                              uint32_t& b1, uint32_t xb, uint32_t yb, uint64_t& c0, uint32_t& c1,
+                                              uint32_t xc, uint32_t yc, uint64_t& d0, uint32_t& d1, uint32_t xd,
+                                              uint32_t yd) {
+    uint64_t ca, cb, cc, cd;
+    asm("v_mad_u64_u32 %0, %4, %12, %13, %0\n\t"
+        "v_mad_u64_u32 %1, %5, %14, %15, %1\n\t"
+        "v_mad_u64_u32 %2, %6, %16, %17, %2\n\t"
+        "v_mad_u64_u32 %3, %7, %18, %19, %3\n\t"
+        "v_addc_co_u32_e64 %8, %4, %8, 0, %4\n\t"
+        "v_addc_co_u32_e64 %9, %5, %9, 0, %5\n\t"
+        "v_addc_co_u32_e64 %10, %6, %10, 0, %6\n\t"
+        "v_addc_co_u32_e64 %11, %7, %11, 0, %7"
+        : "+v"(a0), "+v"(b0), "+v"(c0), "+v"(d0), "=&s"(ca), "=&s"(cb), "=&s"(cc), "=&s"(cd), "+v"(a1), "+v"(b1),
+          "+v"(c1), "+v"(d1)
+        : "v"(xa), "v"(ya), "v"(xb), "v"(yb), "v"(xc), "v"(yc), "v"(xd), "v"(yd));
+  }
+  // Two independent Montgomery products (*r = a b, *s = c d) by one interleaved column scan:
+  // bit-identical to two mul() calls, for code whose time is one wave's instruction stream
+  // (the MSM's reduction trees, single-lane point chains): the two products' chains fill each
+  // other's carry wait states, so the stream carries no s_nop pads.
+  __device__ __forceinline__ static void mul2(const U256& a, const U256& b, const U256& c, const U256& d, U256* r,
+                                              U256* s) {
+    uint32_t m[8], n[8];
+    U256 ra, rb;
+    uint64_t A0 = 0, B0 = 0;
+    uint32_t A1 = 0, B1 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+      const int nm = k < 8 ? k : 8 - lo;
+      uint32_t xa[16], ya[16], xb[16], yb[16];
+      int cnt = 0;
+#pragma unroll
+      for (int i = lo; i <= hi; ++i) {
+        xa[cnt] = a.w[i]; ya[cnt] = b.w[k - i];
+        xb[cnt] = c.w[i]; yb[cnt] = d.w[k - i];
+        ++cnt;
+      }
+#pragma unroll
+      for (int i = lo; i < lo + nm; ++i) {
+        xa[cnt] = m[i]; ya[cnt] = Prm::P[k - i];
+        xb[cnt] = n[i]; yb[cnt] = Prm::P[k - i];
+        ++cnt;
+      }
+      uint64_t A2 = 0, B2 = 0;
+      uint32_t A3 = 0, B3 = 0;
+#pragma unroll
+      for (int t = 0; t + 1 < cnt; t += 2)
+        mac4(A0, A1, xa[t], ya[t], B0, B1, xb[t], yb[t], A2, A3, xa[t + 1], ya[t + 1], B2, B3, xb[t + 1], yb[t + 1]);
+      if (cnt & 1) mac2(A0, A1, xa[cnt - 1], ya[cnt - 1], B0, B1, xb[cnt - 1], yb[cnt - 1]);
+      const uint64_t sa = A0 + A2, sb = B0 + B2;
+      A1 = A1 + A3 + (sa < A0 ? 1u : 0u);
+      B1 = B1 + B3 + (sb < B0 ? 1u : 0u);
+      A0 = sa;
+      B0 = sb;
+      if (k < 8) {
+        m[k] = (uint32_t)A0 * Prm::NP;
+        n[k] = (uint32_t)B0 * Prm::NP;
+        mac2(A0, A1, m[k], Prm::P[0], B0, B1, n[k], Prm::P[0]);
+      } else {
+        ra.w[k - 8] = (uint32_t)A0;
+        rb.w[k - 8] = (uint32_t)B0;
+      }
+      A0 = (A0 >> 32) | ((uint64_t)A1 << 32);
+      B0 = (B0 >> 32) | ((uint64_t)B1 << 32);
+      A1 = 0;
+      B1 = 0;
+    }
+    ra.w[7] = (uint32_t)A0;
+    rb.w[7] = (uint32_t)B0;
+    *r = reduce_once(ra);
+    *s = reduce_once(rb);
+  }
 #else
   // -p^-1 mod 2^64 from the 32-bit constant's modulus by Newton's iteration (x <- x(2 - p x)
   // doubles the correct low bits; p is odd so x = p is right mod 2^3)
@@ -371,6 +448,10 @@ struct Fp256 {
       r.w[2 * i + 1] = (uint32_t)(o >> 32);
     }
     return r;
+  }
+  static void mul2(const U256& a, const U256& b, const U256& c, const U256& d, U256* r, U256* s) {
+    *r = mul(a, b);
+    *s = mul(c, d);
   }
   // CIOS Montgomery product over 8 x 32-bit limbs (host cross-check of mul)
   static U256 mul_cios32(const U256& a, const U256& b) {

@@ -10,11 +10,9 @@
 //   4. msm_chunk_acc: the sorted list cut into fixed chunks of MSM_CH entries, one thread
 //      per chunk accumulating its runs of equal keys in XYZZ (every thread does the same
 //      number of additions whatever the bucket sizes); runs that cross a chunk boundary
-//      leave partial sums, which msm_chunk_join adds up (one thread per bucket that starts
-//      in a chunk and ends in a later one)
-//   5. msm_segments + msm_window_reduce: per window, segments of 8 buckets; running sums
-//      give sum (j-a+1) B_j and sum B_j per segment, + a * (segment sum); the segment
-//      shares are summed by LDS trees over (window, part) workgroups, then per window
+//      leave partial sums, which a tree join adds up (msm_join_step / msm_join_rest)
+//   5. bucket reduction sum_b (b + 1) B_b per window as short parallel trees
+//      (msm_fx_cd / msm_fx_subsets / msm_fx_total, see there)
 //   6. host: Horner over the 16 window sums (2^16 steps), one inversion to affine.
 // The result is a group element, so the canonical affine output is unique.
 #include <hipcub/hipcub.hpp>
@@ -32,7 +30,6 @@ constexpr int MSM_BB = MSM_C - 1;                            // bucket-index bit
 constexpr uint32_t MSM_NB = 1u << MSM_BB;                    // buckets per window
 constexpr uint32_t MSM_SENTINEL = (uint32_t)MSM_NW << MSM_BB;  // sorts after every real key
 constexpr uint32_t MSM_NEG = 0x80000000u;                    // sign flag in the point index
-constexpr int MSM_SEG_THREADS = 256;
 
 __device__ __forceinline__ U256 load_u256(const uint64_t* p) {
   U256 r;
@@ -95,9 +92,6 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
 #endif
 #ifndef PBF_MSM_ACC_WPE
 #define PBF_MSM_ACC_WPE 3
-#endif
-#ifndef PBF_MSM_SEG_WPE
-#define PBF_MSM_SEG_WPE 1
 #endif
 constexpr uint32_t MSM_CH = PBF_MSM_CH;  // sorted entries per accumulation thread
 
@@ -162,77 +156,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
     acc = G1::madd(acc, p);
   }
   flush(c1);
-}
-
-// one thread per chunk owning a boundary-crossing bucket: its tail plus the heads of the
-// following chunks the bucket covers
-__global__ void __launch_bounds__(256) msm_chunk_join(const ChunkPart* head, const ChunkPart* tail,
-                                                      const uint32_t* end, uint32_t nchunks, Xyzz* buckets,
-                                                      uint32_t sent) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nchunks) return;
-  const uint32_t k = tail[t].key;
-  if (k == sent) return;
-  Xyzz acc = tail[t].acc;
-  const uint32_t be = end[k];
-  for (uint32_t u = t + 1; u < nchunks && u * MSM_CH < be; ++u) acc = G1::add(acc, head[u].acc);
-  buckets[k] = acc;
-}
-
-__device__ __forceinline__ Xyzz xyzz_neg(const Xyzz& p) {
-  Xyzz r = p;
-  r.Y = Fq::sub(u256_zero(), p.Y);
-  return r;
-}
-
-// S_w = sum_j (j + 1) * B_{w,j}, in two launches. (a) one thread per (window, segment of
-// MSM_SEG buckets starting at a): running sums give sum (j - a + 1) B_j and sum B_j, and
-// the segment's share is wsum + a * running. (b) one workgroup per window sums its segment
-// shares (sequential per thread, then an LDS tree).
-#ifndef PBF_MSM_SEG
-#define PBF_MSM_SEG 8
-#endif
-constexpr uint32_t MSM_SEG = PBF_MSM_SEG;
-constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
-
-template <uint32_t NB>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_SEG_WPE))) msm_segments(const Xyzz* buckets, Xyzz* shares, uint32_t nw) {
-  constexpr uint32_t NSEG = NB / MSM_SEG;
-  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= nw * NSEG) return;
-  const uint32_t w = id / NSEG, seg = id % NSEG;
-  const uint32_t a = seg * MSM_SEG;
-  const Xyzz* B = buckets + (uint64_t)w * NB;
-  Xyzz running = G1::identity(), wsum = G1::identity();
-  for (int k = (int)(a + MSM_SEG - 1); k >= (int)a; --k) {
-    running = G1::add(running, B[k]);
-    wsum = G1::add(wsum, running);
-  }
-  shares[id] = (a == 0) ? wsum : G1::add(wsum, G1::mul_small(running, a));
-}
-
-// tree sum of `count` points (count <= MSM_SEG_THREADS) into out
-__device__ __forceinline__ void msm_tree_sum(const Xyzz* in, uint32_t count, Xyzz* out) {
-  __shared__ Xyzz red[MSM_SEG_THREADS];
-  const uint32_t t = threadIdx.x;
-  red[t] = t < count ? in[t] : G1::identity();
-  __syncthreads();
-  for (uint32_t st = MSM_SEG_THREADS / 2; st > 0; st >>= 1) {
-    if (t < st) red[t] = G1::add(red[t], red[t + st]);
-    __syncthreads();
-  }
-  if (t == 0) *out = red[0];
-}
-constexpr uint32_t MSM_NPART = MSM_NSEG / MSM_SEG_THREADS;  // partial sums per window
-static_assert(MSM_NSEG % MSM_SEG_THREADS == 0 && MSM_NPART <= MSM_SEG_THREADS, "reduction shape");
-
-// workgroup (window, part): the tree sum of MSM_SEG_THREADS segment shares
-__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_reduce(const Xyzz* shares, Xyzz* parts) {
-  msm_tree_sum(shares + (uint64_t)blockIdx.x * MSM_SEG_THREADS, MSM_SEG_THREADS, parts + blockIdx.x);
-}
-// workgroup w: the window sum from its npart (<= MSM_SEG_THREADS) partial sums
-__global__ void __launch_bounds__(MSM_SEG_THREADS) msm_window_final(const Xyzz* parts, Xyzz* sums, uint32_t npart) {
-  msm_tree_sum(parts + (uint64_t)blockIdx.x * npart, npart, sums + blockIdx.x);
 }
 
 // ---------------------------------------------------------------- fixed-base MSM
@@ -339,20 +262,25 @@ __global__ void __launch_bounds__(256) msm_fx_digits(const uint64_t* scalars, co
   }
 }
 
-// Boundary join for large buckets (the fixed-base form: ~16 n / 2^15 entries per bucket, 512
-// at 2^20 points, so a bucket crossing chunks spans ~16 of them). Tree over each bucket's
+// Boundary join (fixed-base form: ~16 n / 2^15 entries per bucket, 512 at 2^20 points, so a
+// bucket crossing chunks spans ~12 of them; windowed form: ~2 chunks). Tree over each bucket's
 // continuation partials head[o+1 .. e] (o = chunk of the bucket's first entry, e = chunk of
 // its last): at step s, the continuation at o + 1 + 2 s j adds head[o + 1 + 2 s j + s] when
-// that is <= e. After ceil(log2(span)) steps head[o+1] holds their sum; msm_join_final adds
-// it to the owner's tail partial. One work item per (bucket, j) -- not per chunk, so the
+// that is <= e. After ceil(log2(span)) steps head[o+1] holds their sum; fx_bucket adds it
+// to the owner's tail partial. One work item per (bucket, j) -- not per chunk, so the
 // waves of a step hold only adding lanes (a per-chunk grid kept every wave busy at every
 // step for a shrinking share of active lanes).
 // the largest number of chunks a bucket spans (bounds the tree steps that do any work)
 __global__ void __launch_bounds__(256) msm_max_span(const uint32_t* start, const uint32_t* end, uint32_t nb,
                                                     uint32_t* span) {
+  // one global atomic per workgroup (2^19 buckets of the windowed form on one address: 93 us)
+  __shared__ uint32_t bmax;
+  if (threadIdx.x == 0) bmax = 0;
+  __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nb || end[k] <= start[k]) return;
-  atomicMax(span, (end[k] - 1) / MSM_CH - start[k] / MSM_CH);
+  if (k < nb && end[k] > start[k]) atomicMax(&bmax, (end[k] - 1) / MSM_CH - start[k] / MSM_CH);
+  __syncthreads();
+  if (threadIdx.x == 0 && bmax) atomicMax(span, bmax);
 }
 __global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint32_t* start, const uint32_t* end,
                                                      uint32_t nb, uint32_t step, const uint32_t* span) {
@@ -367,18 +295,9 @@ __global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint
     if (be <= bs) continue;
     const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
     const uint32_t u = o + 1 + 2 * step * j;
-    if (u + step <= e) head[u].acc = G1::add(head[u].acc, head[u + step].acc);
+    if (u + step <= e) head[u].acc = G1::add2(head[u].acc, head[u + step].acc);
   }
 }
-__global__ void __launch_bounds__(256) msm_join_final(const ChunkPart* head, const ChunkPart* tail, uint32_t nchunks,
-                                                      Xyzz* buckets, uint32_t sent) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nchunks) return;
-  const uint32_t k = tail[t].key;
-  if (k == sent) return;
-  buckets[k] = G1::add(tail[t].acc, head[t + 1].acc);  // a tail always has a continuation
-}
-
 // bucket bounds and the span counter of a fixed-base MSM, zeroed in one launch
 __global__ void __launch_bounds__(256) msm_fx_clear(uint32_t* start, uint32_t* end, uint32_t* span) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -400,19 +319,19 @@ __global__ void __launch_bounds__(256) msm_join_rest(ChunkPart* head, const uint
   const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH;
   if (e - o <= FX_JOIN_GROUP) return;
   Xyzz acc = head[o + 1].acc;
-  for (uint32_t u = o + 1 + FX_JOIN_GROUP; u <= e; u += FX_JOIN_GROUP) acc = G1::add(acc, head[u].acc);
+  for (uint32_t u = o + 1 + FX_JOIN_GROUP; u <= e; u += FX_JOIN_GROUP) acc = G1::add2(acc, head[u].acc);
   head[o + 1].acc = acc;
 }
 
 // Bucket b's full sum after the join: a bucket spanning chunks o < e is its chunk-o tail run
 // plus the joined continuations head[o + 1]; any other bucket was written whole (or is
-// empty: zero = identity). Fuses what msm_join_final wrote back.
+// empty: never read).
 __device__ __forceinline__ Xyzz fx_bucket(uint32_t k, const Xyzz* buckets, const ChunkPart* head,
                                           const ChunkPart* tail, const uint32_t* start, const uint32_t* end) {
   const uint32_t bs = start[k], be = end[k];
   if (be <= bs) return G1::identity();
   const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
-  return o < e ? G1::add(tail[o].acc, head[o + 1].acc) : buckets[k];
+  return o < e ? G1::add2(tail[o].acc, head[o + 1].acc) : buckets[k];
 }
 
 // Workgroup tree sum of one value per thread (blockDim.x a power of two <= 256) -> *out.
@@ -422,7 +341,7 @@ __device__ __forceinline__ void fx_tree(Xyzz v, Xyzz* out) {
   red[t] = v;
   __syncthreads();
   for (uint32_t st = blockDim.x / 2; st > 0; st >>= 1) {
-    if (t < st) red[t] = G1::add(red[t], red[t + st]);
+    if (t < st) red[t] = G1::add2(red[t], red[t + st]);
     __syncthreads();
   }
   if (t == 0) *out = red[0];
@@ -438,22 +357,53 @@ __device__ __forceinline__ void fx_tree(Xyzz v, Xyzz* out) {
 // segment running sums and their tree.
 constexpr uint32_t FX_NH = FX_NB / 256;  // 128 values of h
 static_assert(FX_NH == 128, "2^15 buckets = 128 x 256");
-// workgroup g < 128: C_g (256 buckets); g >= 128: D_(g-128) (128 buckets)
+// workgroup (g, w): window w's buckets start at w * 2^15 (keys (w << 15) | b); g < 128: C_g
+// (256 buckets), g >= 128: D_(g-128) (128 buckets); cd holds 384 sums per window
 __global__ void __launch_bounds__(256) msm_fx_cd(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
                                                  const uint32_t* start, const uint32_t* end, Xyzz* cd) {
-  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  const uint32_t g = blockIdx.x, t = threadIdx.x, base = blockIdx.y * FX_NB;
   Xyzz v;
   if (g < FX_NH)
-    v = fx_bucket(256 * g + t, buckets, head, tail, start, end);
+    v = fx_bucket(base + 256 * g + t, buckets, head, tail, start, end);
   else
-    v = t < FX_NH ? fx_bucket(256 * t + (g - FX_NH), buckets, head, tail, start, end) : G1::identity();
-  fx_tree(v, cd + g);
+    v = t < FX_NH ? fx_bucket(base + 256 * t + (g - FX_NH), buckets, head, tail, start, end) : G1::identity();
+  fx_tree(v, cd + (uint64_t)blockIdx.y * (FX_NH + 256) + g);
 }
-// workgroup s (128 threads): s < 8: 2^s Y_s; 8 <= s < 15: 2^s Z_(s-8); s = 15: S.
+// The same C_h / D_l sums for many windows at once (the windowed MSM: 16 x 384 trees), where
+// throughput matters more than depth: a 256-tree keeps on average a quarter of its lanes
+// busy, so each thread first adds 8 buckets in sequence. Workgroup (g, w), g < 16: C_h for
+// h = 8g .. 8g+7 (32 threads per h, 8 consecutive buckets each, then 32-lane trees);
+// g >= 16: D_l for l = 16(g-16) .. +15 (16 threads per l, 8 values of h each, then 16-lane
+// trees).
+__global__ void __launch_bounds__(256) msm_fx_cd_seq(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
+                                                     const uint32_t* start, const uint32_t* end, Xyzz* cd) {
+  __shared__ Xyzz red[256];
+  const uint32_t g = blockIdx.x, t = threadIdx.x, base = blockIdx.y * FX_NB;
+  Xyzz* out = cd + (uint64_t)blockIdx.y * (FX_NH + 256);
+  Xyzz acc = G1::identity();
+  uint32_t lanes;
+  if (g < 16) {
+    const uint32_t h = 8 * g + t / 32, l0 = (t % 32) * 8;
+    for (uint32_t i = 0; i < 8; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * h + l0 + i, buckets, head, tail, start, end));
+    lanes = 32;
+  } else {
+    const uint32_t l = 16 * (g - 16) + t / 16, h0 = (t % 16) * 8;
+    for (uint32_t i = 0; i < 8; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * (h0 + i) + l, buckets, head, tail, start, end));
+    lanes = 16;
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (uint32_t st = lanes / 2; st > 0; st >>= 1) {
+    if (t % lanes < st) red[t] = G1::add2(red[t], red[t + st]);
+    __syncthreads();
+  }
+  if (t % lanes == 0) out[g < 16 ? 8 * g + t / 32 : FX_NH + 16 * (g - 16) + t / 16] = red[t];
+}
+// workgroup (s, w) (128 threads): s < 8: 2^s Y_s; 8 <= s < 15: 2^s Z_(s-8); s = 15: S.
 __global__ void __launch_bounds__(128) msm_fx_subsets(const Xyzz* cd, Xyzz* sub) {
   const uint32_t s = blockIdx.x, t = threadIdx.x;
-  const Xyzz* C = cd;
-  const Xyzz* D = cd + FX_NH;
+  const Xyzz* C = cd + (uint64_t)blockIdx.y * (FX_NH + 256);
+  const Xyzz* D = C + FX_NH;
   Xyzz v;
   if (s < 8) {  // the t-th l with bit s set
     v = D[((t >> s) << (s + 1)) | (1u << s) | (t & ((1u << s) - 1))];
@@ -468,12 +418,14 @@ __global__ void __launch_bounds__(128) msm_fx_subsets(const Xyzz* cd, Xyzz* sub)
   if (t == 0) {
     Xyzz r = res;
     const uint32_t e = s < 15 ? s : 0;  // Y_s weight 2^s; Z_k weight 2^(k+8) = 2^s
-    for (uint32_t i = 0; i < e; ++i) r = G1::dbl(r);
-    sub[s] = r;
+    for (uint32_t i = 0; i < e; ++i) r = G1::dbl2(r);
+    sub[blockIdx.y * 16 + s] = r;
   }
 }
-// one workgroup of 16 threads: the sum of the 16 scaled subset sums
-__global__ void __launch_bounds__(16) msm_fx_total(const Xyzz* sub, Xyzz* out) { fx_tree(sub[threadIdx.x], out); }
+// workgroup w (16 threads): window w's sum of its 16 scaled subset sums
+__global__ void __launch_bounds__(16) msm_fx_total(const Xyzz* sub, Xyzz* out) {
+  fx_tree(sub[blockIdx.x * 16 + threadIdx.x], out + blockIdx.x);
+}
 
 // 64-bit fingerprint of n canonical affine points (8 u64 each): block XORs of a position-
 // mixed hash, then one block folds them (validates a cached table against the points)
@@ -583,7 +535,7 @@ static uint64_t grid1(uint64_t count) {
 
 struct MsmWork {
   DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &temp, &head, &tail,
-      &parts;
+      &parts, &span;
 };
 
 // scratch owned by the context (freed with it)
@@ -591,7 +543,7 @@ static MsmWork msm_work(pbf_ctx* ctx) {
   return MsmWork{ctx->buf("msm.pts"),     ctx->buf("msm.inf"),    ctx->buf("msm.keys"),   ctx->buf("msm.vals"),
                  ctx->buf("msm.keys2"),   ctx->buf("msm.vals2"),  ctx->buf("msm.start"),  ctx->buf("msm.end"),
                  ctx->buf("msm.buckets"), ctx->buf("msm.shares"), ctx->buf("msm.sums"),   ctx->buf("msm.temp"),
-                 ctx->buf("msm.head"),    ctx->buf("msm.tail"),   ctx->buf("msm.parts")};
+                 ctx->buf("msm.head"),    ctx->buf("msm.tail"),   ctx->buf("msm.parts"),  ctx->buf("msm.span")};
 }
 
 // Enqueue the device part; window sums land in w.sums (MSM_NW Xyzz, Montgomery).
@@ -606,8 +558,9 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
       (rc = w.vals.ensure(m * 4)) || (rc = w.keys2.ensure(m * 4)) || (rc = w.vals2.ensure(m * 4)) ||
       (rc = w.start.ensure((uint64_t)MSM_NW * MSM_NB * 4)) || (rc = w.end.ensure((uint64_t)MSM_NW * MSM_NB * 4)) ||
       (rc = w.buckets.ensure((uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz))) ||
-      (rc = w.shares.ensure((uint64_t)MSM_NW * MSM_NSEG * sizeof(Xyzz))) ||
-      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))) || (rc = w.parts.ensure(MSM_NW * MSM_NPART * sizeof(Xyzz))) ||
+      (rc = w.shares.ensure((uint64_t)MSM_NW * (FX_NH + 256) * sizeof(Xyzz))) ||
+      (rc = w.sums.ensure(MSM_NW * sizeof(Xyzz))) || (rc = w.parts.ensure(MSM_NW * 16 * sizeof(Xyzz))) ||
+      (rc = w.span.ensure(4)) ||
       (rc = w.head.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))) ||
       (rc = w.tail.ensure((m / MSM_CH + 1) * sizeof(ChunkPart))))
     return rc;
@@ -628,21 +581,31 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
                      (uint32_t*)w.start.p, (uint32_t*)w.end.p, MSM_SENTINEL);
   // the valid (non-sentinel) prefix of the sorted list: the sentinel sorts last; its
-  // length is known only on the device, so chunks past it return at once
-  PBF_HIP(hipMemsetAsync(w.buckets.p, 0, (uint64_t)MSM_NW * MSM_NB * sizeof(Xyzz), s));
+  // length is known only on the device, so chunks past it return at once. No bucket memset:
+  // the reduction reads only the buckets the accumulation wrote (fx_bucket).
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
+  PBF_HIP(hipMemsetAsync(w.span.p, 0, 4, s));
   hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
                      (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
                      (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr);
-  hipLaunchKernelGGL(msm_chunk_join, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const ChunkPart*)w.head.p,
-                     (const ChunkPart*)w.tail.p, (const uint32_t*)w.end.p, nchunks, (Xyzz*)w.buckets.p, MSM_SENTINEL);
-  hipLaunchKernelGGL(msm_segments<MSM_NB>, dim3((MSM_NW * MSM_NSEG + 255) / 256), dim3(256), 0, s,
-                     (const Xyzz*)w.buckets.p, (Xyzz*)w.shares.p, (uint32_t)MSM_NW);
-  hipLaunchKernelGGL(msm_window_reduce, dim3(MSM_NW * MSM_NPART), dim3(MSM_SEG_THREADS), 0, s,
-                     (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
-  hipLaunchKernelGGL(msm_window_final, dim3(MSM_NW), dim3(MSM_SEG_THREADS), 0, s, (const Xyzz*)w.parts.p,
-                     (Xyzz*)w.sums.p, MSM_NPART);
+  // the same tail as the fixed-base form, over 16 windows of 2^15 buckets (bucket id = key)
+  constexpr uint32_t NBT = MSM_NW * MSM_NB;
+  hipLaunchKernelGGL(msm_max_span, dim3(NBT / 256), dim3(256), 0, s, (const uint32_t*)w.start.p,
+                     (const uint32_t*)w.end.p, NBT, (uint32_t*)w.span.p);
+  const uint64_t mean_span = m / ((uint64_t)NBT * MSM_CH) + 2;
+  for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
+    const uint64_t items = (uint64_t)NBT * ((mean_span + 2 * step - 1) / (2 * step));
+    hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, s, (ChunkPart*)w.head.p,
+                       (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, step, (const uint32_t*)w.span.p);
+  }
+  hipLaunchKernelGGL(msm_join_rest, dim3(NBT / 256), dim3(256), 0, s, (ChunkPart*)w.head.p,
+                     (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, (const uint32_t*)w.span.p);
+  hipLaunchKernelGGL(msm_fx_cd_seq, dim3(16 + 16, MSM_NW), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
+                     (const ChunkPart*)w.head.p, (const ChunkPart*)w.tail.p, (const uint32_t*)w.start.p,
+                     (const uint32_t*)w.end.p, (Xyzz*)w.shares.p);
+  hipLaunchKernelGGL(msm_fx_subsets, dim3(16, MSM_NW), dim3(128), 0, s, (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
+  hipLaunchKernelGGL(msm_fx_total, dim3(MSM_NW), dim3(16), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
   PBF_HIP(hipGetLastError());
   return 0;
 }
