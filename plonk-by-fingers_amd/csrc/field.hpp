@@ -55,6 +55,22 @@ __device__ __forceinline__ uint32_t gl_selk(uint32_t a, uint64_t m) {  // m ? K 
   asm("v_cndmask_b32_e64 %0, %1, %3, %2" : "=v"(r) : "v"(a), "s"(m), "i"(K));
   return r;
 }
+// a - b (mod p), canonical, for canonical a, b: 4 VALU. d = a - b over a 32-bit borrow chain;
+// a borrow means d + p = d - EPS = d - 2^32 + 1 (d > EPS then), applied as lo + 1 (carry c)
+// and hi - (borrow & !c): the correction's carries ride in SGPR masks (one SALU andn2)
+// instead of a selected 64-bit addend (two v_cndmask + a 64-bit add).
+__device__ __forceinline__ uint64_t gl_sub_chain(uint64_t a, uint64_t b) {
+  uint64_t bo, c;
+  uint32_t lo, hi, lo2, hi2;
+  asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(lo), "=s"(bo) : "v"((uint32_t)a), "v"((uint32_t)b));
+  asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4"
+      : "=v"(hi), "=s"(bo)
+      : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32)), "s"(bo));
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(lo2), "=s"(c) : "v"(lo), "s"(bo));
+  const uint64_t m = bo & ~c;
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(hi2), "=s"(c) : "v"(hi), "s"(m));
+  return ((uint64_t)hi2 << 32) | lo2;
+}
 // lo + h*(2^32-1) (mod p), canonical; lo < 2^64, h < 2^32. With the carry c of the 64-bit
 // sum r, the value is r + c*EPS: c = 1 leaves r < 2^64 - 2^33, so r + EPS is canonical;
 // c = 0 and r >= p gives r - p = r + EPS (mod 2^64). 6 VALU.
@@ -77,9 +93,17 @@ __device__ __forceinline__ uint64_t gl_red96(uint64_t lo, uint32_t h0, uint32_t 
   const uint64_t r = ((uint64_t)r1 << 32) | r0;
   const uint64_t plus = (m.c & ~c2) | (gl_ge_p(r) & ~(m.c ^ c2));
   const uint64_t minus = c2 & ~m.c;
-  const uint32_t a0 = gl_selk<1u>(gl_selk<0xFFFFFFFFu>(0u, plus), minus);
-  const uint32_t a1 = gl_selk<0xFFFFFFFFu>(0u, minus);
-  return r + (((uint64_t)a1 << 32) | a0);
+  // +EPS = lo - 1, hi + 1 - borrow; -EPS = lo + 1, hi - 1 + carry (plus, minus exclusive):
+  // four carry-chain VALU, the lane masks combined on the SALU (a selected 64-bit addend
+  // took three v_cndmask, a v_mov and two 64-bit adds as compiled)
+  uint64_t c3, c4, c5;
+  uint32_t l1, l2, u1, u2;
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(l1), "=s"(c3) : "v"(r0), "s"(plus));
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(l2), "=s"(c4) : "v"(l1), "s"(minus));
+  const uint64_t up = plus & ~c3, dn = minus & ~c4;
+  asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(u1), "=s"(c5) : "v"(r1), "s"(up));
+  asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(u2), "=s"(c5) : "v"(u1), "s"(dn));
+  return ((uint64_t)u2 << 32) | l2;
 }
 #endif
 
@@ -98,13 +122,7 @@ struct Goldilocks {
   }
   __host__ __device__ __forceinline__ static uint64_t sub(uint64_t a, uint64_t b, const FieldArgs&) {
 #ifdef __HIP_DEVICE_COMPILE__
-    // 32-bit borrow chain: the borrow comes straight out of v_subb_co_u32 (the 64-bit
-    // __builtin_sub_overflow form re-derived it with a v_cmp_gt_u64: one VALU more)
-    unsigned c1, c2;
-    const unsigned lo = __builtin_subc((unsigned)a, (unsigned)b, 0u, &c1);
-    const unsigned hi = __builtin_subc((unsigned)(a >> 32), (unsigned)(b >> 32), c1, &c2);
-    const uint64_t d = ((uint64_t)hi << 32) | lo;
-    return d - (c2 ? EPS : 0);  // d + p (mod 2^64); d > EPS when borrowing
+    return gl_sub_chain(a, b);
 #else
     uint64_t d;
     const bool borrow = __builtin_sub_overflow(a, b, &d);

@@ -157,8 +157,22 @@ K64(k_lshr64, J_LSHR64)
 #define I_DPP(r) "v_mov_b32_dpp " r ", %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
 #define I_PL32(r) "v_permlane32_swap_b32 " r ", %8\n"
 #define I_SUBCO(r) "v_sub_co_u32 " r ", vcc, " r ", %8\n"
+#define I_LSHLOR(r) "v_lshl_or_b32 " r ", " r ", 3, %8\n"
+#define I_ANDOR(r) "v_and_or_b32 " r ", " r ", %8, " r "\n"
+#define I_BFI(r) "v_bfi_b32 " r ", " r ", %8, " r "\n"
+#define I_ADDI(r) "v_add_i32 " r ", " r ", %8\n"
+#define I_ASHRV(r) "v_ashrrev_i32 " r ", %8, " r "\n"
+#define I_PKADDU16(r) "v_pk_add_u16 " r ", " r ", %8\n"
+#define I_BFEI(r) "v_bfe_i32 " r ", " r ", 3, 7\n"
 K(k_dpp, I_DPP)
 K(k_subco, I_SUBCO)
+K(k_lshlor, I_LSHLOR)
+K(k_andor, I_ANDOR)
+K(k_bfi, I_BFI)
+K(k_addi, I_ADDI)
+K(k_ashrv, I_ASHRV)
+K(k_pkaddu16, I_PKADDU16)
+K(k_bfei, I_BFEI)
 
 typedef void (*kfn)(uint32_t*, uint32_t);
 int main() {
@@ -173,7 +187,7 @@ int main() {
       {"v_lshrrev_b32", k_lshr}, {"v_lshlrev_b32 vreg", k_lshlv}, {"v_ashrrev_i32", k_ashr}, {"v_add_co_u32_e64 sdst", k_addco3},
       {"v_mul_u32_u24", k_mulu24}, {"v_fma_f32", k_fmaf}, {"v_mul_f32", k_mulf}, {"v_subrev_u32", k_subrev},
       {"v_lshl_add_u64", k_lshl_add64}, {"v_mad_u64_u32", k_mad64}, {"v_cmp_lt_u64", k_cmp64},
-      {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mov_b32", k_pk_mov}, {"v_mad_i64_i32", k_madi64}, {"v_ashrrev_i64", k_ashr64}, {"v_lshrrev_b64", k_lshr64}, {"v_mov_b32_dpp", k_dpp}, {"v_sub_co_u32", k_subco},
+      {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mov_b32", k_pk_mov}, {"v_mad_i64_i32", k_madi64}, {"v_ashrrev_i64", k_ashr64}, {"v_lshrrev_b64", k_lshr64}, {"v_mov_b32_dpp", k_dpp}, {"v_sub_co_u32", k_subco}, {"v_lshl_or_b32", k_lshlor}, {"v_and_or_b32", k_andor}, {"v_bfi_b32", k_bfi}, {"v_add_i32", k_addi}, {"v_ashrrev_i32 vreg", k_ashrv}, {"v_pk_add_u16", k_pkaddu16}, {"v_bfe_i32", k_bfei},
   };
   const int blocks = 256 * 8 * 4;  // 8 workgroups of 256 threads per CU resident = 8 waves/SIMD, x4 rounds
   uint32_t* out;

@@ -150,6 +150,12 @@ def test_fixed_base_comb_matches_double_and_add(ctx, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert a[:8].tolist() == [0] * 8  # 0 * G = identity
+    # parity anchor: the edge scalars and a sample re-derived by the oracle's double-and-add
+    al = a.cpu().numpy().view(np.uint64)
+    ti = bn254.limbs_to_ints(t)
+    for i in [0, 1, 2, 3, 1000, n - 1]:  # 0, the 0xff/0x00 byte patterns, r - 1, samples
+        want = bn254.g1_mul(bn254.G1_GEN, ti[i] % R)
+        assert tuple(bn254.limbs_to_ints(al[8 * i: 8 * i + 8])) == enc(want), i
 
 
 def _dev_points(pts):

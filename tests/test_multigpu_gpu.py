@@ -124,7 +124,11 @@ def test_sharded_msm_ranges_gpu(ctx, G):
         a, b = ShardedMsm.split(n, G, r)
         parts.append(ops.partial(dp[8 * a:].data_ptr(), ds[4 * a:].data_ptr(), b - a))
     full = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n, stream=st)
-    assert ops.combine(parts) == full
+    got = ops.combine(parts)
+    assert got == full
+    # parity anchor: P_i = t_i G, so the MSM is (sum_i s_i t_i mod r) G, computed by the oracle
+    z = sum(a * b for a, b in zip(bn254.limbs_to_ints(s), bn254.limbs_to_ints(t))) % bn254.R
+    assert got == (bn254.g1_mul(bn254.G1_GEN, z) if z else (0, 0))
 
 
 def _fr_rand(count, seed):

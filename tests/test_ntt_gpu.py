@@ -64,6 +64,28 @@ def test_ntt_vs_oracle_multi_pass(ctx, m, logn):
     assert np.array_equal(ctx.ntt(m, w, ref, inverse=True), oracle.ntt_iter(m, w, ref, inverse=True))
 
 
+EDGE_GL = [0, 1, 2, GOLD - 1, GOLD - 2, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, 1 << 63, (1 << 63) - 1,
+           GOLD - (1 << 32), GOLD - (1 << 32) + 1, (1 << 64) - (1 << 33), 0xFFFFFFFE00000001, 0x00000000FFFFFFFF,
+           0x7FFFFFFF80000000]
+
+
+@pytest.mark.parametrize("logn", [10, 14, 16, 20])
+def test_ntt_edge_values(ctx, logn):
+    """Inputs drawn only from carry/borrow edge values of the Goldilocks add, sub and
+    reduction (0, 1, p-1, 2^32 +- 1, 2^63, p - 2^32, ...), so the first butterfly levels see
+    every edge pair (e.g. 0 - 1: a borrow with a low word of 2^32 - 1): bit-exact vs the oracle
+    both ways."""
+    n = 1 << logn
+    w = root(GOLD, n)
+    rng = np.random.default_rng(logn)
+    a = np.array(EDGE_GL, dtype=np.uint64)[rng.integers(0, len(EDGE_GL), n)]
+    ref = oracle.ntt_iter(GOLD, w, a)
+    got = ctx.ntt(GOLD, w, a)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(ctx.ntt(GOLD, w, a, inverse=True), oracle.ntt_iter(GOLD, w, a, inverse=True))
+    assert np.array_equal(ctx.ntt(GOLD, w, got, inverse=True), a)
+
+
 def test_ntt_recursion_faithful_2p14(ctx):
     # the exact algorithm of fft.rs:90-106 (allocation-faithful restatement) at 2^14
     n = 1 << 14
