@@ -71,6 +71,10 @@ struct NttPlan {
   std::vector<std::shared_ptr<DevBuf>> rtab;  // per pass
   bool gl = false;         // passes run on ntt_gl_pass_kernel (standard Goldilocks roots)
   std::vector<std::shared_ptr<DevBuf>> tc;    // per pass: stage-C tables of ntt_gl_pass_kernel
+  // last pass without a full [r][k] table: w^(r k) = B[kb][r] * A[r][w] for k = kb*W + w
+  // (A: R x W, B: Ns/W x R; null when unused), W = tws_w columns per tile
+  std::shared_ptr<DevBuf> tws_a, tws_b;
+  int tws_w = 0;
 };
 
 // Extra streams and events of the multi-stream NTT group schedule (ntt_launch.hip

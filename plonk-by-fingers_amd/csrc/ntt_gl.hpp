@@ -55,6 +55,8 @@ struct GlPassArgs {
   const uint64_t* tw0;     // two-level table of w (low part)
   const uint64_t* tw1;     //                     (high part)
   const uint64_t* tc;      // stage-C table [r2][k1] = w_R^(r2*k1) (times n^-1 when scaled)
+  const uint64_t* tws_a;   // last pass, split twiddles: A[r][w] = w_p^(r*w)   (or null)
+  const uint64_t* tws_b;   //                          B[kb][r] = w_p^(r*kb*W)
   uint64_t n;
   uint32_t log_n;
   uint32_t log_ns;
@@ -232,6 +234,8 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
           const uint64_t r = (uint64_t)(16 * C * s1 + C * s2 + r2);
           if (a.twpass) {
             tw[uu * 4 + s1] = a.twpass[(r << a.log_ns) + k];
+          } else if (a.tws_a) {  // last pass: k = kb*W + w
+            tw[uu * 4 + s1] = G::mul(a.tws_b[(uint64_t)kb * Sh::R + r], a.tws_a[r * W + w], f);
           } else {
             const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
             tw[uu * 4 + s1] = G::mul(a.tw0[e & ((1ull << a.tw_bits) - 1)], a.tw1[e >> a.tw_bits], f);

@@ -77,6 +77,8 @@ static std::vector<int> default_passes(uint32_t log_n) {
 }
 
 
+static int gl_tile(int logr);
+
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   if (!field_for(m, &p->kind, &p->fa)) return fail(5, "unsupported modulus");
   if (n == 0 || (n & (n - 1))) return fail(1, "n must be a power of two");
@@ -126,14 +128,19 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   int rc = upload(p->tw0, t0);
   if (!rc) rc = upload(p->tw1, t1);
   if (rc) return rc;
-  // per-pass [r][k] twiddle tables while R*Ns <= 2^22 (shared by every polynomial of a
-  // batch, so they stay in the Infinity Cache); larger passes use the two-level table
+  // per-pass [r][k] twiddle tables while R*Ns <= 2^PBF_NTT_TWMAX_LOG (default 24: the last
+  // pass of a 2^24 transform reads a 128 MiB table, shared by every polynomial of a batch,
+  // in 128-B runs like its data; the two-level table's two random gathers per element were
+  // bound by the texture unit: 2^24 x 2 0.545 -> 0.490 ms); larger passes
+  // use the two-level table
   {
     uint64_t ns = 1;
+    const char* tm = getenv("PBF_NTT_TWMAX_LOG");
+    const int twmax = tm ? atoi(tm) : 24;
     for (size_t i = 0; i < p->logr.size(); ++i) {
       const uint64_t R = 1ull << p->logr[i];
       auto b = std::make_shared<DevBuf>();
-      if (ns > 1 && R * ns <= (1ull << 22) && !getenv("PBF_NTT_TWO_LEVEL")) {
+      if (ns > 1 && R * ns <= (1ull << twmax) && !getenv("PBF_NTT_TWO_LEVEL")) {
         const uint64_t step = n / (ns * R);
         std::vector<uint64_t> t(R * ns);
         for (uint64_t r = 0; r < R; ++r) {
@@ -145,6 +152,32 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
         if (rc1) return rc1;
       }
       p->twpass.push_back(b);
+      // the last pass of a standard-root plan whose [r][k] table is not built: split table
+      // (A/B: PBF_NTT_TWSPLIT=1 also replaces a built one)
+      const bool last = i + 1 == p->logr.size();
+      const bool split = getenv("PBF_NTT_TWSPLIT") != nullptr;
+      if (last && ns > 1 && p->e64 >= 0 && !getenv("PBF_NTT_NO_TWSPLIT") && p->logr[i] >= 6 && p->logr[i] <= 10 && (!b->p || split)) {
+        const uint64_t W = (uint64_t)gl_tile(p->logr[i]) >> p->logr[i];
+        if (ns % W == 0) {
+          if (split) p->twpass.back() = std::make_shared<DevBuf>();
+          const uint64_t wp = hpow(w, n / (ns * R), m);
+          std::vector<uint64_t> ta(R * W), tb((ns / W) * R);
+          for (uint64_t r = 0; r < R; ++r) {
+            const uint64_t wr = hpow(wp, r, m);
+            uint64_t z = 1 % m;
+            for (uint64_t c = 0; c < W; ++c) { ta[r * W + c] = z; z = hmul(z, wr, m); }
+            const uint64_t wrw = hpow(wr, W, m);  // (w_p^r)^(kb W)
+            z = 1 % m;
+            for (uint64_t kb = 0; kb < ns / W; ++kb) { tb[kb * R + r] = z; z = hmul(z, wrw, m); }
+          }
+          p->tws_a = std::make_shared<DevBuf>();
+          p->tws_b = std::make_shared<DevBuf>();
+          int rc2 = upload(*p->tws_a, ta);
+          if (!rc2) rc2 = upload(*p->tws_b, tb);
+          if (rc2) return rc2;
+          p->tws_w = (int)W;
+        }
+      }
       ns *= R;
     }
   }
@@ -510,6 +543,9 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;
     a.tc = (const uint64_t*)p.tc[i]->p;
+    const bool tws = !a.twpass && i == P - 1 && p.tws_a && (uint64_t)p.tws_w == W && !blk;
+    a.tws_a = tws ? (const uint64_t*)p.tws_a->p : nullptr;
+    a.tws_b = tws ? (const uint64_t*)p.tws_b->p : nullptr;
     a.n = p.n;
     a.log_n = p.log_n;
     a.log_ns = log_ns;

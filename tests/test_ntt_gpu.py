@@ -186,6 +186,27 @@ def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     assert np.array_equal(d_out.cpu().numpy().view(np.uint64), host)
 
 
+@pytest.mark.parametrize("env", [{"PBF_NTT_TWMAX_LOG": "18"}, {"PBF_NTT_TWSPLIT": "1"},
+                                 {"PBF_NTT_TWMAX_LOG": "18", "PBF_NTT_NO_TWSPLIT": "1"}])
+def test_twiddle_table_paths(monkeypatch, vectors, env):
+    """The three sources of the pass twiddle w^(r k): the per-pass [r][k] table (default up to
+    2^PBF_NTT_TWMAX_LOG = 2^24 entries), the last pass's split table B[kb][r] * A[r][w]
+    (default beyond; forced by PBF_NTT_TWSPLIT) and the two-level table (PBF_NTT_NO_TWSPLIT).
+    A fresh context (plans read the knobs when they are built) must reproduce the 2^16, 2^20
+    and 2^24 golden digests and round-trip."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c2 = pbf.Context(0)
+    try:
+        for c in vectors["large"]:
+            a = oracle.splitmix_field(c["modulus"], c["seed"], c["n"])
+            fwd = c2.ntt(c["modulus"], c["omega"], a)
+            assert sha(fwd) == c["sha256_fwd"], c["n"]
+            assert np.array_equal(c2.ntt(c["modulus"], c["omega"], fwd, inverse=True), a)
+    finally:
+        c2.close()
+
+
 def test_fill_random_matches_host_generator(ctx):
     import torch
 
