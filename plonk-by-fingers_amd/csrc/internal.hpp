@@ -167,5 +167,8 @@ struct pbf_ctx {
   }
   // pairing check: the G2 inputs whose prepared lines sit in buf("pc.lines") (pairing.hip)
   std::vector<uint64_t> pair_g2_key;
+  // prover proving key: the preprocessed polynomials' coefficients and coset evaluations
+  // in buf("pk.coef") / buf("pk.coset"), valid for this key (n, fingerprints, k1 k2)
+  std::vector<uint64_t> pk_key;
   pbf::MsmTail msm_tail;  // destroyed before `named`: its stream drains first
 };

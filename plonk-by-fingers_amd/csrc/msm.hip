@@ -627,17 +627,20 @@ static void msm_finish_host(const Xyzz* sums, uint64_t* out) {
 // ---- fixed-base tables: cached per context, validated by a fingerprint of the points
 constexpr uint32_t FP_BLOCKS = 1024;
 
-static int msm_fingerprint_host(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, uint64_t* out) {
+int fingerprint_words(pbf_ctx* ctx, const uint64_t* d_words, uint64_t words, hipStream_t s, uint64_t* out) {
   DevBuf& fp = ctx->buf("msm.fp");
   int rc = fp.ensure((FP_BLOCKS + 1) * 8);
   if (rc) return rc;
   uint64_t* part = (uint64_t*)fp.p;
-  hipLaunchKernelGGL(msm_fingerprint, dim3(FP_BLOCKS), dim3(256), 0, s, d_pts, 8 * n, part);
+  hipLaunchKernelGGL(msm_fingerprint, dim3(FP_BLOCKS), dim3(256), 0, s, d_words, words, part);
   hipLaunchKernelGGL(msm_fingerprint_fold, dim3(1), dim3(256), 0, s, (const uint64_t*)part, FP_BLOCKS, part + FP_BLOCKS);
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipMemcpyAsync(out, part + FP_BLOCKS, 8, hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
   return 0;
+}
+static int msm_fingerprint_host(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, uint64_t* out) {
+  return fingerprint_words(ctx, d_pts, 8 * n, s, out);
 }
 
 // the window table of the n points at d_pts (built on first use; rebuilt when the points at

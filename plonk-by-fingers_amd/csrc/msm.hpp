@@ -18,6 +18,9 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
 // Orders stream s after every fixed-base MSM tail enqueued on this context so far (call
 // before reading a d_result of msm_fixed_device on s).
 int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s);
+// 64-bit fingerprint of `words` u64 at d_words (position-mixed XOR hash; one stream sync):
+// validates context caches against their inputs
+int fingerprint_words(pbf_ctx* ctx, const uint64_t* d_words, uint64_t words, hipStream_t s, uint64_t* out);
 // canonical affine (x, y as 4 + 4 little-endian u64; identity (0, 0)) of an XYZZ point
 void xyzz_to_affine_u64(const Xyzz& p, uint64_t* out);
 

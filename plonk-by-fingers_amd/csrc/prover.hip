@@ -801,10 +801,37 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
 
   ProverBufs B(ctx);  // context-owned scratch (one ctx per host thread, pbf.h)
   const uint64_t E = 32;           // bytes per element
+  const uint64_t CS = n + 8;       // coefficient slot (room for blinding terms up to x^(n+2))
   int rc;
+  // ---- proving key (one GPU): q_l q_r q_o q_m q_c s1 s2 s3 and l1 depend only on the circuit
+  // (d_q, d_copies, k1, k2) and n. Their coefficients (8 slots) and coset evaluations (9
+  // slots) are kept in the context and reused while the circuit is the same -- what a
+  // PLONK proving key holds -- validated by fingerprints of d_q and d_copies on every call.
+  // PBF_PROVER_NO_PK=1 recomputes them per proof, as the reference does (plonk.rs:233-243,
+  // 339-370).
+  const bool pk_on = P.G == 1 && !getenv("PBF_PROVER_NO_PK");
+  bool pk_hit = false;
+  uint64_t* pkcoef = nullptr;
+  uint64_t* pkcoset = nullptr;
+  std::vector<uint64_t> pk_key;
+  if (pk_on) {
+    uint64_t fq = 0, fc = 0;
+    if ((rc = fingerprint_words(ctx, d_q, 20 * (uint64_t)n, s, &fq)) ||
+        (rc = fingerprint_words(ctx, d_copies, 6 * (uint64_t)n, s, &fc)))
+      return rc;
+    pk_key = {(uint64_t)n, fq, fc};
+    for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
+    DevBuf& kc = ctx->buf("pk.coef");
+    DevBuf& ks = ctx->buf("pk.coset");
+    if ((rc = kc.ensure(8 * CS * E)) || (rc = ks.ensure(9 * N * E))) return rc;
+    pkcoef = (uint64_t*)kc.p;
+    pkcoset = (uint64_t*)ks.p;
+    pk_hit = ctx->pk_key == pk_key;
+    if (!pk_hit) ctx->pk_key.clear();  // the slots are rewritten below; valid again once complete
+  }
   if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure(3 * n * E)) || (rc = B.coef.ensure(11 * (n + 8) * E)) ||
       (rc = B.acc.ensure((n + 8) * E)) || (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure(n * E)) ||
-      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure(14 * P.count() * E)) ||
+      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure((pk_on ? 4 : 14) * P.count() * E)) ||
       (rc = B.t.ensure(N * E)) || (rc = B.work.ensure(3 * N * E)) || (rc = B.flag.ensure(64)) ||
       (rc = B.evals.ensure(16 * E)))
     return rc;
@@ -819,13 +846,17 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   }
   uint64_t* hpow = (uint64_t*)B.hpow.p;
   uint64_t* sigma = (uint64_t*)B.sigma.p;
-  const uint64_t CS = n + 8;  // coefficient slot (room for blinding terms up to x^(n+2))
   uint64_t* coef = (uint64_t*)B.coef.p;
-  auto C = [&](int k) { return coef + 4 * CS * k; };
-  // slots: 0 a, 1 b, 2 c, 3 q_l, 4 q_r, 5 q_o, 6 q_m, 7 q_c, 8 s1, 9 s2, 10 s3
+  // slots: 0 a, 1 b, 2 c, 3 q_l, 4 q_r, 5 q_o, 6 q_m, 7 q_c, 8 s1, 9 s2, 10 s3 (3.. in the proving key)
+  uint64_t* cslot[11];
+  for (int k = 0; k < 11; ++k) cslot[k] = (pk_on && k >= 3) ? pkcoef + 4 * CS * (k - 3) : coef + 4 * CS * k;
+  auto C = [&](int k) { return cslot[k]; };
   uint64_t* coset = (uint64_t*)B.coset.p;
   const uint64_t NE = P.count();  // coset evaluations held here (N; nl = N / G when sharded)
-  auto CE = [&](int k) { return coset + 4 * NE * k; };
+  uint64_t* ceslot[14];
+  for (int k = 0; k < 14; ++k)
+    ceslot[k] = (pk_on && k >= 4 && k <= 12) ? pkcoset + 4 * NE * (k - 4) : coset + 4 * NE * k;
+  auto CE = [&](int k) { return ceslot[k]; };
   // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1 [13 z(w x), sharded]
   uint64_t* work = (uint64_t*)B.work.p;
   uint64_t* W0 = work;
@@ -845,16 +876,19 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
                      k1, k2, sigma, P.d_bad);
   PBF_HIP(hipGetLastError());
   // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
-  PBF_HIP(hipMemsetAsync(coef, 0, 11 * CS * E, s));
+  PBF_HIP(hipMemsetAsync(coef, 0, (pk_on ? 3 : 11) * CS * E, s));
+  if (pk_on && !pk_hit) PBF_HIP(hipMemsetAsync(pkcoef, 0, 8 * CS * E, s));
   for (int k = 0; k < 3; ++k)
     PBF_HIP(hipMemcpyAsync(C(k), d_abc + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
-  for (int k = 0; k < 5; ++k)
-    PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
-  for (int k = 0; k < 3; ++k)
-    PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
-  for (int k = 0; k < 11; ++k)
+  if (!pk_hit) {
+    for (int k = 0; k < 5; ++k)
+      PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < 3; ++k)
+      PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+  }
+  for (int k = 0; k < (pk_hit ? 3 : 11); ++k)
     if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
-  P.mark("interpolate (11 INTT)");
+  P.mark(pk_hit ? "interpolate (3 INTT, key)" : "interpolate (11 INTT)");
   // ---- round 1: a(x) = (b2 + b1 x)(x^n - 1) + f_a(x), likewise b, c (plonk.rs:250-252)
   for (int k = 0; k < 3; ++k) {
     const U256 lo = bl[2 * k + 1], hi = bl[2 * k];  // (b2, b1), (b4, b3), (b6, b5)
@@ -935,9 +969,17 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     // sharded: z(w x) gets its own slot (coefficients z_j w^j) instead of reading z at index i+4,
     // which may sit in another rank's block
     srcs[13] = zx; lens[13] = n + 3; bases[13] = Fr::mul(P.g, P.omega);
-    if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0)))) return rc;
+    if (pk_on) {  // a b c z per proof; the 9 circuit slots once per proving key
+      if ((rc = P.coset_ntt_batch(4, srcs, lens, bases, CE(0)))) return rc;
+      if (!pk_hit) {
+        if ((rc = P.coset_ntt_batch(9, srcs + 4, lens + 4, bases + 4, CE(4)))) return rc;
+        ctx->pk_key = pk_key;
+      }
+    } else if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0)))) {
+      return rc;
+    }
   }
-  P.mark("round 3 coset NTTs (13)");
+  P.mark(pk_hit ? "round 3 coset NTTs (4, key)" : "round 3 coset NTTs (13)");
   QuotArgs qa;
   qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
   qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);

@@ -112,3 +112,35 @@ def test_challenge_on_the_evaluation_coset(ctx):
         pts, fs = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=1)
         assert fs == [x % P.R for x in want_f]
         assert [list(p) if p else None for p in pts] == [list(p) if p else None for p in want_pts]
+
+
+def test_proving_key_cache_matches_cold_proofs(monkeypatch):
+    """The context keeps the preprocessed polynomials (q_*, s_sigma_*, l1: coefficients and
+    coset evaluations) per circuit, checked by fingerprints of the gates and copies on every
+    call. Proofs over interleaved circuits and sizes (A A B A C A) on one context equal the
+    proofs of the same inputs with every preprocessing step recomputed (PBF_PROVER_NO_PK)."""
+    import pbf
+
+    rng = random.Random(4242)
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    circ = {"A": (64, 11), "B": (64, 12), "C": (128, 11)}
+    order = ["A", "A", "B", "A", "C", "A"]
+    warm = pbf.Context(0)
+    try:
+        srs = warm.srs_create(77, 2 * 128 + 2)
+        got = []
+        for name in order:
+            n, seed = circ[name]
+            got.append(warm.plonk_prove_bn254(*P.mul_gates_circuit(n, seed), chal, rnd, srs, mode=1))
+    finally:
+        warm.close()
+    monkeypatch.setenv("PBF_PROVER_NO_PK", "1")
+    cold = pbf.Context(0)
+    try:
+        srs = cold.srs_create(77, 2 * 128 + 2)
+        ref = {name: cold.plonk_prove_bn254(*P.mul_gates_circuit(*circ[name]), chal, rnd, srs, mode=1) for name in circ}
+    finally:
+        cold.close()
+    assert got == [ref[name] for name in order]
+    assert ref["A"] != ref["B"]
