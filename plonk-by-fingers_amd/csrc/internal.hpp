@@ -170,5 +170,8 @@ struct pbf_ctx {
   // prover proving key: the preprocessed polynomials' coefficients and coset evaluations
   // in buf("pk.coef") / buf("pk.coset"), valid for this key (n, fingerprints, k1 k2)
   std::vector<uint64_t> pk_key;
+  // verifier verification key: the 8 preprocessed commitments (vk_pts, 8 x 8 u64) of the
+  // circuit and SRS in vk_key (n, fingerprints of q, copies and the SRS, k1 k2)
+  std::vector<uint64_t> vk_key, vk_pts;
   pbf::MsmTail msm_tail;  // destroyed before `named`: its stream drains first
 };

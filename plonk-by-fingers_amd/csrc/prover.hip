@@ -1247,14 +1247,31 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
     if (!h_on_curve(proof_pts + 8 * i)) return 0;
   for (int i = 0; i < 7; ++i)
     if (Fr::geq_p(u256_from_u64(proof_f + 4 * i))) return 0;
-  // preprocessing (plonk.rs:507-517): commitments of q_m q_l q_r q_o q_c, s_sigma_1..3
+  // preprocessing (plonk.rs:507-517): commitments of q_m q_l q_r q_o q_c, s_sigma_1..3 -- a
+  // verification key: kept in the context for this circuit and SRS (fingerprints checked on
+  // every call; PBF_VERIFIER_NO_VK=1 recomputes them, as the reference does)
+  const U256 omega = hroot(log_n), one = fr_one_m();
+  const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
+  uint64_t pre[8][8];
+  std::vector<uint64_t> vk_key;
+  const bool vk_on = !getenv("PBF_VERIFIER_NO_VK");
+  if (vk_on) {
+    uint64_t fq = 0, fc = 0, fs = 0;
+    if ((rc = fingerprint_words(ctx, d_q, 20 * (uint64_t)n, s, &fq)) ||
+        (rc = fingerprint_words(ctx, d_copies, 6 * (uint64_t)n, s, &fc)) ||
+        (rc = fingerprint_words(ctx, d_srs, 8 * (uint64_t)srs_m, s, &fs)))
+      return rc;
+    vk_key = {(uint64_t)n, fq, fc, fs, (uint64_t)srs_m};
+    for (int i = 0; i < 8; ++i) vk_key.push_back(k1k2[i]);
+  }
+  if (vk_on && ctx->vk_key == vk_key && ctx->vk_pts.size() == 64) {
+    memcpy(pre, ctx->vk_pts.data(), sizeof(pre));
+  } else {
   DevBuf &hp = ctx->buf("vf.hpow"), &sg = ctx->buf("vf.sigma"), &cf = ctx->buf("vf.coef"), &fl = ctx->buf("vf.flag");
   if ((rc = hp.ensure(n * E)) || (rc = sg.ensure(3 * n * E)) || (rc = cf.ensure(8 * n * E)) || (rc = fl.ensure(64)))
     return rc;
-  const U256 omega = hroot(log_n), one = fr_one_m();
   uint64_t w_plain[4];
   hout(w_plain, omega);
-  const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
   PBF_HIP(hipMemsetAsync(fl.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
                      (uint64_t)n, omega, one);
@@ -1268,7 +1285,6 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
     PBF_HIP(hipMemcpyAsync(c + 4 * n * k, d_q + 4 * n * qcol[k], n * E, hipMemcpyDeviceToDevice, s));
   PBF_HIP(hipMemcpyAsync(c + 4 * n * 5, sg.p, 3 * n * E, hipMemcpyDeviceToDevice, s));
   if ((rc = pbf_ntt_fr256_batch_dev(ctx, w_plain, c, c, n, 8, 1, s))) return rc;
-  uint64_t pre[8][8];
   const Affine* tbl = nullptr;  // the SRS window table, when a prove on this context built it
   if ((rc = msm_fixed_lookup(ctx, d_srs, srs_m, s, &tbl))) return rc;
   if (tbl) {
@@ -1289,6 +1305,11 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   PBF_HIP(hipMemcpyAsync(&bad, fl.p, sizeof(int), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
   if (bad) return fail(PBF_EINVAL, "bad copy constraint label");
+  if (vk_on) {
+    ctx->vk_key = vk_key;
+    ctx->vk_pts.assign(&pre[0][0], &pre[0][0] + 64);
+  }
+  }
 
   const U256 alpha = hm(chal), beta = hm(chal + 4), gamma = hm(chal + 8), zc = hm(chal + 12), v = hm(chal + 16);
   const U256 u = hm(u_in);

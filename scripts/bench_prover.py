@@ -77,13 +77,20 @@ def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True) -> d
         g2 = ctx.g2_bn254_mul([G2], [s])[0]
         g2l = pbf._g2_limbs([G2, g2])
         ok = ctypes.c_int(-1)
-        t0 = time.perf_counter()
-        pbf._check(ctx.lib.pbf_plonk_verify_bn254_dev(ctx.h, n, dq.data_ptr(), dc.data_ptr(), dsrs.data_ptr(), srs_m,
-                                                      pbf._ptr(g2l), pbf._ptr(pts), pbf._ptr(fs),
-                                                      pbf._ptr(pbf.ints_to_limbs(chal)),
-                                                      pbf._ptr(pbf.ints_to_limbs([12345])),
-                                                      pbf._ptr(pbf.ints_to_limbs([2, 3])), mode, ctypes.byref(ok), sp))
-        out["verify_ms"] = (time.perf_counter() - t0) * 1e3
+        tv = []
+        for _ in range(6):  # the first call builds the verification key (8 commitments)
+            t0 = time.perf_counter()
+            pbf._check(ctx.lib.pbf_plonk_verify_bn254_dev(ctx.h, n, dq.data_ptr(), dc.data_ptr(), dsrs.data_ptr(),
+                                                          srs_m, pbf._ptr(g2l), pbf._ptr(pts), pbf._ptr(fs),
+                                                          pbf._ptr(pbf.ints_to_limbs(chal)),
+                                                          pbf._ptr(pbf.ints_to_limbs([12345])),
+                                                          pbf._ptr(pbf.ints_to_limbs([2, 3])), mode, ctypes.byref(ok),
+                                                          sp))
+            tv.append((time.perf_counter() - t0) * 1e3)
+            if ok.value != 1:
+                break
+        out["verify_ms_no_key"] = tv[0]
+        out["verify_ms"] = sorted(tv[1:])[len(tv[1:]) // 2] if len(tv) > 1 else tv[0]
         out["verified"] = ok.value == 1
     return out
 

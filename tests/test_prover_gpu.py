@@ -144,3 +144,36 @@ def test_proving_key_cache_matches_cold_proofs(monkeypatch):
         cold.close()
     assert got == [ref[name] for name in order]
     assert ref["A"] != ref["B"]
+
+
+def test_verification_key_cache(ctx, monkeypatch):
+    """The verifier keeps the 8 preprocessed commitments per (circuit, SRS), fingerprint-
+    checked on every call: accept / reject over interleaved inputs (the proof against a
+    circuit with one selector changed, with two copy labels swapped, against another SRS)
+    equals the answers with the commitments recomputed per call (PBF_VERIFIER_NO_VK)."""
+    rng = random.Random(777)
+    n = 64
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    s1, s2 = 1234567, 7654321
+    srs1, srs2 = ctx.srs_create(s1, n + 3), ctx.srs_create(s2, n + 3)
+    g2 = {s: [B.G2_GEN, ctx.g2_bn254_mul([B.G2_GEN], [s])[0]] for s in (s1, s2)}
+    q, cp, abc = P.mul_gates_circuit(n, 21)
+    q_mod = [list(col) for col in q]
+    q_mod[4][0] = (q_mod[4][0] + 1) % P.R
+    cp_mod = [list(col) for col in cp]
+    cp_mod[0][0], cp_mod[0][1] = cp_mod[0][1], cp_mod[0][0]
+    pa = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs1, mode=1)
+    pa2 = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs2, mode=1)
+    runs = [(q, cp, srs1, s1, pa), (q_mod, cp, srs1, s1, pa), (q, cp_mod, srs1, s1, pa), (q, cp, srs1, s1, pa),
+            (q, cp, srs2, s2, pa2), (q, cp, srs2, s2, pa), (q, cp, srs1, s1, pa)]
+
+    def answers():
+        return [ctx.plonk_verify_bn254(qq, cc, srs, g2[s], pr[0], pr[1], chal, 99, mode=1)
+                for qq, cc, srs, s, pr in runs]
+
+    warm = answers()
+    monkeypatch.setenv("PBF_VERIFIER_NO_VK", "1")
+    cold = answers()
+    assert warm == cold, (warm, cold)
+    assert warm == [True, False, False, True, True, False, True], warm
