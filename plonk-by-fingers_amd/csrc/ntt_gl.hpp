@@ -67,6 +67,10 @@ struct GlPassArgs {
   uint32_t out_split_log;  // != 0: store destination-major [n/S][batch][S] (multi-GPU send layout)
   uint32_t xcd_kmajor;     // XCD-aware column-major block order (pass-twiddle table reuse in L2)
   uint32_t blk_log;        // BLK first pass: log2 of the blocked layout's block width W2
+  // padded intermediates (PBF_NTT_PAD): element g of a polynomial sits at g + (g >> rows_log)
+  // * pad, polynomials `pitch` elements apart (user buffers: pad 0, pitch n)
+  uint64_t in_pitch, out_pitch;
+  uint32_t in_pad, out_pad, out_rows_log;
 };
 
 // x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1. Exponents in
@@ -197,8 +201,9 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   gl_tile_coords(a, tile, tiles, &poly, &kb);
   if constexpr (PBF_GL_NOMEM_ON) kb &= 1, poly = 0;
   const uint64_t j0 = (uint64_t)kb * W;
-  const uint64_t* in = a.in + (uint64_t)poly * a.n;
-  const uint64_t stride = a.n >> LOGR;
+  const uint64_t* in = a.in + (uint64_t)poly * a.in_pitch;
+  // input rows (r) are n/R long: a padded input adds in_pad per row
+  const uint64_t stride = (a.n >> LOGR) + a.in_pad;
 
   // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
   uint64_t v[16];
@@ -353,7 +358,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 
   // ---------------- store
   if constexpr (FIRST) {
-    uint64_t* o = a.out + (uint64_t)poly * a.n;
+    uint64_t* o = a.out + (uint64_t)poly * a.out_pitch;
 #pragma unroll
     for (int u = 0; u < Sh::NSUB_C; ++u) {
       int k1, w;
@@ -368,7 +373,9 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
           o[(uint64_t)(k >> bl) * bstride + jw + (k & ((1u << bl) - 1))] = x[u * C + bitrev_c(k2, LOGC)];
         }
       } else {
-        const uint64_t base = (j0 + w) << LOGR;
+        // a run of R outputs never crosses a row of the next pass (R <= n / R_next)
+        const uint64_t base0 = (j0 + w) << LOGR;
+        const uint64_t base = base0 + (base0 >> a.out_rows_log) * a.out_pad;
 #pragma unroll
         for (int k2 = 0; k2 < C; ++k2)
           if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
@@ -377,7 +384,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     }
   } else {
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
-    uint64_t* out = a.out + (uint64_t)poly * a.n;
+    uint64_t* out = a.out + (uint64_t)poly * a.out_pitch;
     const uint32_t sl = a.out_split_log;
 #pragma unroll
     for (int u = 0; u < Sh::NSUB_C; ++u) {
@@ -385,7 +392,13 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
       c_map(u, &k1, &w);
       const uint64_t j = j0 + w;
       const uint64_t base = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask);
-      if (sl == 0) {
+      if (sl == 0 && a.out_pad) {
+#pragma unroll
+        for (int k2 = 0; k2 < C; ++k2) {
+          const uint64_t g = base + ((uint64_t)(k1 + 64 * k2) << a.log_ns);
+          out[g + (g >> a.out_rows_log) * a.out_pad] = x[u * C + bitrev_c(k2, LOGC)];
+        }
+      } else if (sl == 0) {
 #pragma unroll
         for (int k2 = 0; k2 < C; ++k2)
           if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)

@@ -449,6 +449,24 @@ static GlPassFn gl_fn_blk(int logr, bool first) {
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
 
+// Padded intermediates (PBF_NTT_PAD = elements per row, A/B): the scratch between passes i and
+// i+1 keeps each of its rows (n / R_(i+1) elements: what pass i+1 reads as one row r) `pad`
+// elements apart, breaking the power-of-two strides of the strided reads. Not with the
+// persistent or blocked variants.
+static uint64_t gl_pad(const NttPlan& p) {
+  const char* e = getenv("PBF_NTT_PAD");
+  if (!e || !p.gl || p.logr.size() < 2 || getenv("PBF_NTT_PERSIST") || getenv("PBF_NTT_BLK")) return 0;
+  const long long v = atoll(e);
+  return v > 0 && v <= 4096 ? (uint64_t)v : 0;
+}
+// elements per polynomial in the scratch buffers
+static uint64_t gl_pitch(const NttPlan& p) {
+  const uint64_t pad = gl_pad(p);
+  uint64_t rows = 0;
+  for (size_t i = 1; i < p.logr.size(); ++i) rows = std::max<uint64_t>(rows, 1ull << p.logr[i]);
+  return p.n + rows * pad;
+}
+
 int ForkSet::ensure(int streams) {
   if (streams > GL_MAX_STREAMS) streams = GL_MAX_STREAMS;
   if (streams > 1 && !fork) PBF_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
@@ -497,7 +515,7 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   for (size_t g0 = 0; g0 < batch; g0 += G, ++gi) {
     const size_t b = batch - g0 < G ? batch - g0 : G;
     const int rc = run_gl_group(p, d_in + g0 * p.n, d_out + g0 * p.n, b, s0, s1, sts[gi % ns], 0,
-                                ns > 1 ? g0 * p.n : 0);
+                                ns > 1 ? g0 * gl_pitch(p) : 0);
     if (rc) return rc;
   }
   if (ns > 1) {
@@ -539,6 +557,12 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     GlPassArgs a;
     a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p) + soff;
     a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p) + soff;
+    const uint64_t pad = blk ? 0 : gl_pad(p), pitch = gl_pitch(p);
+    a.in_pitch = (i == 0) ? p.n : pitch;
+    a.out_pitch = (i == P - 1) ? p.n : pitch;
+    a.in_pad = (i == 0) ? 0 : (uint32_t)pad;
+    a.out_pad = (i == P - 1) ? 0 : (uint32_t)pad;
+    a.out_rows_log = (i == P - 1) ? 0 : p.log_n - (uint32_t)p.logr[i + 1];
     a.twpass = (const uint64_t*)p.twpass[i]->p;
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;
@@ -591,7 +615,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     return 0;
   }
   const size_t P = p.logr.size();
-  const size_t bytes = batch * p.n * 8;
+  const size_t bytes = batch * (p.gl ? gl_pitch(p) : p.n) * 8;
   int rc = s0.ensure(bytes);
   if (!rc && P > 2) rc = s1.ensure(bytes);
   if (rc) return rc;

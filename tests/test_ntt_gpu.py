@@ -160,7 +160,7 @@ def test_batch_dev_matches_single(ctx):
 @pytest.mark.parametrize("env", [{"PBF_NTT_BLK": "1"}, {"PBF_NTT_PERSIST": "1"}, {"PBF_NTT_GROUP": "2"},
                                  {"PBF_NTT_GROUP": "1", "PBF_NTT_STREAMS": "3"}, {"PBF_NTT_STREAMS": "1"},
                                  {"PBF_NTT_GROUP": "0"}, {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"},
-                                 {"PBF_NTT_NO_KMAJOR": "1"}])
+                                 {"PBF_NTT_NO_KMAJOR": "1"}, {"PBF_NTT_PAD": "16"}, {"PBF_NTT_PAD": "8", "PBF_NTT_STREAMS": "1"}])
 @pytest.mark.parametrize("logn", [16, 20])
 def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     """Every opt-in schedule of the Goldilocks pass kernel (blocked intermediate, persistent
@@ -187,7 +187,7 @@ def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
 
 
 @pytest.mark.parametrize("env", [{"PBF_NTT_TWMAX_LOG": "18"}, {"PBF_NTT_TWSPLIT": "1"},
-                                 {"PBF_NTT_TWMAX_LOG": "18", "PBF_NTT_NO_TWSPLIT": "1"}])
+                                 {"PBF_NTT_TWMAX_LOG": "18", "PBF_NTT_NO_TWSPLIT": "1"}, {"PBF_NTT_PAD": "16"}])
 def test_twiddle_table_paths(monkeypatch, vectors, env):
     """The three sources of the pass twiddle w^(r k): the per-pass [r][k] table (default up to
     2^PBF_NTT_TWMAX_LOG = 2^24 entries), the last pass's split table B[kb][r] * A[r][w]
