@@ -211,7 +211,12 @@ int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars,
  * with mode 0 an honest proof verifies only when (a_z+b*s1_z+g)(b_z+b*s2_z+g)*alpha = 0,
  * as in the reference's n = 4 KAT).
  * Errors: PBF_EINVAL for an unsatisfied circuit (constraints.rs:198), a zero permutation
- * denominator (plonk.rs:297), a non-divisible quotient (plonk.rs:370), short SRS.       */
+ * denominator (plonk.rs:297), a non-divisible quotient (plonk.rs:370), short SRS.
+ * Keys: the context keeps the circuit's preprocessed polynomials (q_*, s_sigma_*, l1:
+ * coefficients and coset evaluations, ~0.6 KiB per gate; single-GPU prove) and the
+ * verifier's 8 preprocessed commitments, checked against 64-bit fingerprints of q /
+ * copies (and the SRS for verify) on every call and rebuilt when they differ. Outputs
+ * are identical either way; PBF_PROVER_NO_PK=1 / PBF_VERIFIER_NO_VK=1 disable the keys.  */
 int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies, const uint64_t* abc,
                           const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* srs,
                           size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f);
