@@ -128,6 +128,9 @@ def load_traffic(log_n: int, batch: int):
     return None
 
 
+COLL_DEVICE = "cuda"  # where bench-side collectives (max over ranks, proof agreement) run
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,7 +144,12 @@ def main() -> int:
     ap.add_argument("--no-traffic", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
     ap.add_argument("--prove-log-n", type=str, default="20,24",
                     help="N > 1: gate counts (log2, comma-separated) of the sharded config-5 prove")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1 collectives: nccl (= RCCL over xGMI, the measured path) or gloo, a rehearsal "
+                         "of the N > 1 code path on fewer GPUs than ranks (ranks share devices, device "
+                         "buffers staged through the host; not a measurement)")
     args = ap.parse_args()
+    global COLL_DEVICE
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -151,28 +159,34 @@ def main() -> int:
             print("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)",
                   file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
+    device = local_rank % torch.cuda.device_count() if args.backend == "gloo" else local_rank
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
         import datetime
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
-                                timeout=datetime.timedelta(seconds=180))
+        if args.backend == "gloo":
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
+            COLL_DEVICE = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                    timeout=datetime.timedelta(seconds=180))
 
     n_local = 1 << args.log_n
     B = args.batch
-    ctx = pbf.Context(local_rank)
+    ctx = pbf.Context(device)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
 
     if world == 1:
         step_fn, n_global = _single_gpu(ctx, n_local, B, sp)
     else:
-        from multigpu import BenchSharded  # plonk-by-fingers_amd/multigpu.py
+        from multigpu import BenchSharded, DistComm  # plonk-by-fingers_amd/multigpu.py
 
-        sh = BenchSharded(ctx, dist, rank, world, args.log_n, B, sp)
+        sh = BenchSharded(ctx, dist if args.backend == "nccl" else DistComm(dist, world), rank, world, args.log_n, B,
+                          sp)
         step_fn, n_global = sh.step, sh.n_global
 
     for _ in range(args.warmup):
@@ -193,7 +207,7 @@ def main() -> int:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ev_ms = ev0.elapsed_time(ev1)
-    t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device="cuda")
+    t = torch.tensor([wall, ev_ms / 1e3], dtype=torch.float64, device=COLL_DEVICE)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max, ev_max = float(t[0]), float(t[1])
@@ -337,10 +351,10 @@ def config5_sharded(ctx, dist, rank: int, world: int, sp: int, log_ns: str) -> d
                 pts, fs = run()
                 torch.cuda.synchronize()
                 ts.append(time.perf_counter() - t0)
-            t = torch.tensor([sorted(ts)[1]], dtype=torch.float64, device="cuda")
+            t = torch.tensor([sorted(ts)[1]], dtype=torch.float64, device=COLL_DEVICE)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             # every rank must hold the same proof
-            mine = torch.from_numpy(np.concatenate([pts, fs]).view(np.int64)).cuda()
+            mine = torch.from_numpy(np.concatenate([pts, fs]).view(np.int64)).to(COLL_DEVICE)
             allp = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(allp, mine)
             same = all(torch.equal(allp[0], x) for x in allp)
