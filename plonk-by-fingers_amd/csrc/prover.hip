@@ -87,6 +87,11 @@ __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_str
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
+  if (in_off + in_stride * i0 >= len) {  // the whole chunk is zero padding (j grows with i): no powers
+    for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64)
+      for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
+    return;
+  }
   U256 x = fr_pow(base, e_off + e_mult * i0);
   const U256 step = fr_pow(base, 64 * e_mult);
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
@@ -332,13 +337,15 @@ struct QuotArgs {
   U256 alpha, beta, gamma, k1, k2, alpha2, g, wN;
   U256 zh_inv[4];
 };
-__global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out) {
+// ch: points per thread (lane l of a wave takes first + 64 k, k < ch); a chunk's first x
+// costs one fr_pow, so ch trades that against the resident waves of a 4n-point grid
+__global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uint32_t ch) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = chunk_first(t);
+  const uint64_t i0 = (t / 64) * 64 * ch + (t % 64);
   if (i0 >= q.N) return;
   U256 x = Fr::mul(q.g, fr_pow(q.wN, blk_index(q.blk, i0)));
   const U256 step = pow64(q.wN);
-  for (uint64_t p = i0, k = 0; k < PV_CHUNK && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
+  for (uint64_t p = i0, k = 0; k < ch && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
     const uint64_t o = 4 * p;
     const uint64_t i = blk_index(q.blk, p);
     const U256 a = ldr(q.a + o), b = ldr(q.b + o), c = ldr(q.c + o), z = ldr(q.z + o);
@@ -1002,7 +1009,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     }
   }
   uint64_t* tq = (uint64_t*)B.t.p;
-  hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, qa, W0);
+  {
+    const char* qc = getenv("PBF_QUOT_CHUNK");
+    const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
+    hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, W0, qch);
+  }
   PBF_HIP(hipGetLastError());
   if ((rc = P.coset_intt(W0, tq))) return rc;
   const uint64_t m = n + 2;  // coefficients per t part
