@@ -75,6 +75,58 @@ def cpu_baseline(log_n: int, budget_s: float) -> dict:
                                     f"(iterative radix-2, one polynomial per thread), {el2:.1f} s"}}
 
 
+def cpu_baselines_bn254(budget_s: float = 3.0) -> dict:
+    """CPU baselines of configs 3-5 (1 core, the Python oracle's restatements of the
+    reference, which is single-threaded), timed on bounded samples and extrapolated only
+    where the reference's cost model is exact:
+      config 3: mul_ntt (fft.rs:109-132) at 2^12 x 2^12 -> n log n to 2^22 x 2^22;
+      config 4: the naive-fold MSM (plonk.rs:51-58) on 8 points -> linear to 2^20;
+      config 5: Plonk::prove (plonk.rs:191-466, literal: Vandermonde interpolation, long
+                division) at n = 8, not extrapolated (its cost grows as n^3)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import random as _r
+
+    import bn254  # checker/baseline only (never on the GPU path)
+    import plonk_bn254 as PB
+
+    rng = _r.Random(0x5EED0003)
+    out = {}
+    la = 1 << 12
+    a = [rng.randrange(bn254.R) for _ in range(la)]
+    b = [rng.randrange(bn254.R) for _ in range(la)]
+    w = bn254.root_of_unity(2 * la)
+    runs, t0 = 0, time.perf_counter()
+    while runs < 1 or time.perf_counter() - t0 < budget_s:
+        bn254.mul_ntt(a, b, w)
+        runs += 1
+    t = (time.perf_counter() - t0) / runs
+    big, small = (1 << 23) * 23, (2 * la) * 13
+    out["config3_polymul_2p22"] = {"ms": t * big / small * 1e3, "unit": "ms (extrapolated n log n)", "cores": 1,
+                                   "kind": "port", "sample": f"{runs} x mul_ntt 2^12 x 2^12 (NTT 2^13) in "
+                                                             f"{t * 1e3:.1f} ms each, oracle/bn254.py"}
+    npts = 8
+    pts = [bn254.g1_mul(bn254.G1_GEN, rng.randrange(1, bn254.R)) for _ in range(npts)]
+    sc = [rng.randrange(bn254.R) for _ in range(npts)]
+    t0 = time.perf_counter()
+    bn254.msm_naive(pts, sc)
+    t = time.perf_counter() - t0
+    out["config4_msm_2p20"] = {"ms": t * (1 << 20) / npts * 1e3, "unit": "ms (extrapolated linearly)", "cores": 1,
+                               "kind": "port", "sample": f"naive fold of {npts} points in {t * 1e3:.0f} ms, "
+                                                         "oracle/bn254.py msm_naive"}
+    prov = {}
+    for n in (8,):
+        st = PB.Setup(n, 1234567, n + 3)
+        q, cp, abc = PB.mul_gates_circuit(n, 0x5EED0005)
+        chal = [rng.randrange(bn254.R) for _ in range(5)]
+        rnd = [rng.randrange(bn254.R) for _ in range(9)]
+        t0 = time.perf_counter()
+        PB.prove(st, q, cp, abc, chal, rnd, mode="paper")
+        prov[f"n{n}_ms"] = (time.perf_counter() - t0) * 1e3
+    out["config5_prove"] = dict(prov, cores=1, kind="port", sample="oracle/plonk_bn254.py literal Plonk::prove "
+                                "(O(n^3) interpolation), not extrapolated")
+    return out
+
+
 def live_traffic(log_n: int, batch: int, steps: int = 6) -> dict | None:
     """HBM bytes per step of the NTT bench workload, measured now: two rocprofv3 PMC passes
     (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots")
@@ -269,6 +321,11 @@ def main() -> int:
                                                              "tallied at half (MI355X_MICROARCH.md, HBM)")
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
+            if "extra" in out:
+                try:
+                    out["extra"]["cpu_baselines_configs_3_5"] = cpu_baselines_bn254()
+                except Exception as e:  # reported, never fatal to the headline line
+                    out["extra"]["cpu_baselines_configs_3_5"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
