@@ -399,8 +399,13 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
     a.tw_bits = p.tw_bits;
     a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
     a.batch = (uint32_t)batch;
-    a.conv_in = (i == 0);
-    a.conv_out = (i == P - 1);
+    // no Montgomery conversions: the twiddles (and n^-1) are stored in Montgomery form, so
+    // mont(x, w R) = x w keeps canonical data canonical through every product, and the adds
+    // are the same in both forms -- the first pass's to_mont and the last pass's from_mont
+    // (one product per element each) are not needed (conv_* kept for A/B: PBF_NTT256_CONV=1)
+    const bool conv = getenv("PBF_NTT256_CONV") != nullptr;
+    a.conv_in = conv && i == 0;
+    a.conv_out = conv && i == P - 1;
     a.scale = (p.inverse && i == P - 1);
     Pass256Fn fn = pass256_fn(lr);
     if (!fn) return fail(PBF_EINVAL, "no 256-bit kernel for this radix");

@@ -24,8 +24,13 @@ def test_small_vs_recursion_faithful(ctx, logn):
     assert ctx.ntt_fr(w, got, inverse=True) == a
 
 
+@pytest.mark.parametrize("conv", [False, True])
 @pytest.mark.parametrize("logn", [12, 13, 14, 15, 16, 17])
-def test_multi_pass_vs_oracle(ctx, logn):
+def test_multi_pass_vs_oracle(ctx, monkeypatch, logn, conv):
+    """Multi-pass Fr NTT both ways vs the oracle; conv: with the (optional) Montgomery
+    conversions of the first and last pass (PBF_NTT256_CONV), which the default skips."""
+    if conv:
+        monkeypatch.setenv("PBF_NTT256_CONV", "1")
     n = 1 << logn
     w = bn254.root_of_unity(n)
     a = bn254.limbs_to_ints(bn254.random_limbs(n, 20 + logn))
