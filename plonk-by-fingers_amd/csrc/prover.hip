@@ -82,8 +82,10 @@ __device__ __forceinline__ U256 pow64(U256 b) {
 // (coset scaling with zero padding; with in_stride = e_mult = G, in_off = e_off = rank it
 // extracts rank's stride shard of the scaled vector). The product of a canonical value and
 // a Montgomery-form power is the canonical product (a * xR * R^-1): no conversions.
+// c0 (Montgomery form, used when has_c0): an extra constant factor of every output -- the
+// quotient's circuit slots come out at a chosen R-degree this way, for free (see QuotArgs)
 __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out,
-                            uint64_t count, U256 base, uint64_t e_off, uint64_t e_mult) {
+                            uint64_t count, U256 base, uint64_t e_off, uint64_t e_mult, U256 c0, uint32_t has_c0) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
@@ -93,6 +95,7 @@ __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_str
     return;
   }
   U256 x = fr_pow(base, e_off + e_mult * i0);
+  if (has_c0) x = Fr::mul(x, c0);
   const U256 step = fr_pow(base, 64 * e_mult);
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     const uint64_t j = in_off + in_stride * i;
@@ -321,21 +324,31 @@ __global__ void k_lincomb(LinComb L, uint64_t* out, uint64_t count) {
   str(out + 4 * i, acc);
 }
 
+// out = a b for canonical a and b held at R-degree 1 (b R: mont(a, b R) = a b, canonical)
 __global__ void k_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t count) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) str(out + 4 * i, Fr::mul(ldr(a + 4 * i), ldr(b + 4 * i)));
+  if (i < count) u256_to_u64(Fr::mul(u256_from_u64(a + 4 * i), u256_from_u64(b + 4 * i)), out + 4 * i);
 }
 
 // t(x_i) for x_i = g w_N^i on the coset (N = 4n): the numerator of plonk.rs:358-368
 // divided by Z_H(x_i) = g^n w_4^(i mod 4) - 1 (inverses zh_inv[0..3] from the host)
+// No Montgomery conversions (late round 2): a stored value u "has R-degree d" for the field
+// value v when u = v R^d (mod p); mont(u1, u2) = u1 u2 / R adds degrees minus one and adds
+// need equal degrees. The coset slots come out of coset_ntt_batch at the degrees
+// QUOT_DEG gives (a b c z z(wx) qc raw; ql qr qo s1 s2 s3 l1 at 1; qm at 2) and the host
+// passes every constant at the degree its use needs, so every term below lands at degree 0
+// and the output is canonical with no to_mont / from_mont (14 products per point fewer).
+constexpr int QUOT_DEG[14] = {0, 0, 0, 0, 1, 1, 1, 2, 0, 1, 1, 1, 1, 0};
 struct QuotArgs {
   const uint64_t *a, *b, *c, *z, *ql, *qr, *qo, *qm, *qc, *s1, *s2, *s3, *l1;
   const uint64_t* zw;  // z(w x) evaluations (sharded layout), or null: z at index i + 4
   uint64_t N;          // evaluations held here (N, or nl on a rank of a sharded prove)
   uint64_t N_all;      // 4n
   Blk blk;
-  U256 alpha, beta, gamma, k1, k2, alpha2, g, wN;
-  U256 zh_inv[4];
+  U256 beta0, gamma0;  // degree 0
+  U256 alpha4;         // degree 4
+  U256 k1, k2, alpha2, g, wN;  // degree 1 (Montgomery form)
+  U256 zh_inv[4];      // degree 1
 };
 // ch: points per thread (lane l of a wave takes first + 64 k, k < ch); a chunk's first x
 // costs one fr_pow, so ch trades that against the resident waves of a 4n-point grid
@@ -348,29 +361,31 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uin
   for (uint64_t p = i0, k = 0; k < ch && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
     const uint64_t o = 4 * p;
     const uint64_t i = blk_index(q.blk, p);
-    const U256 a = ldr(q.a + o), b = ldr(q.b + o), c = ldr(q.c + o), z = ldr(q.z + o);
-    const U256 zw = q.zw ? ldr(q.zw + o) : ldr(q.z + 4 * ((i + 4) % q.N_all));  // z(w x_i): w = w_N^4
-    // t1: a b q_m + a q_l + b q_r + c q_o + q_c
-    U256 t1 = Fr::mul(Fr::mul(a, b), ldr(q.qm + o));
-    t1 = Fr::add(t1, Fr::mul(a, ldr(q.ql + o)));
-    t1 = Fr::add(t1, Fr::mul(b, ldr(q.qr + o)));
-    t1 = Fr::add(t1, Fr::mul(c, ldr(q.qo + o)));
-    t1 = Fr::add(t1, ldr(q.qc + o));
-    // t2: alpha (a + beta x + gamma)(b + beta k1 x + gamma)(c + beta k2 x + gamma) z
-    const U256 bx = Fr::mul(q.beta, x);
-    U256 t2 = Fr::mul(q.alpha, Fr::add(Fr::add(a, bx), q.gamma));
-    t2 = Fr::mul(t2, Fr::add(Fr::add(b, Fr::mul(bx, q.k1)), q.gamma));
-    t2 = Fr::mul(t2, Fr::add(Fr::add(c, Fr::mul(bx, q.k2)), q.gamma));
+    auto ld = [](const uint64_t* p) { return u256_from_u64(p); };  // as stored (its slot's degree)
+    const U256 a = ld(q.a + o), b = ld(q.b + o), c = ld(q.c + o), z = ld(q.z + o);
+    const U256 zw = q.zw ? ld(q.zw + o) : ld(q.z + 4 * ((i + 4) % q.N_all));  // z(w x_i): w = w_N^4
+    // t1: a b q_m + a q_l + b q_r + c q_o + q_c                   (degrees -1+2, 0+1, 0)
+    U256 t1 = Fr::mul(Fr::mul(a, b), ld(q.qm + o));
+    t1 = Fr::add(t1, Fr::mul(a, ld(q.ql + o)));
+    t1 = Fr::add(t1, Fr::mul(b, ld(q.qr + o)));
+    t1 = Fr::add(t1, Fr::mul(c, ld(q.qo + o)));
+    t1 = Fr::add(t1, ld(q.qc + o));
+    // t2 - t3 = (a + beta x + gamma)(b + beta k1 x + gamma)(c + beta k2 x + gamma) z
+    //         - (a + beta s1 + gamma)(b + beta s2 + gamma)(c + beta s3 + gamma) z(w x)   (degree -3),
+    // times alpha once (alpha at degree 4)
+    const U256 bx = Fr::mul(q.beta0, x);  // x at degree 1
+    U256 t2 = Fr::mul(Fr::add(Fr::add(a, bx), q.gamma0), Fr::add(Fr::add(b, Fr::mul(bx, q.k1)), q.gamma0));
+    t2 = Fr::mul(t2, Fr::add(Fr::add(c, Fr::mul(bx, q.k2)), q.gamma0));
     t2 = Fr::mul(t2, z);
-    // t3: alpha (a + beta s1 + gamma)(b + beta s2 + gamma)(c + beta s3 + gamma) z(w x)
-    U256 t3 = Fr::mul(q.alpha, Fr::add(Fr::add(a, Fr::mul(q.beta, ldr(q.s1 + o))), q.gamma));
-    t3 = Fr::mul(t3, Fr::add(Fr::add(b, Fr::mul(q.beta, ldr(q.s2 + o))), q.gamma));
-    t3 = Fr::mul(t3, Fr::add(Fr::add(c, Fr::mul(q.beta, ldr(q.s3 + o))), q.gamma));
+    U256 t3 = Fr::mul(Fr::add(Fr::add(a, Fr::mul(q.beta0, ld(q.s1 + o))), q.gamma0),
+                      Fr::add(Fr::add(b, Fr::mul(q.beta0, ld(q.s2 + o))), q.gamma0));
+    t3 = Fr::mul(t3, Fr::add(Fr::add(c, Fr::mul(q.beta0, ld(q.s3 + o))), q.gamma0));
     t3 = Fr::mul(t3, zw);
-    // t4: alpha^2 (z - 1) L1
-    const U256 t4 = Fr::mul(Fr::mul(q.alpha2, Fr::sub(z, fr_one_m())), ldr(q.l1 + o));
-    const U256 num = Fr::add(Fr::sub(Fr::add(t1, t2), t3), t4);
-    str(out + o, Fr::mul(num, q.zh_inv[i & 3]));
+    const U256 t23 = Fr::mul(Fr::sub(t2, t3), q.alpha4);
+    // t4: alpha^2 (z - 1) L1                                        (0+1-1, then +1-1)
+    const U256 t4 = Fr::mul(Fr::mul(Fr::sub(z, Fr::one_plain()), ld(q.l1 + o)), q.alpha2);
+    const U256 num = Fr::add(Fr::add(t1, t23), t4);
+    u256_to_u64(Fr::mul(num, q.zh_inv[i & 3]), out + o);
   }
 }
 
@@ -634,20 +649,27 @@ struct Prover {
     return 0;
   }
   void scale(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out, uint64_t cnt,
-             const U256& base, uint64_t e_off, uint64_t e_mult) {
+             const U256& base, uint64_t e_off, uint64_t e_mult, int deg = 0) {
+    // outputs at R-degree deg: the constant R^deg in Montgomery form is R^(deg + 1)
+    U256 c0 = Fr::one_plain();
+    for (int d = 0; d <= deg; ++d) c0 = Fr::to_mont(c0);
     hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
-                       in_stride, len, out, cnt, base, e_off, e_mult);
+                       in_stride, len, out, cnt, base, e_off, e_mult, c0, (uint32_t)(deg != 0));
   }
   // k coset NTTs of size N: slot i = evaluations of sum_j srcs[i][j] (bases[i] x)^j at g w_N^e
-  // (this rank's blocks when sharded), slots count() apart in `out`
-  int coset_ntt_batch(int k, const uint64_t* const* srcs, const uint64_t* lens, const U256* bases, uint64_t* out) {
+  // (this rank's blocks when sharded), slots count() apart in `out`, at R-degree degs[i]
+  // (null: canonical)
+  int coset_ntt_batch(int k, const uint64_t* const* srcs, const uint64_t* lens, const U256* bases, uint64_t* out,
+                      const int* degs = nullptr) {
     if (G == 1) {
-      for (int i = 0; i < k; ++i) scale(srcs[i], 0, 1, lens[i], out + 4 * N * i, N, bases[i], 0, 1);
+      for (int i = 0; i < k; ++i)
+        scale(srcs[i], 0, 1, lens[i], out + 4 * N * i, N, bases[i], 0, 1, degs ? degs[i] : 0);
       PBF_HIP(hipGetLastError());
       return ntt(wN_plain, out, out, N, k, 0);  // one batched NTT (fuller GPU, one plan lookup)
     }
     uint64_t* sh = (uint64_t*)shard->p;
-    for (int i = 0; i < k; ++i) scale(srcs[i], rank, G, lens[i], sh + 4 * nl * i, nl, bases[i], rank, G);
+    for (int i = 0; i < k; ++i)
+      scale(srcs[i], rank, G, lens[i], sh + 4 * nl * i, nl, bases[i], rank, G, degs ? degs[i] : 0);
     PBF_HIP(hipGetLastError());
     int rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, sh, (uint64_t*)comm->send, nl, k, 0, s);
     if (!rc) rc = a2a((size_t)k * S * 32);
@@ -977,12 +999,12 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     // which may sit in another rank's block
     srcs[13] = zx; lens[13] = n + 3; bases[13] = Fr::mul(P.g, P.omega);
     if (pk_on) {  // a b c z per proof; the 9 circuit slots once per proving key
-      if ((rc = P.coset_ntt_batch(4, srcs, lens, bases, CE(0)))) return rc;
+      if ((rc = P.coset_ntt_batch(4, srcs, lens, bases, CE(0), QUOT_DEG))) return rc;
       if (!pk_hit) {
-        if ((rc = P.coset_ntt_batch(9, srcs + 4, lens + 4, bases + 4, CE(4)))) return rc;
+        if ((rc = P.coset_ntt_batch(9, srcs + 4, lens + 4, bases + 4, CE(4), QUOT_DEG + 4))) return rc;
         ctx->pk_key = pk_key;
       }
-    } else if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0)))) {
+    } else if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0), QUOT_DEG))) {
       return rc;
     }
   }
@@ -994,7 +1016,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   qa.N = NE;
   qa.N_all = N;
   qa.blk = P.blk();
-  qa.alpha = alpha; qa.beta = beta; qa.gamma = gamma; qa.k1 = k1; qa.k2 = k2;
+  // constants at the R-degrees the quotient's terms need (QuotArgs): Montgomery form is degree 1
+  qa.beta0 = Fr::from_mont(beta);
+  qa.gamma0 = Fr::from_mont(gamma);
+  qa.alpha4 = Fr::to_mont(Fr::to_mont(Fr::to_mont(alpha)));
+  qa.k1 = k1; qa.k2 = k2;
   qa.alpha2 = Fr::mul(alpha, alpha);
   qa.g = P.g; qa.wN = P.omegaN;
   {
