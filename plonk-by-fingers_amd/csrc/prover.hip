@@ -181,26 +181,33 @@ __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64
   }
 }
 
-// round 2 terms (plonk.rs:282-297) for row j < n-1: num_j = dend, den_j = dsor
+// round 2 terms (plonk.rs:282-297) for row j < n-1: num_j = dend, den_j = dsor.
+// Conversion-free (R-degrees as in QuotArgs): canonical a b c w sigma, beta k1 k2 in
+// Montgomery form (degree 1), gamma0 canonical: each factor lands at degree 0, each
+// three-factor product at degree -2 -- num and den alike, and k_div_batch takes them so.
 __global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n, U256 beta,
-                             U256 gamma, U256 k1, U256 k2, uint64_t* num, uint64_t* den) {
+                             U256 gamma0, U256 k1, U256 k2, uint64_t* num, uint64_t* den) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j + 1 >= n) return;
-  const U256 a = ldr(abc + 4 * j), b = ldr(abc + 4 * (n + j)), c = ldr(abc + 4 * (2 * n + j));
-  const U256 w = ldr(hpow + 4 * j);
+  auto ld = [](const uint64_t* p) { return u256_from_u64(p); };
+  const U256 a = ld(abc + 4 * j), b = ld(abc + 4 * (n + j)), c = ld(abc + 4 * (2 * n + j));
+  const U256 w = ld(hpow + 4 * j);
   const U256 bw = Fr::mul(beta, w);
-  U256 d1 = Fr::add(Fr::add(a, bw), gamma);
-  U256 d2 = Fr::add(Fr::add(b, Fr::mul(bw, k1)), gamma);
-  U256 d3 = Fr::add(Fr::add(c, Fr::mul(bw, k2)), gamma);
-  str(num + 4 * j, Fr::mul(Fr::mul(d1, d2), d3));
-  U256 e1 = Fr::add(Fr::add(a, Fr::mul(beta, ldr(sigma + 4 * j))), gamma);
-  U256 e2 = Fr::add(Fr::add(b, Fr::mul(beta, ldr(sigma + 4 * (n + j)))), gamma);
-  U256 e3 = Fr::add(Fr::add(c, Fr::mul(beta, ldr(sigma + 4 * (2 * n + j)))), gamma);
-  str(den + 4 * j, Fr::mul(Fr::mul(e1, e2), e3));
+  U256 d1 = Fr::add(Fr::add(a, bw), gamma0);
+  U256 d2 = Fr::add(Fr::add(b, Fr::mul(bw, k1)), gamma0);
+  U256 d3 = Fr::add(Fr::add(c, Fr::mul(bw, k2)), gamma0);
+  u256_to_u64(Fr::mul(Fr::mul(d1, d2), d3), num + 4 * j);
+  U256 e1 = Fr::add(Fr::add(a, Fr::mul(beta, ld(sigma + 4 * j))), gamma0);
+  U256 e2 = Fr::add(Fr::add(b, Fr::mul(beta, ld(sigma + 4 * (n + j)))), gamma0);
+  U256 e3 = Fr::add(Fr::add(c, Fr::mul(beta, ld(sigma + 4 * (2 * n + j)))), gamma0);
+  u256_to_u64(Fr::mul(Fr::mul(e1, e2), e3), den + 4 * j);
 }
 
 // out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
-// chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297)
+// chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297).
+// num and den are read as stored: with both at R-degree e the quotient comes out at
+// degree 1 (the Montgomery inverse of a degree-e value is at degree 2 - e), which the final
+// from_mont turns canonical. num == null: 1 / den (den at degree 1).
 #ifndef PBF_INV_CHUNK
 #define PBF_INV_CHUNK 32
 #endif
@@ -213,17 +220,17 @@ __global__ void __launch_bounds__(256) k_div_batch(const uint64_t* num, const ui
   U256 pre[INV_CHUNK];
   U256 acc = fr_one_m();
   for (int k = 0; k < m; ++k) {
-    const U256 d = ldr(den + 4 * (i0 + k));
+    const U256 d = u256_from_u64(den + 4 * (i0 + k));
     if (Fr::is_zero(d)) { *bad = 1; return; }
     pre[k] = acc;
     acc = Fr::mul(acc, d);
   }
   U256 inv = fr_inv(acc);  // 1 / prod
   for (int k = m - 1; k >= 0; --k) {
-    const U256 d = ldr(den + 4 * (i0 + k));
+    const U256 d = u256_from_u64(den + 4 * (i0 + k));
     const U256 dinv = Fr::mul(inv, pre[k]);  // 1 / d_k
     inv = Fr::mul(inv, d);
-    str(out + 4 * (i0 + k), num ? Fr::mul(ldr(num + 4 * (i0 + k)), dinv) : dinv);
+    str(out + 4 * (i0 + k), num ? Fr::mul(u256_from_u64(num + 4 * (i0 + k)), dinv) : dinv);
   }
 }
 
@@ -318,10 +325,11 @@ struct LinComb {
 __global__ void k_lincomb(LinComb L, uint64_t* out, uint64_t count) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  U256 acc = i == 0 ? L.c0 : u256_zero();
+  // conversion-free: canonical inputs times Montgomery-form constants are canonical products
+  U256 acc = i == 0 ? Fr::from_mont(L.c0) : u256_zero();
   for (int k = 0; k < L.k; ++k)
-    if (i < L.len[k]) acc = Fr::add(acc, Fr::mul(L.c[k], ldr(L.in[k] + 4 * i)));
-  str(out + 4 * i, acc);
+    if (i < L.len[k]) acc = Fr::add(acc, Fr::mul(L.c[k], u256_from_u64(L.in[k] + 4 * i)));
+  u256_to_u64(acc, out + 4 * i);
 }
 
 // out = a b for canonical a and b held at R-degree 1 (b R: mont(a, b R) = a b, canonical)
@@ -519,7 +527,8 @@ __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* par
   if (start < e.len[p]) {
     uint64_t end = start + EV_PER;
     if (end > e.len[p]) end = e.len[p];
-    for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul(acc, x), ldr(e.poly[p] + 4 * j));
+    // conversion-free Horner: canonical acc times Montgomery-form x stays canonical
+    for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul(acc, x), u256_from_u64(e.poly[p] + 4 * j));
     acc = Fr::mul(acc, fr_pow(x, start));
   }
   sh[t] = acc;
@@ -528,14 +537,14 @@ __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* par
     if (t < s) sh[t] = Fr::add(sh[t], sh[t + s]);
     __syncthreads();
   }
-  if (t == 0) str(partial + 4 * blockIdx.x, sh[0]);
+  if (t == 0) u256_to_u64(sh[0], partial + 4 * blockIdx.x);
 }
 __global__ void k_eval_final(const uint64_t* partial, uint64_t chunks, uint64_t np, uint64_t* out) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= np) return;
   U256 acc = u256_zero();
-  for (uint64_t i = 0; i < chunks; ++i) acc = Fr::add(acc, ldr(partial + 4 * (p * chunks + i)));
-  str(out + 4 * p, acc);
+  for (uint64_t i = 0; i < chunks; ++i) acc = Fr::add(acc, u256_from_u64(partial + 4 * (p * chunks + i)));
+  u256_to_u64(acc, out + 4 * p);
 }
 
 // ---------------------------------------------------------------- host helpers
@@ -941,7 +950,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* den = (uint64_t*)B.tmp1.p;
   PBF_HIP(hipMemsetAsync(acc, 0, CS * E, s));
   hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(n)), dim3(256), 0, s, d_abc, (const uint64_t*)sigma,
-                     (const uint64_t*)hpow, (uint64_t)n, beta, gamma, k1, k2, num, den);
+                     (const uint64_t*)hpow, (uint64_t)n, beta, Fr::from_mont(gamma), k1, k2, num, den);
   hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((n - 1 + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
                      (const uint64_t*)num, (const uint64_t*)den, num, (uint64_t)(n - 1), P.d_bad);
   PBF_HIP(hipGetLastError());
