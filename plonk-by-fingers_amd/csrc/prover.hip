@@ -409,10 +409,12 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uin
 // threads with multipliers z^(HS_PER 2^j)) and leaves its total; (2) one block turns the
 // totals into each block's incoming s (multiplier z^HS_BLK); (3) s_k += z^(k - k_b + 1) s_in.
 constexpr int HS_T = 256, HS_PER = 16, HS_BLK = HS_T * HS_PER, HS_LOG_T = 8;
+// Conversion-free: the recurrence is linear with Montgomery-form multipliers (z, z^k), so
+// canonical coefficients give canonical s_k, totals and quotients throughout.
 struct HsArgs {
   const uint64_t* p;
   uint64_t L;
-  U256 y;                 // subtracted from p_0 (Montgomery)
+  U256 y;                 // subtracted from p_0 (canonical)
   U256 z;                 // Montgomery
   U256 zs[HS_LOG_T];      // z^(HS_PER 2^j)
 };
@@ -428,7 +430,7 @@ __global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* t
     const uint64_t k = k0 + m;
     U256 u = u256_zero();
     if (k < a.L) {
-      u = ldr(a.p + 4 * (a.L - 1 - k));
+      u = u256_from_u64(a.p + 4 * (a.L - 1 - k));
       if (k == a.L - 1) u = Fr::sub(u, a.y);
     }
     acc = Fr::add(u, Fr::mul(a.z, acc));
@@ -452,10 +454,10 @@ __global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* t
     const uint64_t k = k0 + m;
     const U256 sk = Fr::add(v[m], Fr::mul(zk, carry));
     zk = Fr::mul(zk, a.z);
-    if (k + 1 < a.L) str(q + 4 * (a.L - 2 - k), sk);
-    else if (k + 1 == a.L) str(rem, sk);
+    if (k + 1 < a.L) u256_to_u64(sk, q + 4 * (a.L - 2 - k));
+    else if (k + 1 == a.L) u256_to_u64(sk, rem);
   }
-  if (t == HS_T - 1) str(totals + 4 * blockIdx.x, sh[t]);
+  if (t == HS_T - 1) u256_to_u64(sh[t], totals + 4 * blockIdx.x);
 }
 // totals[b] <- s_(b HS_BLK - 1), the s entering block b (0 for b = 0); one block
 __global__ void __launch_bounds__(HS_T) k_hs2(uint64_t* totals, uint64_t nb, U256 zb) {
@@ -465,7 +467,7 @@ __global__ void __launch_bounds__(HS_T) k_hs2(uint64_t* totals, uint64_t nb, U25
   const uint64_t b0 = (uint64_t)t * per;
   U256 acc = u256_zero();
   for (uint64_t k = 0; k < per; ++k)
-    if (b0 + k < nb) acc = Fr::add(ldr(totals + 4 * (b0 + k)), Fr::mul(zb, acc));
+    if (b0 + k < nb) acc = Fr::add(u256_from_u64(totals + 4 * (b0 + k)), Fr::mul(zb, acc));
   sh[t] = acc;
   __syncthreads();
   U256 m = fr_pow(zb, per);  // multiplier across one thread's range
@@ -480,8 +482,8 @@ __global__ void __launch_bounds__(HS_T) k_hs2(uint64_t* totals, uint64_t nb, U25
   U256 c = t ? sh[t - 1] : u256_zero();
   for (uint64_t k = 0; k < per; ++k) {
     if (b0 + k >= nb) break;
-    const U256 x = ldr(totals + 4 * (b0 + k));
-    str(totals + 4 * (b0 + k), c);
+    const U256 x = u256_from_u64(totals + 4 * (b0 + k));
+    u256_to_u64(c, totals + 4 * (b0 + k));
     c = Fr::add(x, Fr::mul(zb, c));
   }
 }
@@ -490,7 +492,7 @@ __global__ void __launch_bounds__(HS_T) k_hs3(uint64_t* q, uint64_t L, U256 z, c
                                               uint64_t* rem) {
   const uint64_t b = blockIdx.x;
   if (b == 0) return;  // block 0 enters with s = 0
-  const U256 cin = ldr(totals + 4 * b);
+  const U256 cin = u256_from_u64(totals + 4 * b);
   const uint64_t k0 = b * HS_BLK + (uint64_t)threadIdx.x * HS_PER;
   if (k0 >= L) return;
   U256 zk = fr_pow(z, (uint64_t)threadIdx.x * HS_PER + 1);
@@ -498,7 +500,7 @@ __global__ void __launch_bounds__(HS_T) k_hs3(uint64_t* q, uint64_t L, U256 z, c
     const uint64_t k = k0 + m;
     if (k >= L) break;
     uint64_t* dst = k + 1 < L ? q + 4 * (L - 2 - k) : rem;
-    str(dst, Fr::add(ldr(dst), Fr::mul(zk, cin)));
+    u256_to_u64(Fr::add(u256_from_u64(dst), Fr::mul(zk, cin)), dst);
     zk = Fr::mul(zk, z);
   }
 }
@@ -747,7 +749,7 @@ struct Prover {
     HsArgs a;
     a.p = p;
     a.L = L;
-    a.y = y;
+    a.y = Fr::from_mont(y);
     a.z = z;
     for (int j = 0; j < HS_LOG_T; ++j) a.zs[j] = hpow64(z, (uint64_t)HS_PER << j);
     hipLaunchKernelGGL(k_hs1, dim3((uint32_t)nb), dim3(HS_T), 0, s, a, q, totals, rem);
