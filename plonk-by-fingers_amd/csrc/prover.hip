@@ -154,10 +154,10 @@ __global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n
     for (int k = 0; k < 4; ++k) sigma[4 * id + k] = 0;
     return;
   }
-  U256 h = ldr(hpow + 4 * (idx - 1));
+  U256 h = u256_from_u64(hpow + 4 * (idx - 1));  // canonical; k1, k2 Montgomery: products canonical
   if (kind == 1) h = Fr::mul(h, k1);
   if (kind == 2) h = Fr::mul(h, k2);
-  str(sigma + 4 * id, h);
+  u256_to_u64(h, sigma + 4 * id);
 }
 
 // Constrains::satisfies (constraints.rs:198-230, with its q_l * b term): gates and copies
