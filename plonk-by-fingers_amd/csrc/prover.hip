@@ -849,7 +849,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // PLONK proving key holds -- validated by fingerprints of d_q and d_copies on every call.
   // PBF_PROVER_NO_PK=1 recomputes them per proof, as the reference does (plonk.rs:233-243,
   // 339-370).
-  const bool pk_on = P.G == 1 && !getenv("PBF_PROVER_NO_PK");
+  const bool pk_on = !getenv("PBF_PROVER_NO_PK");  // sharded too: this rank's coset blocks
   bool pk_hit = false;
   uint64_t* pkcoef = nullptr;
   uint64_t* pkcoset = nullptr;
@@ -859,11 +859,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     if ((rc = fingerprint_words(ctx, d_q, 20 * (uint64_t)n, s, &fq)) ||
         (rc = fingerprint_words(ctx, d_copies, 6 * (uint64_t)n, s, &fc)))
       return rc;
-    pk_key = {(uint64_t)n, fq, fc};
+    pk_key = {(uint64_t)n, fq, fc, (uint64_t)P.G, (uint64_t)P.rank};
     for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
     DevBuf& kc = ctx->buf("pk.coef");
     DevBuf& ks = ctx->buf("pk.coset");
-    if ((rc = kc.ensure(8 * CS * E)) || (rc = ks.ensure(9 * N * E))) return rc;
+    if ((rc = kc.ensure(8 * CS * E)) || (rc = ks.ensure(9 * P.count() * E))) return rc;
     pkcoef = (uint64_t*)kc.p;
     pkcoset = (uint64_t*)ks.p;
     pk_hit = ctx->pk_key == pk_key;
@@ -871,7 +871,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   }
   if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure(3 * n * E)) || (rc = B.coef.ensure(11 * (n + 8) * E)) ||
       (rc = B.acc.ensure((n + 8) * E)) || (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure(n * E)) ||
-      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure((pk_on ? 4 : 14) * P.count() * E)) ||
+      (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure((pk_on ? 5 : 14) * P.count() * E)) ||
       (rc = B.t.ensure(N * E)) || (rc = B.work.ensure(3 * N * E)) || (rc = B.flag.ensure(64)) ||
       (rc = B.evals.ensure(16 * E)))
     return rc;
@@ -895,7 +895,9 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   const uint64_t NE = P.count();  // coset evaluations held here (N; nl = N / G when sharded)
   uint64_t* ceslot[14];
   for (int k = 0; k < 14; ++k)
-    ceslot[k] = (pk_on && k >= 4 && k <= 12) ? pkcoset + 4 * NE * (k - 4) : coset + 4 * NE * k;
+    ceslot[k] = (pk_on && k >= 4 && k <= 12) ? pkcoset + 4 * NE * (k - 4)
+                : (pk_on && k == 13)        ? coset + 4 * NE * 4  // z(w x) after a b c z
+                                            : coset + 4 * NE * k;
   auto CE = [&](int k) { return ceslot[k]; };
   // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1 [13 z(w x), sharded]
   uint64_t* work = (uint64_t*)B.work.p;
@@ -1009,8 +1011,12 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     // sharded: z(w x) gets its own slot (coefficients z_j w^j) instead of reading z at index i+4,
     // which may sit in another rank's block
     srcs[13] = zx; lens[13] = n + 3; bases[13] = Fr::mul(P.g, P.omega);
-    if (pk_on) {  // a b c z per proof; the 9 circuit slots once per proving key
-      if ((rc = P.coset_ntt_batch(4, srcs, lens, bases, CE(0), QUOT_DEG))) return rc;
+    if (pk_on) {  // a b c z (and z(w x) when sharded) per proof, all canonical; the 9 circuit
+                  // slots once per proving key
+      const uint64_t* ps[5] = {srcs[0], srcs[1], srcs[2], srcs[3], srcs[13]};
+      const uint64_t pl[5] = {lens[0], lens[1], lens[2], lens[3], lens[13]};
+      const U256 pb[5] = {bases[0], bases[1], bases[2], bases[3], bases[13]};
+      if ((rc = P.coset_ntt_batch(P.G > 1 ? 5 : 4, ps, pl, pb, CE(0)))) return rc;
       if (!pk_hit) {
         if ((rc = P.coset_ntt_batch(9, srcs + 4, lens + 4, bases + 4, CE(4), QUOT_DEG + 4))) return rc;
         ctx->pk_key = pk_key;
