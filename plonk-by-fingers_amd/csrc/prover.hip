@@ -164,9 +164,12 @@ __global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n
 __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64_t* copies, uint64_t n, int* bad) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const U256 ql = ldr(q + 4 * i), qo = ldr(q + 4 * (2 * n + i)), qm = ldr(q + 4 * (3 * n + i)),
-             qc = ldr(q + 4 * (4 * n + i));
-  const U256 a = ldr(abc + 4 * i), b = ldr(abc + 4 * (n + i)), c = ldr(abc + 4 * (2 * n + i));
+  // every term at R-degree -1 (the zero test does not depend on the degree): canonical
+  // products of two canonical values; q_m lifted to degree 1, q_c lowered to -1
+  auto ld = [](const uint64_t* p) { return u256_from_u64(p); };
+  const U256 ql = ld(q + 4 * i), qo = ld(q + 4 * (2 * n + i)), qm = Fr::to_mont(ld(q + 4 * (3 * n + i))),
+             qc = Fr::from_mont(ld(q + 4 * (4 * n + i)));
+  const U256 a = ld(abc + 4 * i), b = ld(abc + 4 * (n + i)), c = ld(abc + 4 * (2 * n + i));
   U256 r = Fr::add(Fr::mul(ql, a), Fr::mul(ql, b));
   r = Fr::add(r, Fr::mul(qo, c));
   r = Fr::add(r, Fr::mul(Fr::mul(qm, a), b));
