@@ -639,7 +639,7 @@ struct Prover {
     if (bad) return fail(PBF_EINVAL, what);
     return 0;
   }
-  int ntt(const uint64_t* w, uint64_t* in, uint64_t* out, uint64_t size, uint64_t batch, int inverse) {
+  int ntt(const uint64_t* w, const uint64_t* in, uint64_t* out, uint64_t size, uint64_t batch, int inverse) {
     return pbf_ntt_fr256_batch_dev(ctx, w, in, out, size, batch, inverse, s);
   }
 
@@ -923,16 +923,19 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
   PBF_HIP(hipMemsetAsync(coef, 0, (pk_on ? 3 : 11) * CS * E, s));
   if (pk_on && !pk_hit) PBF_HIP(hipMemsetAsync(pkcoef, 0, 8 * CS * E, s));
+  // a b c: one batched INTT of the (contiguous) witness columns into the work buffer, then
+  // into their padded coefficient slots
+  if ((rc = P.ntt(P.w_plain, d_abc, W0, n, 3, 1))) return rc;
   for (int k = 0; k < 3; ++k)
-    PBF_HIP(hipMemcpyAsync(C(k), d_abc + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    PBF_HIP(hipMemcpyAsync(C(k), W0 + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
   if (!pk_hit) {
     for (int k = 0; k < 5; ++k)
       PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
     for (int k = 0; k < 3; ++k)
       PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    for (int k = 3; k < 11; ++k)
+      if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
   }
-  for (int k = 0; k < (pk_hit ? 3 : 11); ++k)
-    if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
   P.mark(pk_hit ? "interpolate (3 INTT, key)" : "interpolate (11 INTT)");
   // ---- round 1: a(x) = (b2 + b1 x)(x^n - 1) + f_a(x), likewise b, c (plonk.rs:250-252)
   for (int k = 0; k < 3; ++k) {
