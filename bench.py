@@ -29,7 +29,12 @@ import pbf  # noqa: E402
 
 GOLD = pbf.GOLDILOCKS
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FQ_MUL_PEAK = 1.0e11  # BN254 Fq Montgomery products/s, all CUs (scripts/ubench/pairing_lat.hip k_tput)
+# BN254 Fq Montgomery products/s of the whole chip at the instruction level: a product is
+# 136 v_mad_u64_u32 + 136 carry folds (csrc/fp256.hpp), 4 cycles per wave-instruction each
+# (profiles/r02/valu_rates.log), 64 lanes, 1024 SIMDs at 2.4 GHz. (scripts/ubench/
+# pairing_lat.hip k_tput measures 1.0e11 with two chains per lane; the MSM accumulation
+# reaches 1.2e11, so the measured figure is not the ceiling.)
+FQ_MUL_PEAK = 1024 * 2.4e9 * 64 / (272 * 4)
 
 
 def root_of_unity(n: int) -> int:
@@ -459,16 +464,16 @@ def other_configs(ctx, sp) -> dict:
     torch.cuda.synchronize()
     t = _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp))
     # compute roofline of the MSM: 16 m mixed XYZZ additions of 10 Fq products each (the
-    # accumulation; the bucket reduction adds < 1 %) against the measured Fq-product
-    # throughput of the chip (scripts/ubench/pairing_lat.hip k_tput: every lane of a full grid
-    # running independent Fq products, 9.7-10.2e10/s on MI355X)
+    # accumulation; the bucket reduction adds < 1 %) against the chip's instruction-level
+    # Fq-product rate (FQ_MUL_PEAK, 1.45e11/s)
     fq_products = 16 * m * 10
 
     def msm_roof(ms):
         ach = fq_products / (ms / 1e3)
         return {"bound": "valu (Fq products)", "achieved": ach, "peak": FQ_MUL_PEAK, "unit": "Fq products/s",
                 "frac": ach / FQ_MUL_PEAK, "fq_products": fq_products,
-                "peak_source": "scripts/ubench/pairing_lat.hip k_tput (measured)"}
+                "peak_source": "instruction count: 272 four-cycle VALU per Fq product, 1024 SIMDs x 64 lanes "
+                               "at 2.4 GHz (k_tput measures 1.0e11; the accumulation kernel alone reaches 1.2e11)"}
 
     res["config4_bn254_msm_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3), roofline=msm_roof(t["ms"]),
                                          note="Pippenger c=16, 16 windows (bucket accumulation, window sums, "
