@@ -206,6 +206,9 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   const uint64_t stride = (a.n >> LOGR) + a.in_pad;
 
   // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
+#ifdef PBF_GL_SETPRIO
+  __builtin_amdgcn_s_setprio(3);  // A/B: issue this tile's loads ahead of other waves' math
+#endif
   uint64_t v[16];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -255,6 +258,9 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #endif
     }
   }
+#ifdef PBF_GL_SETPRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   if constexpr (PERSIST) gl_bar<true>();  // raw tile consumed before Z overwrites it
 #pragma unroll
   for (int u = 0; u < 4; ++u) PBF_GL_MATH((dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f)));
