@@ -16,11 +16,15 @@
  *     the context's host stream. `_dev` entry points take device pointers and a
  *     hipStream_t (void*) and are stream-ordered on that stream (NULL = the HIP null
  *     stream, as everywhere in HIP): their work starts after everything enqueued on
- *     it before the call and finishes before anything enqueued after. Internally a
- *     batched Goldilocks NTT of >= 8 polynomials (pbf_ntt_u64_batch_dev) forks half
- *     its groups onto a stream private to the context (an event fork/join pair, also
- *     the context's) and joins back before returning; nothing else is ever enqueued
- *     on streams the caller did not pass.
+ *     it before the call and finishes before anything enqueued after. Two entry points
+ *     also use streams private to the context, always joined back by events on the
+ *     caller's stream before they return: a batched Goldilocks NTT of >= 8 polynomials
+ *     (pbf_ntt_u64_batch_dev) forks half its groups onto a second stream, and the
+ *     fixed-base MSM (pbf_msm_g1_bn254_fixed_dev, and the commitments inside
+ *     pbf_plonk_prove_bn254*) runs its bucket join and reduction on a side stream while
+ *     the caller's stream goes on; the fixed-base MSM, prove and verify order the
+ *     caller's stream after that side stream (an event wait) before returning. Nothing
+ *     else is ever enqueued on streams the caller did not pass.
  *   - Input and output may alias (in-place is allowed).
  *   - Supported moduli for the u64 entry points: Goldilocks p = 2^64-2^32+1, and any
  *     odd M < 2^32 (the range where the reference's `(a*b)%M` in u64 is exact,
@@ -60,6 +64,11 @@ const char* pbf_last_error(void);
  * non-blocking stream created with the context). `_dev` calls ignore it.     */
 int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream);
 int pbf_device_sync(pbf_ctx* ctx);
+/* Frees the context's derived caches -- the prover's proving key, the verifier's
+ * verification key, the fixed-base MSM window table, the pairing check's prepared lines
+ * and the device copies that validate them -- after waiting for the context's streams.
+ * The next call that needs one rebuilds it. Plans and scratch buffers stay.   */
+int pbf_ctx_release_caches(pbf_ctx* ctx);
 
 /* ---- FFT trait ------------------------------------------------------------ */
 /* CooleyTurkey::new(EvaluationDomainGenerator{omega, size: n}) + fft / fft_inv
@@ -162,9 +171,10 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
                          uint64_t* out, void* stream);
 /* The same sum against a FIXED base set (KZG commitments: the SRS): out = sum_{i<n}
  * scalars[i] * points[i], n <= n_points. The first call for a base set precomputes its
- * window table 2^(16w) P_i (16 x n_points affine points, cached in the context and
- * revalidated by a device fingerprint of the points on every call, so rewriting the points
- * in place is safe); then every (point, window) digit shares one set of 2^15 buckets.     */
+ * window table 2^(16w) P_i (16 x n_points affine points, cached in the context with a
+ * device copy of the points it was built from, and revalidated against that copy word for
+ * word on every call, so rewriting the points in place is safe); then every (point,
+ * window) digit shares one set of 2^15 buckets.                                           */
 int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
                                size_t n, uint64_t* out, void* stream);
 /* out_i = scalars_i * G (G = (1, 2)), device pointers                               */
@@ -213,10 +223,13 @@ int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_t* scalars,
  * Errors: PBF_EINVAL for an unsatisfied circuit (constraints.rs:198), a zero permutation
  * denominator (plonk.rs:297), a non-divisible quotient (plonk.rs:370), short SRS.
  * Keys: the context keeps the circuit's preprocessed polynomials (q_*, s_sigma_*, l1:
- * coefficients and coset evaluations, ~0.6 KiB per gate; single-GPU prove) and the
- * verifier's 8 preprocessed commitments, checked against 64-bit fingerprints of q /
- * copies (and the SRS for verify) on every call and rebuilt when they differ. Outputs
- * are identical either way; PBF_PROVER_NO_PK=1 / PBF_VERIFIER_NO_VK=1 disable the keys.  */
+ * 8 coefficient slots of n+8 and 9 coset slots of 4n (of 4n/world when sharded) Fr
+ * elements, ~1.4 KiB per gate, ~23.6 GB at 2^24 gates on one GPU) and the verifier's 8
+ * preprocessed commitments, plus device copies of the q / copies (and, for verify, SRS)
+ * arrays they were built from (~0.2 KiB per gate each); every call compares its inputs
+ * with those copies word for word and rebuilds on any difference. Outputs are identical
+ * either way; PBF_PROVER_NO_PK=1 / PBF_VERIFIER_NO_VK=1 disable the keys, and
+ * pbf_ctx_release_caches frees them (and the MSM window table) between circuits.        */
 int pbf_plonk_prove_bn254(pbf_ctx* ctx, size_t n, const uint64_t* q, const uint64_t* copies, const uint64_t* abc,
                           const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* srs,
                           size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f);

@@ -92,6 +92,27 @@ void pbf_ctx_destroy(pbf_ctx* ctx) {
   delete ctx;
 }
 
+int pbf_ctx_release_caches(pbf_ctx* ctx) {
+  if (!ctx) return fail(PBF_EINVAL, "null ctx");
+  PBF_HIP(hipSetDevice(ctx->device));
+  PBF_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->msm_tail.aux) PBF_HIP(hipStreamSynchronize(ctx->msm_tail.aux));
+  PBF_HIP(hipDeviceSynchronize());  // _dev callers' streams may still read the caches
+  ctx->pk_key.clear();
+  ctx->vk_key.clear();
+  ctx->vk_pts.clear();
+  ctx->pair_g2_key.clear();
+  ctx->fixed_base.valid = false;
+  ctx->fixed_base.n = 0;
+  ctx->fixed_base.table.release();
+  ctx->fixed_base.inf.release();
+  for (const char* name : {"pk.coef", "pk.coset", "pc.lines", "pc.qinf"}) ctx->named.erase(name);
+  for (auto it = ctx->named.begin(); it != ctx->named.end();)
+    it = it->first.compare(0, 5, "snap.") == 0 ? ctx->named.erase(it) : std::next(it);
+  ctx->snap_words.clear();
+  return PBF_OK;
+}
+
 int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream) {
   if (!ctx) return fail(PBF_EINVAL, "null ctx");
   ctx->user_stream = (hipStream_t)stream;

@@ -50,6 +50,7 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   int ensure(size_t need);
+  void release();  // frees the allocation (ensure() allocates again)
   ~DevBuf();
 };
 
@@ -146,8 +147,8 @@ struct pbf_ctx {
   pbf::ForkSet fork;  // aux streams of the NTT group schedule (this context only)
   // fixed-base MSM window table (msm.hip msm_fixed_table): the points it was built from
   struct FixedBase {
-    const void* ptr = nullptr;
-    uint64_t n = 0, fingerprint = 0;
+    bool valid = false;  // built from the points in snapshot "fx.pts" (msm.hip snapshot_check)
+    uint64_t n = 0;
     pbf::DevBuf table;
     pbf::DevBuf inf;  // per point: 1 = the identity (contributes nothing)
   } fixed_base;
@@ -165,13 +166,18 @@ struct pbf_ctx {
     if (!b) b.reset(new pbf::DevBuf());
     return *b;
   }
+  // snapshots of cache inputs (msm.hpp snapshot_check): device copies in buf("snap." + name),
+  // their lengths in u64 words here
+  std::map<std::string, uint64_t> snap_words;
   // pairing check: the G2 inputs whose prepared lines sit in buf("pc.lines") (pairing.hip)
   std::vector<uint64_t> pair_g2_key;
   // prover proving key: the preprocessed polynomials' coefficients and coset evaluations
-  // in buf("pk.coef") / buf("pk.coset"), valid for this key (n, fingerprints, k1 k2)
+  // in buf("pk.coef") / buf("pk.coset"), valid for this key (n, world, rank, k1 k2) while the
+  // gates and copies equal their snapshots "pk.q" / "pk.copies"
   std::vector<uint64_t> pk_key;
   // verifier verification key: the 8 preprocessed commitments (vk_pts, 8 x 8 u64) of the
-  // circuit and SRS in vk_key (n, fingerprints of q, copies and the SRS, k1 k2)
+  // circuit and SRS in vk_key (n, srs_m, k1 k2) while q, copies and the SRS equal their
+  // snapshots "vk.q" / "vk.copies" / "vk.srs"
   std::vector<uint64_t> vk_key, vk_pts;
   pbf::MsmTail msm_tail;  // destroyed before `named`: its stream drains first
 };

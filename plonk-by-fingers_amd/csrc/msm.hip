@@ -427,37 +427,13 @@ __global__ void __launch_bounds__(16) msm_fx_total(const Xyzz* sub, Xyzz* out) {
   fx_tree(sub[blockIdx.x * 16 + threadIdx.x], out + blockIdx.x);
 }
 
-// 64-bit fingerprint of n canonical affine points (8 u64 each): block XORs of a position-
-// mixed hash, then one block folds them (validates a cached table against the points)
-__device__ __forceinline__ uint64_t fp_mix(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-__global__ void __launch_bounds__(256) msm_fingerprint(const uint64_t* pts, uint64_t words, uint64_t* partial) {
-  __shared__ uint64_t red[256];
-  uint64_t h = 0;
+// Exact-content cache validation (snapshot_check below): diff[0] = 1 when a and b differ in
+// any of their `words` u64 (benign same-value race; vector stores only).
+__global__ void __launch_bounds__(256) k_snap_compare(const uint64_t* a, const uint64_t* b, uint64_t words, int* diff) {
+  uint64_t d = 0;
   for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < words; j += (uint64_t)gridDim.x * 256)
-    h ^= fp_mix(pts[j] + 0x9E3779B97F4A7C15ull * (j + 1));
-  red[threadIdx.x] = h;
-  __syncthreads();
-  for (uint32_t st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st) red[threadIdx.x] ^= red[threadIdx.x + st];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
-}
-__global__ void __launch_bounds__(256) msm_fingerprint_fold(const uint64_t* partial, uint32_t count, uint64_t* out) {
-  __shared__ uint64_t red[256];
-  uint64_t h = 0;
-  for (uint32_t j = threadIdx.x; j < count; j += 256) h ^= partial[j];
-  red[threadIdx.x] = h;
-  __syncthreads();
-  for (uint32_t st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st) red[threadIdx.x] ^= red[threadIdx.x + st];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = red[0];
+    d |= a[j] ^ b[j];
+  if (d) diff[0] = 1;
 }
 
 // Fixed-base comb for s * G (SRS::create): table[w][d-1] = d * 2^(8w) * G (affine,
@@ -624,37 +600,61 @@ static void msm_finish_host(const Xyzz* sums, uint64_t* out) {
   }
 }
 
-// ---- fixed-base tables: cached per context, validated by a fingerprint of the points
-constexpr uint32_t FP_BLOCKS = 1024;
-
-int fingerprint_words(pbf_ctx* ctx, const uint64_t* d_words, uint64_t words, hipStream_t s, uint64_t* out) {
-  DevBuf& fp = ctx->buf("msm.fp");
-  int rc = fp.ensure((FP_BLOCKS + 1) * 8);
+// ---- context caches validated by exact content (the 64-bit XOR fingerprint they
+// used before is linear over GF(2), so a chosen circuit or point set could collide with a cached
+// one). The context keeps a device copy -- a snapshot -- of every input a cache is derived from;
+// a hit requires the input to equal its snapshot word for word.
+int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bool* same) {
+  DevBuf& fl = ctx->buf("snap.flags");
+  int rc = fl.ensure((size_t)k * sizeof(int));
   if (rc) return rc;
-  uint64_t* part = (uint64_t*)fp.p;
-  hipLaunchKernelGGL(msm_fingerprint, dim3(FP_BLOCKS), dim3(256), 0, s, d_words, words, part);
-  hipLaunchKernelGGL(msm_fingerprint_fold, dim3(1), dim3(256), 0, s, (const uint64_t*)part, FP_BLOCKS, part + FP_BLOCKS);
+  int* flags = (int*)fl.p;
+  PBF_HIP(hipMemsetAsync(flags, 0, (size_t)k * sizeof(int), s));
+  std::vector<int> fresh(k, 0), diff(k, 0);
+  for (int i = 0; i < k; ++i) {
+    DevBuf& b = ctx->buf(std::string("snap.") + items[i].name);
+    auto it = ctx->snap_words.find(items[i].name);
+    if (!b.p || it == ctx->snap_words.end() || it->second != items[i].words) {
+      fresh[i] = 1;
+      continue;
+    }
+    if (items[i].words == 0) continue;
+    uint64_t blocks = (items[i].words + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_snap_compare, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint64_t*)b.p, items[i].p,
+                       items[i].words, flags + i);
+  }
   PBF_HIP(hipGetLastError());
-  PBF_HIP(hipMemcpyAsync(out, part + FP_BLOCKS, 8, hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipMemcpyAsync(diff.data(), flags, (size_t)k * sizeof(int), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));
+  *same = true;
+  for (int i = 0; i < k; ++i) {
+    if (!fresh[i] && !diff[i]) continue;
+    *same = false;
+    DevBuf& b = ctx->buf(std::string("snap.") + items[i].name);
+    ctx->snap_words.erase(items[i].name);  // valid again only once the copy is enqueued
+    if ((rc = b.ensure(items[i].words * 8 + 8))) return rc;
+    if (items[i].words) PBF_HIP(hipMemcpyAsync(b.p, items[i].p, items[i].words * 8, hipMemcpyDeviceToDevice, s));
+    ctx->snap_words[items[i].name] = items[i].words;
+  }
   return 0;
 }
-static int msm_fingerprint_host(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, uint64_t* out) {
-  return fingerprint_words(ctx, d_pts, 8 * n, s, out);
-}
 
-// the window table of the n points at d_pts (built on first use; rebuilt when the points at
-// that address changed); the table's identity flags are kept with it (fixed_base.inf)
+// the window table of the n points at d_pts (built on first use; rebuilt when the points
+// differ from the ones it was built from, wherever they live); the table's identity flags are
+// kept with it (fixed_base.inf)
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
   if (n == 0 || n > 0x7FFFFFFFull / FX_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
-  uint64_t fp = 0;
-  int rc = msm_fingerprint_host(ctx, d_pts, n, s, &fp);
+  const SnapItem it{"fx.pts", d_pts, 8 * n};
+  bool same = false;
+  int rc = snapshot_check(ctx, &it, 1, s, &same);
   if (rc) return rc;
   auto& fb = ctx->fixed_base;
-  if (fb.ptr == (const void*)d_pts && fb.n == n && fb.fingerprint == fp && fb.table.p) {
+  if (same && fb.valid && fb.n == n && fb.table.p) {
     *out = (const Affine*)fb.table.p;
     return 0;
   }
+  fb.valid = false;
   if ((rc = fb.table.ensure((uint64_t)FX_NW * n * sizeof(Affine))) || (rc = fb.inf.ensure(n))) return rc;
   Affine* tbl = (Affine*)fb.table.p;
   hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, tbl, (uint8_t*)fb.inf.p, n);
@@ -662,23 +662,33 @@ int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t
     hipLaunchKernelGGL(msm_table_window, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
                        (const Affine*)(tbl + (uint64_t)(w - 1) * n), tbl + (uint64_t)w * n, n);
   PBF_HIP(hipGetLastError());
-  fb.ptr = d_pts;
   fb.n = n;
-  fb.fingerprint = fp;
+  fb.valid = true;
   *out = tbl;
   return 0;
 }
 
-// the context's window table if it was built from exactly these points (fingerprint
-// checked), else null; never builds one
+// the context's window table if it was built from exactly these points (content checked),
+// else null; never builds one
 int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
   *out = nullptr;
   auto& fb = ctx->fixed_base;
-  if (fb.ptr != (const void*)d_pts || fb.n != n || !fb.table.p) return 0;
-  uint64_t fp = 0;
-  int rc = msm_fingerprint_host(ctx, d_pts, n, s, &fp);
+  if (!fb.valid || fb.n != n || !fb.table.p) return 0;
+  auto w = ctx->snap_words.find("fx.pts");
+  if (w == ctx->snap_words.end() || w->second != 8 * n) return 0;
+  DevBuf& fl = ctx->buf("snap.flags");
+  int rc = fl.ensure(sizeof(int));
   if (rc) return rc;
-  if (fp == fb.fingerprint) *out = (const Affine*)fb.table.p;
+  PBF_HIP(hipMemsetAsync(fl.p, 0, sizeof(int), s));
+  uint64_t blocks = (8 * n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_snap_compare, dim3((uint32_t)blocks), dim3(256), 0, s,
+                     (const uint64_t*)ctx->buf("snap.fx.pts").p, d_pts, 8 * n, (int*)fl.p);
+  PBF_HIP(hipGetLastError());
+  int diff = 0;
+  PBF_HIP(hipMemcpyAsync(&diff, fl.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  PBF_HIP(hipStreamSynchronize(s));
+  if (!diff) *out = (const Affine*)fb.table.p;
   return 0;
 }
 
@@ -856,7 +866,8 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
 }
 
 // SRS::eval_at_s against a fixed base set (KZG commitments): the first call for a base set
-// builds its window table (cached in the context, revalidated by a fingerprint each call)
+// builds its window table (cached in the context, revalidated against a device copy of the
+// points on every call)
 int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
                                size_t n, uint64_t* out, void* stream) {
   if (!ctx || !out || (n && (!d_points || !d_scalars))) return fail(PBF_EINVAL, "null argument");

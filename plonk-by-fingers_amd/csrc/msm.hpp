@@ -6,9 +6,10 @@
 namespace pbf {
 
 // Window table (16 x n affine points, Montgomery) of the n canonical affine points at d_pts,
-// cached in the context and revalidated by a fingerprint of the points (one stream sync).
+// cached in the context and revalidated against a device copy of the points (one compare
+// kernel and one stream sync per call; rebuilt when they differ).
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out);
-// The cached table of exactly these points (fingerprint checked), or null (nothing built).
+// The cached table of exactly these points (content checked), or null (nothing built).
 int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out);
 // sum_{i<n} scalars[i] * P_(first+i) against a table of n_table points; the XYZZ result
 // (Montgomery) is written to *d_result by the context's side stream (see msm_fixed_wait);
@@ -18,9 +19,16 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
 // Orders stream s after every fixed-base MSM tail enqueued on this context so far (call
 // before reading a d_result of msm_fixed_device on s).
 int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s);
-// 64-bit fingerprint of `words` u64 at d_words (position-mixed XOR hash; one stream sync):
-// validates context caches against their inputs
-int fingerprint_words(pbf_ctx* ctx, const uint64_t* d_words, uint64_t words, hipStream_t s, uint64_t* out);
+// Exact-content validation of context caches: *same = every item's `words` u64 equal the
+// context's snapshot named `name` (same length, word for word). Items that differ (or have no
+// snapshot yet) get their snapshot replaced by a device copy of the input, so the caller
+// rebuilds its cache from these inputs. One compare kernel per item, one stream sync in all.
+struct SnapItem {
+  const char* name;
+  const uint64_t* p;
+  uint64_t words;
+};
+int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bool* same);
 // canonical affine (x, y as 4 + 4 little-endian u64; identity (0, 0)) of an XYZZ point
 void xyzz_to_affine_u64(const Xyzz& p, uint64_t* out);
 

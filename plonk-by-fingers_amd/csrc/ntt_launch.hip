@@ -1,6 +1,7 @@
 // Kernel instantiation, NTT planning and launchers for libpbf.so (gfx950).
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include "internal.hpp"
 #include "ntt_gl.hpp"
 
@@ -43,9 +44,12 @@ int DevBuf::ensure(size_t need) {
   bytes = need;
   return 0;
 }
-DevBuf::~DevBuf() {
+void DevBuf::release() {
   if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
 }
+DevBuf::~DevBuf() { release(); }
 
 static int upload(DevBuf& b, const std::vector<uint64_t>& v) {
   int rc = b.ensure(v.size() * 8);
@@ -377,21 +381,29 @@ int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, u
 
 // Persistent grid: every resident workgroup slot once (blocks per CU from the
 // occupancy query x CUs), never more than there are tiles.
+// The answer depends only on the kernel, the block size and the device, never on a context's
+// state, so one process-wide table under a lock serves every context (pbf.h: contexts share
+// no mutable state a caller could observe).
 static uint32_t persistent_grid(const void* fn, int nt, uint64_t tiles) {
-  static std::map<std::pair<const void*, int>, uint32_t> cache;
-  auto key = std::make_pair(fn, nt);
-  auto it = cache.find(key);
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, int>, uint32_t> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const auto key = std::make_tuple(fn, nt, dev);
   uint32_t slots;
-  if (it != cache.end()) {
-    slots = it->second;
-  } else {
-    int dev = 0, cus = 256, per_cu = 1;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    slots = (uint32_t)(cus * per_cu);
-    cache[key] = slots;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      slots = it->second;
+    } else {
+      int cus = 256, per_cu = 1;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+      slots = (uint32_t)(cus * per_cu);
+      cache[key] = slots;
+    }
   }
   const char* env = getenv("PBF_NTT_GRID_MULT");  // A/B: oversubscribe the persistent grid
   if (env) slots *= (uint32_t)atoi(env);

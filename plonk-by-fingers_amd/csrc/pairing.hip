@@ -943,6 +943,7 @@ int pbf::pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_
   auto& key = ctx->pair_g2_key;
   const bool hit = key.size() == 16 * n && memcmp(key.data(), g2, n * 128) == 0 && cl.p && cq.p;
   if (!hit) {
+    key.clear();  // the lines are rewritten below; a failure in between must not leave a stale hit
     if ((rc = cl.ensure(n * NSTEP * sizeof(PrepLine))) || (rc = cq.ensure(n))) return rc;
     PBF_HIP(hipMemcpyAsync(b2.p, g2, n * 128, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(prep_lines_kernel, dim3((uint32_t)n), dim3(PT), 0, s, (const uint64_t*)b2.p, n,

@@ -202,21 +202,19 @@ bool g1_valid(const uint32_t* p) {
   return p[0] < pbh::P && p[1] < pbh::P && pbh::pw(p[1], 2, pbh::P) == (pbh::pw(p[0], 3, pbh::P) + 3) % pbh::P;
 }
 
-// Device round trip helper: copy n*w words in, launch, copy back.
+// Device round trip helper: copy n*w words in, launch, copy back. The buffers are the
+// context's own named buffers (freed by pbf_ctx_destroy), so contexts share nothing.
 struct Dev {
-  pbf::DevBuf a, b, c, d;
+  pbf::DevBuf &a, &b, &c, &d;
 };
-Dev& dev_for(pbf_ctx* ctx) {
-  static std::map<pbf_ctx*, std::unique_ptr<Dev>> m;
-  auto& p = m[ctx];
-  if (!p) p.reset(new Dev());
-  return *p;
+Dev dev_for(pbf_ctx* ctx) {
+  return Dev{ctx->buf("pbh.a"), ctx->buf("pbh.b"), ctx->buf("pbh.c"), ctx->buf("pbh.d")};
 }
 
 int gpu_g1_mul(pbf_ctx* ctx, const std::vector<uint32_t>& pts, const std::vector<uint32_t>& s, std::vector<uint32_t>& out) {
   const uint32_t n = (uint32_t)s.size();
   if (n == 0) { out.clear(); return 0; }
-  Dev& d = dev_for(ctx);
+  Dev d = dev_for(ctx);
   int rc;
   if ((rc = d.a.ensure(pts.size() * 4)) || (rc = d.b.ensure(s.size() * 4)) || (rc = d.c.ensure(pts.size() * 4))) return rc;
   hipStream_t st = ctx->host_stream();
@@ -233,7 +231,7 @@ int gpu_g1_mul(pbf_ctx* ctx, const std::vector<uint32_t>& pts, const std::vector
 
 int gpu_msm(pbf_ctx* ctx, const std::vector<uint32_t>& pts, const std::vector<uint32_t>& s, uint32_t out[3]) {
   const uint32_t n = (uint32_t)s.size();
-  Dev& d = dev_for(ctx);
+  Dev d = dev_for(ctx);
   int rc;
   if ((rc = d.a.ensure(pts.size() * 4 + 4)) || (rc = d.b.ensure(s.size() * 4 + 4)) || (rc = d.c.ensure(16))) return rc;
   hipStream_t st = ctx->host_stream();
@@ -251,7 +249,7 @@ int gpu_msm(pbf_ctx* ctx, const std::vector<uint32_t>& pts, const std::vector<ui
 
 int gpu_pairing(pbf_ctx* ctx, const std::vector<uint32_t>& g1, const std::vector<uint32_t>& g2, std::vector<uint32_t>& out) {
   const uint32_t n = (uint32_t)(g2.size() / 2);
-  Dev& d = dev_for(ctx);
+  Dev d = dev_for(ctx);
   int rc;
   if ((rc = d.a.ensure(g1.size() * 4 + 4)) || (rc = d.b.ensure(g2.size() * 4 + 4)) || (rc = d.c.ensure(g2.size() * 4 + 4)))
     return rc;
@@ -393,7 +391,7 @@ int pbf_pbh_pairing(pbf_ctx* ctx, const uint32_t* g1, const uint32_t* g2, size_t
 
 int pbf_pbh_g2_mul(pbf_ctx* ctx, const uint32_t* pts, const uint32_t* scalars, size_t n, uint32_t* out) {
   if (!ctx || (n && (!pts || !scalars || !out))) return fail(PBF_EINVAL, "null argument");
-  Dev& d = dev_for(ctx);
+  Dev d = dev_for(ctx);
   int rc;
   if ((rc = d.a.ensure(n * 8 + 8)) || (rc = d.b.ensure(n * 4 + 4)) || (rc = d.c.ensure(n * 8 + 8)) || (rc = d.d.ensure(4)))
     return rc;
@@ -414,7 +412,7 @@ int pbf_pbh_g2_mul(pbf_ctx* ctx, const uint32_t* pts, const uint32_t* scalars, s
 
 int pbf_pbh_gt_pow(pbf_ctx* ctx, const uint32_t* x, const uint32_t* e, size_t n, uint32_t* out) {
   if (!ctx || (n && (!x || !e || !out))) return fail(PBF_EINVAL, "null argument");
-  Dev& d = dev_for(ctx);
+  Dev d = dev_for(ctx);
   int rc;
   if ((rc = d.a.ensure(n * 8 + 8)) || (rc = d.b.ensure(n * 4 + 4)) || (rc = d.c.ensure(n * 8 + 8))) return rc;
   hipStream_t st = ctx->host_stream();

@@ -23,6 +23,7 @@
 //
 // Field elements at rest in HBM: canonical Fr, 4 x u64 little-endian (the ABI layout);
 // kernels convert to Montgomery on load and back on store.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -719,25 +720,19 @@ struct Prover {
   // SRS::eval_at_s (plonk.rs:51-58) as a fixed-base MSM against the SRS window table
   // (msm.hpp), its XYZZ result left in device slot `slot` (finish_commits collects all of
   // them with one copy: the challenges are inputs, nothing waits on a commitment). Sharded:
-  // this rank's point range; the G partial sums are all-gathered into the slot's G entries.
+  // this rank's point range, its partial sum left in slot `slot` too; finish_commits
+  // all-gathers the partials of every commitment at once, so no commitment's tail (bucket
+  // join and reduction on the MSM side stream) is waited for before the end of the proof.
   const Affine* srs_tbl = nullptr;
   uint64_t srs_n = 0;
-  Xyzz* slots = nullptr;  // 9 x G
+  Xyzz* slots = nullptr;  // 9 (this rank's partial sums when sharded)
   int commit(const uint64_t* coeff, uint64_t len, int slot) {
     if (G == 1) return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot);
     const uint64_t base = len / G, extra = len % G;
     const uint64_t start = rank * base + (rank < extra ? rank : extra);
     const uint64_t cnt = base + (rank < extra ? 1 : 0);
-    int rc;
-    if (cnt) {
-      if ((rc = msm_fixed_device(ctx, srs_tbl, srs_n, start, coeff + 4 * start, cnt, s, (Xyzz*)comm->send)) ||
-          (rc = msm_fixed_wait(ctx, s)))
-        return rc;
-    } else {
-      PBF_HIP(hipMemsetAsync(comm->send, 0, sizeof(Xyzz), s));  // ZZ = 0: the identity
-    }
-    if ((rc = ag(sizeof(Xyzz)))) return rc;
-    PBF_HIP(hipMemcpyAsync(slots + (uint64_t)slot * G, comm->recv, G * sizeof(Xyzz), hipMemcpyDeviceToDevice, s));
+    if (cnt) return msm_fixed_device(ctx, srs_tbl, srs_n, start, coeff + 4 * start, cnt, s, slots + slot);
+    PBF_HIP(hipMemsetAsync(slots + slot, 0, sizeof(Xyzz), s));  // ZZ = 0: the identity
     return 0;
   }
   // q = (p - y) / (x - z) for p of L coefficients (k_hs1..3); a nonzero remainder fails with `err`
@@ -763,14 +758,29 @@ struct Prover {
     return check_bad(err);
   }
   int finish_commits(int count, uint64_t (*out)[8]) {
-    std::vector<Xyzz> h((size_t)count * G);
+    std::vector<Xyzz> h((size_t)count * G);  // [rank][commitment]
     int rc = msm_fixed_wait(ctx, s);
     if (rc) return rc;
-    PBF_HIP(hipMemcpyAsync(h.data(), slots, h.size() * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+    if (G == 1) {
+      PBF_HIP(hipMemcpyAsync(h.data(), slots, h.size() * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+    } else {
+      // the partial sums of every commitment in as few all-gathers as the comm buffers allow
+      // (one for any n >= 64; capacity >= 16 (4n / G) 32 B always holds G of them)
+      const int per = (int)std::min<size_t>((size_t)count, comm->capacity / ((size_t)G * sizeof(Xyzz)));
+      if (per < 1) return fail(PBF_EINVAL, "comm buffers too small for the commitment all-gather");
+      for (int k0 = 0; k0 < count; k0 += per) {
+        const int m = std::min(per, count - k0);
+        PBF_HIP(hipMemcpyAsync(comm->send, slots + k0, (size_t)m * sizeof(Xyzz), hipMemcpyDeviceToDevice, s));
+        if ((rc = ag((size_t)m * sizeof(Xyzz)))) return rc;
+        for (uint32_t r = 0; r < G; ++r)
+          PBF_HIP(hipMemcpyAsync(h.data() + (size_t)r * count + k0, (const Xyzz*)comm->recv + (size_t)r * m,
+                                 (size_t)m * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+      }
+    }
     PBF_HIP(hipStreamSynchronize(s));
     for (int k = 0; k < count; ++k) {
-      Xyzz acc = h[(size_t)k * G];
-      for (uint32_t r = 1; r < G; ++r) acc = G1::add(acc, h[(size_t)k * G + r]);
+      Xyzz acc = h[k];
+      for (uint32_t r = 1; r < G; ++r) acc = G1::add(acc, h[(size_t)r * count + k]);
       xyzz_to_affine_u64(acc, out[k]);
     }
     return 0;
@@ -849,7 +859,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // ---- proving key (one GPU): q_l q_r q_o q_m q_c s1 s2 s3 and l1 depend only on the circuit
   // (d_q, d_copies, k1, k2) and n. Their coefficients (8 slots) and coset evaluations (9
   // slots) are kept in the context and reused while the circuit is the same -- what a
-  // PLONK proving key holds -- validated by fingerprints of d_q and d_copies on every call.
+  // PLONK proving key holds -- validated on every call by comparing d_q and d_copies with the
+  // context's device copies of the gates and copies the key was built from (exact content).
   // PBF_PROVER_NO_PK=1 recomputes them per proof, as the reference does (plonk.rs:233-243,
   // 339-370).
   const bool pk_on = !getenv("PBF_PROVER_NO_PK");  // sharded too: this rank's coset blocks
@@ -858,11 +869,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* pkcoset = nullptr;
   std::vector<uint64_t> pk_key;
   if (pk_on) {
-    uint64_t fq = 0, fc = 0;
-    if ((rc = fingerprint_words(ctx, d_q, 20 * (uint64_t)n, s, &fq)) ||
-        (rc = fingerprint_words(ctx, d_copies, 6 * (uint64_t)n, s, &fc)))
-      return rc;
-    pk_key = {(uint64_t)n, fq, fc, (uint64_t)P.G, (uint64_t)P.rank};
+    const SnapItem items[2] = {{"pk.q", d_q, 20 * (uint64_t)n}, {"pk.copies", d_copies, 6 * (uint64_t)n}};
+    bool same = false;
+    if ((rc = snapshot_check(ctx, items, 2, s, &same))) return rc;
+    if (!same) ctx->pk_key.clear();
+    pk_key = {(uint64_t)n, (uint64_t)P.G, (uint64_t)P.rank};
     for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
     DevBuf& kc = ctx->buf("pk.coef");
     DevBuf& ks = ctx->buf("pk.coset");
@@ -882,7 +893,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   PBF_HIP(hipMemsetAsync(P.d_bad, 0, sizeof(int), s));
   {
     DevBuf& sl = ctx->buf("pv.commits");
-    if ((rc = sl.ensure(9 * (uint64_t)P.G * sizeof(Xyzz)))) return rc;
+    if ((rc = sl.ensure(9 * sizeof(Xyzz)))) return rc;
     P.slots = (Xyzz*)sl.p;
     P.srs_n = srs_m;
     if ((rc = msm_fixed_table(ctx, d_srs, srs_m, s, &P.srs_tbl))) return rc;  // built once per SRS
@@ -1308,20 +1319,22 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   for (int i = 0; i < 7; ++i)
     if (Fr::geq_p(u256_from_u64(proof_f + 4 * i))) return 0;
   // preprocessing (plonk.rs:507-517): commitments of q_m q_l q_r q_o q_c, s_sigma_1..3 -- a
-  // verification key: kept in the context for this circuit and SRS (fingerprints checked on
-  // every call; PBF_VERIFIER_NO_VK=1 recomputes them, as the reference does)
+  // verification key: kept in the context for this circuit and SRS (q, copies and the SRS
+  // compared with device copies of the ones it was built from on every call;
+  // PBF_VERIFIER_NO_VK=1 recomputes them, as the reference does)
   const U256 omega = hroot(log_n), one = fr_one_m();
   const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
   uint64_t pre[8][8];
   std::vector<uint64_t> vk_key;
   const bool vk_on = !getenv("PBF_VERIFIER_NO_VK");
   if (vk_on) {
-    uint64_t fq = 0, fc = 0, fs = 0;
-    if ((rc = fingerprint_words(ctx, d_q, 20 * (uint64_t)n, s, &fq)) ||
-        (rc = fingerprint_words(ctx, d_copies, 6 * (uint64_t)n, s, &fc)) ||
-        (rc = fingerprint_words(ctx, d_srs, 8 * (uint64_t)srs_m, s, &fs)))
-      return rc;
-    vk_key = {(uint64_t)n, fq, fc, fs, (uint64_t)srs_m};
+    const SnapItem items[3] = {{"vk.q", d_q, 20 * (uint64_t)n},
+                               {"vk.copies", d_copies, 6 * (uint64_t)n},
+                               {"vk.srs", d_srs, 8 * (uint64_t)srs_m}};
+    bool same = false;
+    if ((rc = snapshot_check(ctx, items, 3, s, &same))) return rc;
+    if (!same) ctx->vk_key.clear();  // rebuilt below; valid again once complete
+    vk_key = {(uint64_t)n, (uint64_t)srs_m};
     for (int i = 0; i < 8; ++i) vk_key.push_back(k1k2[i]);
   }
   if (vk_on && ctx->vk_key == vk_key && ctx->vk_pts.size() == 64) {

@@ -20,6 +20,8 @@ max(compute, exchange) instead of their sum.
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 
 import torch
@@ -331,20 +333,33 @@ class ShardedProver:
         self.send = torch.empty(self.words, dtype=torch.int64, device=device)
         self.recv = torch.empty(self.words, dtype=torch.int64, device=device)
         cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+        on_cuda = torch.device(device).type == "cuda"
 
-        def a2a(_user, nbytes, _stream):
+        def on_stream(stream_ptr):
+            # pbf.h: the exchange is ordered on the stream the library passes. torch.distributed
+            # (RCCL), LocalComm's copies and DistComm's host staging all order against torch's
+            # CURRENT stream, so make that stream current for the duration of the collective.
+            if not on_cuda:
+                return contextlib.nullcontext()
+            st = (torch.cuda.ExternalStream(stream_ptr) if stream_ptr
+                  else torch.cuda.default_stream(torch.device(device)))
+            return torch.cuda.stream(st)
+
+        def a2a(_user, nbytes, stream_ptr):
             try:
                 k = nbytes // 8
-                self.comm.all_to_all_single(self.recv[:world * k], self.send[:world * k])
+                with on_stream(stream_ptr):
+                    self.comm.all_to_all_single(self.recv[:world * k], self.send[:world * k])
                 return 0
             except Exception as e:  # surfaces as PBF_ECOMM
                 self.error = e
                 return 1
 
-        def ag(_user, nbytes, _stream):
+        def ag(_user, nbytes, stream_ptr):
             try:
                 k = nbytes // 8
-                self.comm.all_gather_into_tensor(self.recv[:world * k], self.send[:k])
+                with on_stream(stream_ptr):
+                    self.comm.all_gather_into_tensor(self.recv[:world * k], self.send[:k])
                 return 0
             except Exception as e:
                 self.error = e

@@ -43,6 +43,7 @@ SIGNATURES = [
     ("pbf_last_error", ctypes.c_char_p, []),
     ("pbf_ctx_set_stream", ctypes.c_int, [_vp, _vp]),
     ("pbf_device_sync", ctypes.c_int, [_vp]),
+    ("pbf_ctx_release_caches", ctypes.c_int, [_vp]),
     ("pbf_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
     ("pbf_ntt_u64_batch_dev", ctypes.c_int, [_vp, _u64, _u64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
     ("pbf_mul_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
@@ -157,6 +158,11 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def release_caches(self) -> None:
+        """pbf_ctx_release_caches: free the proving / verification keys, the fixed-base MSM
+        window table, the pairing check's prepared lines and their validating copies."""
+        _check(self.lib.pbf_ctx_release_caches(self.h))
 
     def set_stream(self, stream_ptr: int) -> None:
         _check(self.lib.pbf_ctx_set_stream(self.h, _vp(stream_ptr)))

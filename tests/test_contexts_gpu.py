@@ -67,3 +67,38 @@ def test_context_on_other_thread_default_device(ctx):
     assert np.array_equal(c2.ntt(GOLD, w, a), oracle.ntt_iter(GOLD, w, a))
     c2.close()
     assert np.array_equal(ctx.ntt(GOLD, w, a), oracle.ntt_iter(GOLD, w, a))
+
+
+def test_context_churn_pbh_two_threads():
+    """Contexts destroyed and recreated in a loop on two threads, running plonk-by-hand
+    ops whose device buffers are per-context (pbh.hip dev_for -> pbf_ctx named buffers):
+    a context allocated at a freed context's address must not inherit its buffers. Sizes
+    change every iteration so the buffers are (re)allocated inside each context."""
+    import random
+
+    errors = []
+
+    def worker(seed):
+        rng = random.Random(seed)
+        try:
+            for it in range(25):
+                ctx = pbf.Context(0)
+                m = rng.randrange(1, 400)
+                pts = [list(oracle.g1_mul((1, 2, 0), rng.randrange(1, 17))) for _ in range(m)]
+                sc = [rng.randrange(0, 101) for _ in range(m)]
+                got = ctx.pbh_g1_mul(pts, sc)
+                want = [oracle.g1_mul(tuple(p), s) for p, s in zip(pts, sc)]
+                ctx.close()
+                if got != want:
+                    errors.append(f"seed {seed} iteration {it}: mismatch")
+                    return
+        except Exception as e:  # surfaced in the main thread
+            errors.append(f"seed {seed}: {e!r}")
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in (5, 6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "worker hung"
+    assert not errors, errors

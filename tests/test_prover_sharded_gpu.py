@@ -89,6 +89,56 @@ def test_sharded_prove_virtual_ranks(G, log_n, mode):
     ctx0.close()
 
 
+@pytest.mark.parametrize("G", [2, 4])
+def test_sharded_prove_on_a_non_current_stream(G):
+    """pbf.h: the comm callbacks are ordered on the stream the library passes, which need not
+    be torch's current stream. Each rank proves on stream A while torch's current stream is B,
+    and A starts behind a long queue of work, so a collective that ordered itself on B (the
+    round-2 bug: ShardedProver ignored the stream argument) would read `send` before the
+    library wrote it."""
+    import torch
+
+    import pbf
+    from multigpu import LocalComm, LocalGroup, ShardedProver
+
+    n = 1 << 10
+    ctx0, (dq, dc, dabc, dsrs, srs_m, chal, rnd), (pts0, fs0) = _inputs(n, 0x5EED0777, 1)
+    group = LocalGroup(G)
+    out, errs = [None] * G, []
+
+    def rank_main(r):
+        try:
+            c = pbf.Context(0)
+            lib_stream, cur_stream = torch.cuda.Stream(), torch.cuda.Stream()
+            x = torch.randn(2048, 2048, device="cuda")
+            with torch.cuda.stream(lib_stream):
+                for _ in range(40):  # delays everything enqueued on lib_stream after it
+                    x = x @ x
+                    x = x / x.norm()
+            with torch.cuda.stream(cur_stream):
+                sp = ShardedProver(c, LocalComm(group, r), r, G, n, stream=lib_stream.cuda_stream)
+                assert torch.cuda.current_stream().cuda_stream != lib_stream.cuda_stream
+                out[r] = sp.prove(dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(), srs_m,
+                                  mode=1)
+            lib_stream.synchronize()
+            c.close()
+        except Exception as e:  # reported by the main thread
+            errs.append(f"rank {r}: {e!r}")
+            group.barrier.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "rank hung"
+    assert not errs, errs
+    for r in range(G):
+        pts, fs = out[r]
+        assert np.array_equal(pts, pts0) and np.array_equal(fs, fs0), f"rank {r} proof differs from one GPU's"
+    ctx0.close()
+
+
 def _gloo_rank(rank, world, port, n, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
