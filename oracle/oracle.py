@@ -48,6 +48,11 @@ _SIG = [
     ("oracle_gt_mul", None, [_p64, _p64, _p64]),
     ("oracle_gt_pow", None, [_p64, _u64, _p64]),
     ("oracle_pairing", ctypes.c_int, [_p64, _p64, _p64]),
+    ("oracle_fr_mul_ntt", ctypes.c_int, [_p64, _sz, _p64, _sz, _p64, _p64]),
+    ("oracle_g1_msm_naive", ctypes.c_int, [_p64, _p64, _sz, _p64]),
+    ("oracle_g1_msm_pippenger", ctypes.c_int, [_p64, _p64, _sz, ctypes.c_int, _p64]),
+    ("oracle_g1_mul_gen", ctypes.c_int, [_p64, _sz, _p64]),
+    ("oracle_g1_progression", ctypes.c_int, [_p64, _p64, _sz, _p64]),
     ("oracle_pbh_prove", ctypes.c_int, [_sz, _p64, _p64, _p64, _p64, _p64, _u64, _u64, _u64, _u64, _p64, _p64,
                                         _pint]),
 ]
@@ -268,3 +273,67 @@ def splitmix_field(modulus: int, seed: int, count: int, offset: int = 0) -> np.n
         else:
             z = z % np.uint64(modulus)
     return z
+
+
+# ---------------------------------------------------------------- BN254 CPU baselines (bn254_cpu.cpp)
+def _limbs(values, width=4):
+    a = np.zeros((len(values), width), dtype=np.uint64)
+    for i, v in enumerate(values):
+        for j in range(width):
+            a[i, j] = (int(v) >> (64 * j)) & 0xFFFFFFFFFFFFFFFF
+    return a
+
+
+def _ints(a, width=4):
+    a = np.asarray(a, dtype=np.uint64).reshape(-1, width)
+    return [sum(int(r[j]) << (64 * j) for j in range(width)) for r in a]
+
+
+def fr_mul_ntt(a_limbs: np.ndarray, b_limbs: np.ndarray, omega: int) -> np.ndarray:
+    """mul_ntt (fft.rs:109-132) over BN254 Fr, recursion-faithful, 1 core; limb arrays
+    (n x 4 u64) in and out."""
+    a = np.ascontiguousarray(a_limbs, dtype=np.uint64).reshape(-1, 4)
+    b = np.ascontiguousarray(b_limbs, dtype=np.uint64).reshape(-1, 4)
+    n = len(a) + len(b)
+    out = np.zeros((n, 4), dtype=np.uint64)
+    w = _limbs([omega])
+    if lib().oracle_fr_mul_ntt(_p(a), len(a), _p(b), len(b), _p(w), _p(out)):
+        raise ValueError("la + lb must be a power of two")
+    return out
+
+
+def _pts_out(o):
+    x, y = _ints(o.reshape(2, 4))
+    return None if (x, y) == (0, 0) else (x, y)
+
+
+def g1_msm_naive(points: np.ndarray, scalars: np.ndarray):
+    """SRS::eval_at_s (plonk.rs:51-58) literally: affine double-and-add per point, left fold."""
+    p = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, 8)
+    s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+    o = np.zeros(8, dtype=np.uint64)
+    lib().oracle_g1_msm_naive(_p(p), _p(s), len(p), _p(o))
+    return _pts_out(o)
+
+
+def g1_msm_pippenger(points: np.ndarray, scalars: np.ndarray, threads: int = 1):
+    p = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1, 8)
+    s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+    o = np.zeros(8, dtype=np.uint64)
+    lib().oracle_g1_msm_pippenger(_p(p), _p(s), len(p), threads, _p(o))
+    return _pts_out(o)
+
+
+def g1_mul_gen(scalars: np.ndarray) -> np.ndarray:
+    """k_i G as affine limb rows (n x 8), the MSM baselines' points."""
+    s = np.ascontiguousarray(scalars, dtype=np.uint64).reshape(-1, 4)
+    out = np.zeros((len(s), 8), dtype=np.uint64)
+    lib().oracle_g1_mul_gen(_p(s), len(s), _p(out))
+    return out
+
+
+def g1_progression(k0: int, d: int, n: int) -> np.ndarray:
+    """(k0 + i d) G for i < n, affine limb rows (n x 8)."""
+    out = np.zeros((n, 8), dtype=np.uint64)
+    lib().oracle_g1_progression(_p(_limbs([k0])), _p(_limbs([d])), n, _p(out))
+    return out

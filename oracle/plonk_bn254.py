@@ -232,3 +232,124 @@ def evaluations_at_z(n, q, copies, abc, chal, rnd, mode="reference", k1=2, k2=3)
             r3 = -(beta * zw_z * k3) * s3_z % R
         out[md] = [a_z, b_z, c_z, s1_z, s2_z, (r1 + r2 + r3 + r4) % R, zw_z]
     return out if mode == "both" else out[mode]
+
+
+def _accumulator(n, omega, h, sig, a, b, c, beta, gamma, k1, k2):
+    """acc_i = prod_{j<i} dend_j / dsor_j (plonk.rs:278-299): prefix products, one batch
+    inversion (the same computation as in evaluations_at_z)."""
+    nums, dens = [1] * n, [1] * n
+    pn = pd = 1
+    for i in range(1, n):
+        wi = h[i - 1]
+        pn = pn * ((a[i - 1] + beta * wi + gamma) * (b[i - 1] + beta * k1 * wi + gamma)
+                   * (c[i - 1] + beta * k2 * wi + gamma)) % R
+        pd = pd * ((a[i - 1] + beta * sig[0][i - 1] + gamma) * (b[i - 1] + beta * sig[1][i - 1] + gamma)
+                   * (c[i - 1] + beta * sig[2][i - 1] + gamma)) % R
+        nums[i], dens[i] = pn, pd
+    pre = [1] * (n + 1)
+    for i in range(n):
+        pre[i + 1] = pre[i] * dens[i] % R
+    inv = pow(pre[n], R - 2, R)
+    acc = [0] * n
+    for i in range(n - 1, -1, -1):
+        acc[i] = nums[i] * (inv * pre[i] % R) % R
+        inv = inv * dens[i] % R
+    return acc
+
+
+def commitment_scalars(n, q, copies, abc, chal, rnd, s, k1=2, k2=3):
+    """O(n) pinning of all 9 commitments of Plonk::prove (plonk.rs:245-446) for an SRS
+    [s^i]G with known s (SRS::create, plonk.rs:35-48): SRS::eval_at_s(p) = [p(s)]G, and
+    every polynomial the prover commits to is evaluated at s from its values on H by the
+    barycentric formula (plus its blinding terms), exactly as evaluations_at_z does at z.
+    Returns, per mode ("reference", "paper"):
+      a, b, c, z:  a(s), b(s), c(s), z(s)                 -> a_s = [a(s)]G, ...
+      t:           t(s) = T(s) / Z_H(s) (T = t_1 + t_2 - t_3 + t_4, plonk.rs:339-370)
+                                                          -> t_lo + [s^(n+2)] t_mid + [s^(2n+4)] t_hi = [t(s)]G
+      wz:          the scalar W with (s - z) W_z(s) = t_lo(s) + z^(n+2) t_mid(s)
+                   + z^(2n+4) t_hi(s) + W  (plonk.rs:424-438 with t_z = T(z) / Z_H(z))
+                                                          -> [s - z] w_z - t_lo - [z^(n+2)] t_mid - [z^(2n+4)] t_hi = [W]G
+      wzw:         (z(s) - z(omega z)) / (s - omega z)    -> w_zw = [wzw]G (plonk.rs:440-442)
+      fields:      the proof's 7 field elements (as evaluations_at_z)."""
+    omega = F.root_of_unity(n)
+    alpha, beta, gamma, z, v = (x % R for x in chal)
+    b1, b2, b3, b4, b5, b6, b7, b8, b9 = (x % R for x in rnd)
+    s %= R
+    h = [1] * n
+    for i in range(1, n):
+        h[i] = h[i - 1] * omega % R
+    tab = (h, [x * k1 % R for x in h], [x * k2 % R for x in h])
+    sig = [[tab[k][i - 1] for k, i in col] for col in copies]
+    a, b, c = ([x % R for x in col] for col in abc)
+    qs = [[x % R for x in col] for col in q]  # q_l q_r q_o q_m q_c
+    acc = _accumulator(n, omega, h, sig, a, b, c, beta, gamma, k1, k2)
+
+    def z_at(x):  # z(x) = (b7 x^2 + b8 x + b9) Z_H(x) + acc interpolated (plonk.rs:315)
+        w, sc = _bary_weights(n, omega, x)
+        return ((b7 * x * x + b8 * x + b9) * (pow(x, n, R) - 1) + _bary(acc, w, sc)) % R
+
+    def at(x):
+        w, sc = _bary_weights(n, omega, x)
+        ev = lambda vals: _bary(vals, w, sc)  # noqa: E731
+        zh = (pow(x, n, R) - 1) % R
+        d = {"x": x, "zh": zh}
+        d["a"] = ((b1 * x + b2) * zh + ev(a)) % R
+        d["b"] = ((b3 * x + b4) * zh + ev(b)) % R
+        d["c"] = ((b5 * x + b6) * zh + ev(c)) % R
+        d["z"] = ((b7 * x * x + b8 * x + b9) * zh + ev(acc)) % R
+        d["s1"], d["s2"], d["s3"] = ev(sig[0]), ev(sig[1]), ev(sig[2])
+        d["ql"], d["qr"], d["qo"], d["qm"], d["qc"] = (ev(col) for col in qs)
+        d["l1"] = zh * pow(n * (x - 1) % R, R - 2, R) % R
+        return d
+
+    def numerator(d, zw):  # T(x) = t_1 + t_2 - t_3 + t_4 (plonk.rs:339-366) from values at x
+        x = d["x"]
+        t1 = d["a"] * d["b"] * d["qm"] + d["a"] * d["ql"] + d["b"] * d["qr"] + d["c"] * d["qo"] + d["qc"]
+        t2 = alpha * (d["a"] + beta * x + gamma) * (d["b"] + beta * k1 * x + gamma) \
+            * (d["c"] + beta * k2 * x + gamma) % R * d["z"]
+        t3 = alpha * (d["a"] + beta * d["s1"] + gamma) * (d["b"] + beta * d["s2"] + gamma) \
+            * (d["c"] + beta * d["s3"] + gamma) % R * zw
+        t4 = (d["z"] - 1) * alpha * alpha % R * d["l1"]
+        return (t1 + t2 - t3 + t4) % R
+
+    S, Z = at(s), at(z)
+    zw_s, zw_z = z_at(omega * s % R), z_at(omega * z % R)
+    t_s = numerator(S, zw_s) * pow(S["zh"], R - 2, R) % R
+    t_z = numerator(Z, zw_z) * pow(Z["zh"], R - 2, R) % R
+    a_z, b_z, c_z, s1_z, s2_z = Z["a"], Z["b"], Z["c"], Z["s1"], Z["s2"]
+    k3 = (a_z + beta * s1_z + gamma) * (b_z + beta * s2_z + gamma) * alpha % R
+    c2 = (a_z + beta * z + gamma) * (b_z + beta * k1 * z + gamma) * (c_z + beta * k2 * z + gamma) * alpha % R
+    out = {}
+    for md in ("reference", "paper"):
+        def r_at(d, md=md):  # r(x) with the round-4 scalars (plonk.rs:401-419)
+            r1 = d["qm"] * a_z * b_z + d["ql"] * a_z + d["qr"] * b_z + d["qo"] * c_z + d["qc"]
+            r2 = d["z"] * c2
+            if md == "reference":
+                r3 = d["z"] * d["s3"] % R * beta * zw_z % R * k3
+            else:
+                r3 = -(beta * zw_z * k3) * d["s3"]
+            r4 = d["z"] * Z["l1"] * alpha * alpha
+            return (r1 + r2 + r3 + r4) % R
+        r_z = r_at(Z)
+        wz = (-t_z + v * (r_at(S) - r_z) + v ** 2 * (S["a"] - a_z) + v ** 3 * (S["b"] - b_z)
+              + v ** 4 * (S["c"] - c_z) + v ** 5 * (S["s1"] - s1_z) + v ** 6 * (S["s2"] - s2_z)) % R
+        out[md] = {"a": S["a"], "b": S["b"], "c": S["c"], "z": S["z"], "t": t_s, "wz": wz,
+                   "wzw": (S["z"] - zw_z) * pow((s - omega * z) % R, R - 2, R) % R,
+                   "fields": [a_z, b_z, c_z, s1_z, s2_z, r_z, zw_z]}
+    return out
+
+
+def commitments_match(n, pts, cs, s, z):
+    """The five commitment identities of commitment_scalars (one mode's dict `cs`) on the 9
+    proof points (affine tuples, None = identity): a_s b_s c_s z_s, the recombined t parts,
+    W_z and W_zw. Returns {name: bool}."""
+    G, mul, add, neg = B.G1_GEN, B.g1_mul, B.g1_add, B.g1_neg
+    a_s, b_s, c_s, z_s, t_lo, t_mid, t_hi, w_z, w_zw = (None if p is None else tuple(p) for p in pts)
+    s, z = s % R, z % R
+    res = {k: mul(G, cs[k]) == p for k, p in (("a", a_s), ("b", b_s), ("c", c_s), ("z", z_s))}
+    t_rec = add(add(t_lo, mul(t_mid, pow(s, n + 2, R))), mul(t_hi, pow(s, 2 * n + 4, R)))
+    res["t"] = t_rec == mul(G, cs["t"])
+    lhs = add(mul(w_z, (s - z) % R), neg(add(add(t_lo, mul(t_mid, pow(z, n + 2, R))), mul(t_hi, pow(z, 2 * n + 4, R)))))
+    res["w_z"] = lhs == mul(G, cs["wz"])
+    res["w_zw"] = w_zw == mul(G, cs["wzw"])
+    return res

@@ -76,6 +76,12 @@ struct NttPlan {
   // (A: R x W, B: Ns/W x R; null when unused), W = tws_w columns per tile
   std::shared_ptr<DevBuf> tws_a, tws_b;
   int tws_w = 0;
+  // round-3 schedule (ntt_ip.hpp): in-place digit slots, persistent prefetching passes;
+  // ip_r = radix bits per pass (top slot first), per-pass twiddle and stage-C tables
+  bool ip = false;
+  std::vector<int> ip_r;
+  std::vector<std::shared_ptr<DevBuf>> ip_tw, ip_tc;
+  std::shared_ptr<DevBuf> ip_twa;  // row pass TA[x][w] (split form), null: full T[K][x]
 };
 
 // Extra streams and events of the multi-stream NTT group schedule (ntt_launch.hip
@@ -105,6 +111,8 @@ struct MsmTail {
   ~MsmTail();  // waits for the side stream (declared after the buffers it uses)
 };
 
+// Round-3 schedule of a plan with p.ip (ntt_ip.hip): the whole batch, scratch s0
+int run_ip(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, hipStream_t stream);
 // Build a plan (validates omega's order and n^-1). Returns PBF status.
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p);
 // Enqueue a batched transform of a planned size on `stream` (d_in may equal d_out).

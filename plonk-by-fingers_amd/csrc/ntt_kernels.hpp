@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(256) shard_split_inv_kernel(CombineArgs a) {
 
 // Gather the inverse's received blocks recv[g][b][kk] (from rank g, block of this
 // rank r) into per-polynomial natural order y[b][g*S + kk] for the local INTT.
-__global__ void shard_unsplit_kernel(const uint64_t* recv, uint64_t* out, uint64_t s, uint64_t nl, uint32_t batch,
+static __global__ void shard_unsplit_kernel(const uint64_t* recv, uint64_t* out, uint64_t s, uint64_t nl, uint32_t batch,
                                      uint32_t G) {
   const uint64_t total = nl * batch;
   for (uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; id < total;

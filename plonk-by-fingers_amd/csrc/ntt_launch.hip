@@ -83,6 +83,111 @@ static std::vector<int> default_passes(uint32_t log_n) {
 
 static int gl_tile(int logr);
 
+// ---- round-3 schedule (ntt_ip.hpp) ----------------------------------------------------
+int ip_tile_of(int r) { return r >= 10 ? 8192 : 4096; }
+int ip_w(int r) { return ip_tile_of(r) >> r; }
+
+// radix bits per pass, top slot first; empty when the schedule does not apply
+static std::vector<int> ip_radices(uint32_t L) {
+  std::vector<int> v;
+  if (const char* env = getenv("PBF_NTT_IP_PASSES")) {  // A/B override, e.g. "8,8,8"
+    int sum = 0;
+    for (const char* c = env; *c;) {
+      v.push_back(atoi(c));
+      sum += v.back();
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+    if (sum != (int)L) v.clear();
+  } else if (L >= 12 && L <= 30) {
+    const int P = L <= 20 ? 2 : 3;
+    v.assign(P, (int)L / P);
+    for (int i = 0; i < (int)(L % P); ++i) v[i] += 1;
+  }
+  if (v.size() < 2 || v.size() > 4) return {};  // IP_MAXP (ntt_ip.hpp)
+  int lo = (int)L;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (v[i] < 6 || v[i] > 10) return {};
+    lo -= v[i];
+    if (i + 1 < v.size() && (1 << lo) < ip_w(v[i])) return {};  // column blocks of W
+  }
+  if ((1 << v[0]) < ip_w(v.back())) return {};  // row pass: W consecutive K vary k_0 only
+  return v;
+}
+
+static int make_ip_plan(NttPlan* p, uint64_t w) {
+  const uint64_t m = p->m, n = p->n;
+  const uint32_t L = p->log_n;
+  p->ip_r = ip_radices(L);
+  if (p->ip_r.empty()) return 0;
+  const size_t P = p->ip_r.size();
+  std::vector<int> lo(P);
+  {
+    int l = (int)L;
+    for (size_t i = 0; i < P; ++i) { l -= p->ip_r[i]; lo[i] = l; }
+  }
+  const uint64_t scale = p->inverse ? p->n_inv : 1;
+  for (size_t i = 0; i < P; ++i) {
+    const int r = p->ip_r[i];
+    const uint64_t R = 1ull << r, C = R / 64, W = (uint64_t)ip_w(r);
+    // stage-C table w_R^(r2 k1) (unscaled: the inverse scales in the row pass's twiddles)
+    {
+      const uint64_t wr = hpow(w, n / R, m);
+      std::vector<uint64_t> tc(C * 64);
+      for (uint64_t r2 = 0; r2 < C; ++r2)
+        for (uint64_t k1 = 0; k1 < 64; ++k1) tc[r2 * 64 + k1] = hpow(wr, r2 * k1, m);
+      auto b = std::make_shared<DevBuf>();
+      int rc = upload(*b, tc);
+      if (rc) return rc;
+      p->ip_tc.push_back(b);
+    }
+    auto tb = std::make_shared<DevBuf>();
+    if (i > 0 && i + 1 < P) {
+      // column pass: T[h][x] = w^(2^lo_i x K(h)), K(h) = the earlier digits, k_0 lowest
+      const uint64_t H = 1ull << (L - lo[i] - r);
+      std::vector<uint64_t> t(H * R);
+      for (uint64_t h = 0; h < H; ++h) {
+        uint64_t K = 0, sh = 0;
+        for (size_t j = 0; j < i; ++j) {
+          const uint64_t kj = (h >> (lo[j] - lo[i] - r)) & ((1ull << p->ip_r[j]) - 1);
+          K |= kj << sh;
+          sh += (uint64_t)p->ip_r[j];
+        }
+        const uint64_t z = hpow(w, (((uint64_t)1 << lo[i]) * K) % n, m);
+        uint64_t y = 1;
+        for (uint64_t x = 0; x < R; ++x) { t[h * R + x] = y; y = hmul(y, z, m); }
+      }
+      int rc = upload(*tb, t);
+      if (rc) return rc;
+    } else if (i + 1 == P) {
+      // row pass: w^(x K) (x n^-1 for the inverse), K < n / R
+      const uint64_t NK = n / R;
+      const bool full = n <= (1ull << 21) && !getenv("PBF_NTT_IP_SPLIT");
+      std::vector<uint64_t> t(full ? NK * R : (NK / W) * R);
+      for (uint64_t kb = 0; kb < (full ? NK : NK / W); ++kb) {
+        const uint64_t z = hpow(w, full ? kb : kb * W, m);
+        uint64_t y = scale;
+        for (uint64_t x = 0; x < R; ++x) { t[kb * R + x] = y; y = hmul(y, z, m); }
+      }
+      int rc = upload(*tb, t);
+      if (rc) return rc;
+      if (!full) {
+        std::vector<uint64_t> ta(R * W);
+        for (uint64_t x = 0; x < R; ++x) {
+          const uint64_t z = hpow(w, x, m);
+          uint64_t y = 1;
+          for (uint64_t c = 0; c < W; ++c) { ta[x * W + c] = y; y = hmul(y, z, m); }
+        }
+        p->ip_twa = std::make_shared<DevBuf>();
+        if ((rc = upload(*p->ip_twa, ta))) return rc;
+      }
+    }
+    p->ip_tw.push_back(tb);
+  }
+  p->ip = true;
+  return 0;
+}
+
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   if (!field_for(m, &p->kind, &p->fa)) return fail(5, "unsupported modulus");
   if (n == 0 || (n & (n - 1))) return fail(1, "n must be a power of two");
@@ -216,6 +321,12 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
       if (rc) return rc;
       p->tc.push_back(b);
     }
+  }
+  // round-3 in-place schedule: opt-in (PBF_NTT_IP=1) while it measures slower than the
+  // round-2 Stockham plan
+  if (p->gl && getenv("PBF_NTT_IP") && !getenv("PBF_NTT_V2")) {
+    int rc2 = make_ip_plan(p, w);
+    if (rc2) return rc2;
   }
   return 0;
 }
@@ -384,7 +495,7 @@ int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, u
 // The answer depends only on the kernel, the block size and the device, never on a context's
 // state, so one process-wide table under a lock serves every context (pbf.h: contexts share
 // no mutable state a caller could observe).
-static uint32_t persistent_grid(const void* fn, int nt, uint64_t tiles) {
+uint32_t persistent_grid(const void* fn, int nt, uint64_t tiles) {
   static std::mutex mu;
   static std::map<std::tuple<const void*, int, int>, uint32_t> cache;
   int dev = 0;
@@ -612,6 +723,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
   if (batch == 0) return 0;
+  if (p.ip && split_log == 0 && p.n > 1) return run_ip(p, d_in, d_out, batch, s0, stream);
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * 8, hipMemcpyDeviceToDevice, stream));
     return 0;  // size-1 DFT is the identity; n^-1 = 1

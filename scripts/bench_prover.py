@@ -20,7 +20,37 @@ G2 = ((1085704699902305713594457076223282948137075635957851808699051999328565585
        4082367875863433681332203403145435568316851327593401208105741076214120093531))
 
 
-def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True) -> dict:
+def breakdown(fn) -> dict:
+    """Per-round wall times of one proof: PBF_PROVER_TIMING=1 makes the prover synchronise its
+    stream at each round mark and print it on stderr (csrc/prover.hip Prover::mark); fd 2 is
+    captured around the call. The marks serialise the proof, so their sum exceeds prove_ms."""
+    import tempfile
+
+    os.environ["PBF_PROVER_TIMING"] = "1"
+    sys.stderr.flush()
+    saved = os.dup(2)
+    with tempfile.TemporaryFile(mode="w+b") as tf:
+        os.dup2(tf.fileno(), 2)
+        try:
+            fn()
+            torch.cuda.synchronize()
+        finally:
+            os.dup2(saved, 2)
+            os.close(saved)
+            del os.environ["PBF_PROVER_TIMING"]
+        tf.seek(0)
+        text = tf.read().decode(errors="replace")
+    out = {}
+    for line in text.splitlines():
+        if line.startswith("[pbf prover]"):
+            body = line[len("[pbf prover]"):].rsplit(None, 2)
+            if len(body) == 3 and body[2] == "ms":
+                out[body[0].strip()] = float(body[1])
+    return out
+
+
+def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True, no_key: bool = True,
+        rounds: bool = True) -> dict:
     n = 1 << log_n
     sp = torch.cuda.current_stream().cuda_stream
     dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
@@ -48,29 +78,38 @@ def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True) -> d
         ts.append(time.perf_counter() - t0)
     ts.sort()
     t_prove = ts[len(ts) // 2]
-    # the same proof with the circuit's preprocessing (8 INTTs + 9 coset NTTs of the
-    # selector / permutation / l1 polynomials) recomputed per proof, as the reference does
-    os.environ["PBF_PROVER_NO_PK"] = "1"
-    tc = []
-    try:
-        for _ in range(max(3, reps // 2)):
-            t0 = time.perf_counter()
-            pts_c, fs_c = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd,
-                                                    dsrs.data_ptr(), srs_m, mode=mode, stream=sp)
-            torch.cuda.synchronize()
-            tc.append(time.perf_counter() - t0)
-    finally:
-        del os.environ["PBF_PROVER_NO_PK"]
-    tc.sort()
-    t_cold = tc[len(tc) // 2]
-    out = {"log_n": log_n, "gates": n, "mode": mode, "prove_ms": t_prove * 1e3, "prove_ms_min": ts[0] * 1e3,
+    out = {"log_n": log_n, "gates": n, "mode": mode,
+           "mode_name": "paper linearisation" if mode == 1 else "the reference's r_3 (plonk.rs:414-416)",
+           "prove_ms": t_prove * 1e3, "prove_ms_min": ts[0] * 1e3,
            "prove_ms_max": ts[-1] * 1e3, "reps": reps, "proofs_per_s": 1 / t_prove,
            "proving_key": "preprocessed q_*, s_sigma_*, l1 (coefficients + coset evaluations) kept in the "
-                          "context per circuit, fingerprint-checked every proof",
-           "prove_ms_no_key": t_cold * 1e3, "proofs_per_s_no_key": 1 / t_cold, "reps_no_key": len(tc),
-           "same_proof_with_and_without_key": bool(np.array_equal(np.asarray(pts_c), np.asarray(pts))
-                                                   and np.array_equal(np.asarray(fs_c), np.asarray(fs))),
+                          "context per circuit, validated against device copies of q / copies every proof",
            "srs_create_ms": t_srs * 1e3}
+    if no_key:
+        # the same proof with the circuit's preprocessing (8 INTTs + 9 coset NTTs of the
+        # selector / permutation / l1 polynomials) recomputed per proof, as the reference does
+        os.environ["PBF_PROVER_NO_PK"] = "1"
+        tc = []
+        try:
+            for _ in range(max(3, reps // 2)):
+                t0 = time.perf_counter()
+                pts_c, fs_c = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd,
+                                                        dsrs.data_ptr(), srs_m, mode=mode, stream=sp)
+                torch.cuda.synchronize()
+                tc.append(time.perf_counter() - t0)
+        finally:
+            del os.environ["PBF_PROVER_NO_PK"]
+        tc.sort()
+        t_cold = tc[len(tc) // 2]
+        out.update({"prove_ms_no_key": t_cold * 1e3, "proofs_per_s_no_key": 1 / t_cold, "reps_no_key": len(tc),
+                    "same_proof_with_and_without_key": bool(np.array_equal(np.asarray(pts_c), np.asarray(pts))
+                                                            and np.array_equal(np.asarray(fs_c), np.asarray(fs)))})
+    if rounds:
+        out["rounds_ms"] = breakdown(lambda: ctx.plonk_prove_bn254_dev(
+            n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(), srs_m, mode=mode,
+            stream=sp))
+        out["rounds_note"] = ("one proof with a stream synchronisation at every round mark "
+                              "(PBF_PROVER_TIMING): where the time goes, not the overlapped total")
     if verify:
         import ctypes
 

@@ -39,3 +39,20 @@ def test_linear_time_checker_matches_fixtures():
     for c in gold:
         q, cp, abc = P.mul_gates_circuit(c["n"], c["circuit_seed"])
         assert P.evaluations_at_z(c["n"], q, cp, abc, c["chal"], c["rnd"], mode=c["mode"]) == c["fields"]
+
+
+def test_commitment_checker_matches_fixtures():
+    # oracle/plonk_bn254.py:commitment_scalars / commitments_match (the O(n) pinning of all 9
+    # commitments used at 2^20 gates on the GPU) agree with every committed literal-oracle proof
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "plonk_bn254.json")))["cases"]
+    for c in gold:
+        q, cp, abc = P.mul_gates_circuit(c["n"], c["circuit_seed"])
+        cs = P.commitment_scalars(c["n"], q, cp, abc, c["chal"], c["rnd"], c["s"])[c["mode"]]
+        assert cs["fields"] == c["fields"]
+        pts = [None if p is None else tuple(p) for p in c["pts"]]
+        res = P.commitments_match(c["n"], pts, cs, c["s"], c["chal"][3])
+        assert all(res.values()), (c["n"], c["mode"], res)
+        # and they reject a proof with two commitments swapped
+        bad = list(pts)
+        bad[4], bad[5] = bad[5], bad[4]
+        assert not all(P.commitments_match(c["n"], bad, cs, c["s"], c["chal"][3]).values())

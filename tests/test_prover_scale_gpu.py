@@ -2,16 +2,20 @@
 (pbf_plonk_prove_bn254_dev / pbf_plonk_verify_bn254_dev), checked by properties that do
 not need an O(n^2) oracle:
 * all 7 proof field elements (a_z, b_z, c_z, s_sigma_1_z, s_sigma_2_z, r_z, z_omega_z)
-  recomputed in O(n) from the witness by oracle/plonk_bn254.py:evaluations_at_z (the
+  recomputed in O(n) from the witness by oracle/plonk_bn254.py:commitment_scalars (the
   barycentric form of plonk.rs:393-422; pinned to the literal oracle and its fixtures in
   tests/test_prover_oracle.py), in both modes;
 * the quotient's divisibility: the prover fails with PBF_EINVAL unless coefficients
   3n+6.. of t(x) and the remainders of W_z / W_zw are all zero (plonk.rs:370, 438, 442),
   so a successful return certifies them;
-* the 9 commitments through the verifier: the paper-mode proof verifies, a proof with a
-  changed evaluation or a swapped commitment does not. (The reference-mode proof is
-  checked by its evaluations only: with the reference's r_3(x) an honest proof verifies
-  only when k3 = (a_z + beta s1_z + gamma)(b_z + beta s2_z + gamma) alpha = 0, as in the
+* all 9 commitments exactly, in both modes: SRS = [s^i]G with s known, so a_s = [a(s)]G
+  etc. with a(s) from the same barycentric form at s (oracle/plonk_bn254.py:
+  commitment_scalars); t_lo / t_mid / t_hi through [t(s)]G = t_lo + s^(n+2) t_mid +
+  s^(2n+4) t_hi, W_z and W_zw through their division identities at s;
+* the verifier: the paper-mode proof verifies, a proof with a changed evaluation or a
+  swapped commitment does not. (The reference-mode proof is pinned by its evaluations and
+  commitments but is expected NOT to verify: with the reference's r_3(x) an honest proof
+  verifies only when k3 = (a_z + beta s1_z + gamma)(b_z + beta s2_z + gamma) alpha = 0, as in the
   reference's n = 4 KAT where (b_z + beta s2_z + gamma) = 170 = 0 mod 17)
 """
 import os
@@ -28,6 +32,18 @@ import bn254_pairing as B  # noqa: E402
 import plonk_bn254 as P  # noqa: E402
 
 pytestmark = pytest.mark.gpu
+
+
+def _points(flat):
+    """9 x 8 u64 limbs -> affine int tuples ((0, 0) -> None, the GPU's identity encoding)."""
+    import pbf
+
+    v = pbf.limbs_to_ints(np.asarray(flat, dtype=np.uint64).reshape(-1))
+    out = []
+    for k in range(len(v) // 2):
+        x, y = v[2 * k], v[2 * k + 1]
+        out.append(None if (x, y) == (0, 0) else (x, y))
+    return out
 
 
 def _ints(t, width):
@@ -78,14 +94,57 @@ def test_prove_2p20_gates(ctx, log_n):
     assert not verify(bad_p.reshape(-1), fs, chal, 1)
     assert not verify(pts0, fs0, chal1, 0)  # the reference's r_3: k3 != 0 here
 
-    # field elements: O(n) recomputation from the witness
+    # field elements and all 9 commitments: O(n) recomputation from the witness and the SRS
+    # secret s (oracle/plonk_bn254.py:commitment_scalars, pinned to the literal oracle's
+    # proofs in tests/test_prover_oracle.py), in both modes
     qv = _ints(dq, 4)
     q = tuple(qv[i * n:(i + 1) * n] for i in range(5))
     cv = _ints(dc, 2).reshape(3, n, 2)
     copies = tuple([(int(k), int(i)) for k, i in cv[col]] for col in range(3))
     av = _ints(dabc, 4)
     abc = tuple(av[i * n:(i + 1) * n] for i in range(3))
-    ev = P.evaluations_at_z(n, q, copies, abc, chal, rnd, mode="paper")
-    assert pbf.limbs_to_ints(fs) == ev
-    ev0 = P.evaluations_at_z(n, q, copies, abc, chal1, rnd, mode="reference")
-    assert pbf.limbs_to_ints(fs0) == ev0
+    cs = P.commitment_scalars(n, q, copies, abc, chal, rnd, s)
+    assert pbf.limbs_to_ints(fs) == cs["paper"]["fields"]
+    assert pbf.limbs_to_ints(fs0) == cs["reference"]["fields"]
+    for md, p in (("paper", pts), ("reference", pts0)):
+        res = P.commitments_match(n, _points(p), cs[md], s, chal[3])
+        assert all(res.values()), (md, res)
+
+
+def test_prove_2p24_gates(ctx):
+    """BASELINE config 5 at its own size on one GPU: 2^24 gates, paper mode. The prover's
+    built-in checks (constraints satisfied, the accumulator's product = 1, t(x) divisible by
+    Z_H with coefficients 3n+6.. zero, zero remainders of W_z / W_zw: plonk.rs:199, 307,
+    370, 438, 442) pass, the proof verifies, and a changed evaluation or two swapped
+    commitments are rejected. (The O(n) Python checker of test_prove_2p20_gates is not run
+    at this size: 16x its ~30 s.)"""
+    import torch
+
+    n = 1 << 24
+    rng = random.Random(0x5EED0024)
+    sp = torch.cuda.current_stream().cuda_stream
+    dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
+    dc = torch.empty(3 * n * 2, dtype=torch.int64, device="cuda")
+    dabc = torch.empty(3 * n * 4, dtype=torch.int64, device="cuda")
+    ctx.plonk_synth_circuit_dev(n, 0x5EED0024, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), stream=sp)
+    s = rng.randrange(2, P.R)
+    srs_m = n + 3
+    dsrs = torch.empty(srs_m * 8, dtype=torch.int64, device="cuda")
+    ctx.srs_create_dev(s, srs_m - 1, dsrs.data_ptr(), stream=sp)
+    g2s = [B.G2_GEN, ctx.g2_bn254_mul([B.G2_GEN], [s])[0]]
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    u = rng.randrange(P.R)
+    pts, fs = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(),
+                                        srs_m, mode=1, stream=sp)
+    torch.cuda.synchronize()
+    verify = lambda p, f: ctx.plonk_verify_bn254_dev(  # noqa: E731
+        n, dq.data_ptr(), dc.data_ptr(), dsrs.data_ptr(), srs_m, g2s, p, f, chal, u, mode=1, stream=sp)
+    assert verify(pts, fs)
+    bad_f = fs.copy()
+    bad_f[5 * 4] ^= 1  # r_z
+    assert not verify(pts, bad_f)
+    bad_p = pts.copy().reshape(9, 8)
+    bad_p[[4, 6]] = bad_p[[6, 4]]  # t_lo <-> t_hi
+    assert not verify(bad_p.reshape(-1), fs)
+    ctx.release_caches()  # ~24 GB of proving key; later tests start from a clean context
