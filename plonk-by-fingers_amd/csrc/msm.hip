@@ -5,7 +5,7 @@
 //
 // MSM = Pippenger, window c = 16 (16 windows over the 254-bit scalars):
 //   1. msm_digits: key = (window << 16) | digit per (point, window), digit 0 skipped
-//   2. hipCUB radix sort of (key, point index) pairs  -> points grouped by bucket
+//   2. radix sort of (key, point index) pairs (msm_sort.hpp) -> points grouped by bucket
 //   3. msm_bucket_bounds: [start, end) of every bucket in the sorted order
 //   4. msm_chunk_acc: the sorted list cut into fixed chunks of MSM_CH entries, one thread
 //      per chunk accumulating its runs of equal keys in XYZZ (every thread does the same
@@ -15,10 +15,10 @@
 //      (msm_fx_cd / msm_fx_subsets / msm_fx_total, see there)
 //   6. host: Horner over the 16 window sums (2^16 steps), one inversion to affine.
 // The result is a group element, so the canonical affine output is unique.
-#include <hipcub/hipcub.hpp>
 #include <vector>
 #include "../../include/pbf.h"
 #include "msm.hpp"
+#include "msm_sort.hpp"
 
 namespace pbf {
 
@@ -510,16 +510,30 @@ static uint64_t grid1(uint64_t count) {
 }
 
 struct MsmWork {
-  DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &temp, &head, &tail,
-      &parts, &span;
+  DevBuf &pts, &inf, &keys, &vals, &keys2, &vals2, &start, &end, &buckets, &shares, &sums, &head, &tail, &parts,
+      &span;
 };
 
 // scratch owned by the context (freed with it)
 static MsmWork msm_work(pbf_ctx* ctx) {
   return MsmWork{ctx->buf("msm.pts"),     ctx->buf("msm.inf"),    ctx->buf("msm.keys"),   ctx->buf("msm.vals"),
                  ctx->buf("msm.keys2"),   ctx->buf("msm.vals2"),  ctx->buf("msm.start"),  ctx->buf("msm.end"),
-                 ctx->buf("msm.buckets"), ctx->buf("msm.shares"), ctx->buf("msm.sums"),   ctx->buf("msm.temp"),
-                 ctx->buf("msm.head"),    ctx->buf("msm.tail"),   ctx->buf("msm.parts"),  ctx->buf("msm.span")};
+                 ctx->buf("msm.buckets"), ctx->buf("msm.shares"), ctx->buf("msm.sums"),   ctx->buf("msm.head"),
+                 ctx->buf("msm.tail"),    ctx->buf("msm.parts"),  ctx->buf("msm.span")};
+}
+
+// (key, value) pairs sorted by key bits [0, bits) into keys2 / vals2 (msm_sort.hpp), with the
+// context's scratch
+static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* vals, uint32_t* keys2, uint32_t* vals2,
+                          uint64_t m, int bits, hipStream_t s) {
+  if (m > 0xFFFFFFFFull - RS_TILE) return fail(PBF_EINVAL, "too many MSM entries");
+  DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
+  const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
+  int rc;
+  if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
+  rs_sort(keys, vals, keys2, vals2, (uint32_t*)tk.p, (uint32_t*)tv.p, (uint32_t)m, bits, (uint32_t*)hb.p, s);
+  PBF_HIP(hipGetLastError());
+  return 0;
 }
 
 // Enqueue the device part; window sums land in w.sums (MSM_NW Xyzz, Montgomery).
@@ -544,14 +558,9 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
                      (uint8_t*)w.inf.p, n);
   hipLaunchKernelGGL(msm_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, (const uint8_t*)w.inf.p,
                      (uint32_t*)w.keys.p, (uint32_t*)w.vals.p, n);
-  size_t temp_bytes = 0;
-  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (const uint32_t*)w.keys.p, (uint32_t*)w.keys2.p,
-                                             (const uint32_t*)w.vals.p, (uint32_t*)w.vals2.p, (int)m, 0,
-                                             MSM_BB + 5, s));
-  if ((rc = w.temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
-  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(w.temp.p, temp_bytes, (const uint32_t*)w.keys.p, (uint32_t*)w.keys2.p,
-                                             (const uint32_t*)w.vals.p, (uint32_t*)w.vals2.p, (int)m, 0,
-                                             MSM_BB + 5, s));
+  if ((rc = msm_sort_pairs(ctx, (const uint32_t*)w.keys.p, (const uint32_t*)w.vals.p, (uint32_t*)w.keys2.p,
+                           (uint32_t*)w.vals2.p, m, MSM_BB + 5, s)))
+    return rc;
   PBF_HIP(hipMemsetAsync(w.start.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
@@ -584,6 +593,19 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   hipLaunchKernelGGL(msm_fx_total, dim3(MSM_NW), dim3(16), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
   PBF_HIP(hipGetLastError());
   return 0;
+}
+
+// The 16-window Horner on the device (A/B against msm_finish_host, PBF_MSM_DEVICE_HORNER=1): one
+// lane, 15 x (16 doublings + 1 addition) in sequence -- a latency chain that a GPU lane runs at
+// ~1 Fq product per ~2200 cycles, the host core far faster.
+__global__ void msm_horner_kernel(const Xyzz* sums, Xyzz* out) {
+  if (threadIdx.x != 0) return;
+  Xyzz acc = sums[MSM_NW - 1];
+  for (int w = MSM_NW - 2; w >= 0; --w) {
+    for (int i = 0; i < MSM_C; ++i) acc = G1::dbl(acc);
+    acc = G1::add(acc, sums[w]);
+  }
+  *out = acc;
 }
 
 static void msm_finish_host(const Xyzz* sums, uint64_t* out) {
@@ -738,7 +760,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   const int slot = tl.next;
   const std::string pre = "msm.f" + std::to_string(slot) + ".";
   DevBuf &keys = ctx->buf("msm.keys"), &vals = ctx->buf("msm.vals"), &keys2 = ctx->buf("msm.keys2"),
-         &vals2 = ctx->buf("msm.vals2"), &temp = ctx->buf("msm.temp");
+         &vals2 = ctx->buf("msm.vals2");
   DevBuf &start = ctx->buf(pre + "start"), &end = ctx->buf(pre + "end"), &buckets = ctx->buf(pre + "buckets"),
          &shares = ctx->buf(pre + "shares"), &parts = ctx->buf(pre + "parts"), &head = ctx->buf(pre + "head"),
          &tail = ctx->buf(pre + "tail"), &spb = ctx->buf(pre + "span");
@@ -756,12 +778,9 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   // ---- digits, sort by bucket, bucket bounds
   hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
                      (uint32_t*)keys.p, (uint32_t*)vals.p);
-  size_t temp_bytes = 0;
-  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
-                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, FX_C, s));
-  if ((rc = temp.ensure(temp_bytes ? temp_bytes : 1))) return rc;
-  PBF_HIP(hipcub::DeviceRadixSort::SortPairs(temp.p, temp_bytes, (const uint32_t*)keys.p, (uint32_t*)keys2.p,
-                                             (const uint32_t*)vals.p, (uint32_t*)vals2.p, (int)m, 0, FX_C, s));
+  if ((rc = msm_sort_pairs(ctx, (const uint32_t*)keys.p, (const uint32_t*)vals.p, (uint32_t*)keys2.p,
+                           (uint32_t*)vals2.p, m, FX_C, s)))
+    return rc;
   hipLaunchKernelGGL(msm_fx_clear, dim3(FX_NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
                      (uint32_t*)spb.p);
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
@@ -858,6 +877,17 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
   MsmWork w = msm_work(ctx);
   int rc = msm_device(ctx, d_points, d_scalars, n, s, w);
   if (rc) return rc;
+  if (getenv("PBF_MSM_DEVICE_HORNER")) {
+    DevBuf& res = ctx->buf("msm.horner");
+    if ((rc = res.ensure(sizeof(Xyzz)))) return rc;
+    hipLaunchKernelGGL(msm_horner_kernel, dim3(1), dim3(64), 0, s, (const Xyzz*)w.sums.p, (Xyzz*)res.p);
+    PBF_HIP(hipGetLastError());
+    Xyzz r;
+    PBF_HIP(hipMemcpyAsync(&r, res.p, sizeof(Xyzz), hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    xyzz_to_affine_u64(r, out);
+    return PBF_OK;
+  }
   std::vector<Xyzz> sums(MSM_NW);
   PBF_HIP(hipMemcpyAsync(sums.data(), w.sums.p, MSM_NW * sizeof(Xyzz), hipMemcpyDeviceToHost, s));
   PBF_HIP(hipStreamSynchronize(s));

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r03/pmc
 B="python bench.py --log-n ${LOGN:-24} --batch ${BATCH:-2} --steps 6 --warmup 1 --no-cpu --no-extra --no-traffic"
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE"
-for v in "v2 PBF_NTT_V2=1" "ip PBF_X=0"; do
+for v in "v2 PBF_NTT_V2=1" "ip PBF_NTT_IP=1"; do
   set -- $v; name=$1; shift
   i=0
   for ctr in "$SQ" "FETCH_SIZE" "WRITE_SIZE"; do
