@@ -37,6 +37,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FQ_MUL_PEAK = 1024 * 2.4e9 * 64 / (272 * 4)
 
 
+BUFFER_SETS = 3  # input/output pairs the NTT steps rotate over
+
+
 def root_of_unity(n: int) -> int:
     return pow(7, (GOLD - 1) // n, GOLD)
 
@@ -471,8 +474,17 @@ def other_configs(ctx, sp) -> dict:
     db[: la * 4] = rand_fr(la)
     dc = torch.empty_like(da)
     t = _median_ms(lambda: ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1, stream=sp))
-    res["config3_bn254_polymul_2p22"] = dict(t, ntt_elements_per_s=3 * n / (t["ms"] / 1e3),
-                                             note="2 forward + 1 inverse NTT of 2^23 + pointwise, 256-bit Montgomery")
+    # compute roofline: 3 (n/2) log2 n butterfly products + n
+    # pointwise products = 2.98e8 Fr products at n = 2^23, against the same instruction-level
+    # 254-bit Montgomery product rate as the MSM's Fq (FQ_MUL_PEAK; Fr and Fq are both 8 x 32-bit)
+    fr_products = 3 * (n // 2) * (n.bit_length() - 1) + n
+    ach3 = fr_products / (t["ms"] / 1e3)
+    res["config3_bn254_polymul_2p22"] = dict(
+        t, ntt_elements_per_s=3 * n / (t["ms"] / 1e3),
+        roofline={"bound": "valu (Fr products)", "achieved": ach3, "peak": FQ_MUL_PEAK, "unit": "Fr products/s",
+                  "frac": ach3 / FQ_MUL_PEAK, "fr_products": fr_products,
+                  "hbm_bytes_alg": 32 * 3 * n, "hbm_frac": 32 * 3 * n / (t["ms"] / 1e3) / 1e9 / HBM_PEAK_GBS},
+        note="2 forward + 1 inverse NTT of 2^23 + pointwise, 256-bit Montgomery")
     del da, db, dc
     # config 4: BN254 G1 MSM of 2^20 points (points = t_i * G from the batch fixed-base kernel)
     m = 1 << 20
@@ -561,13 +573,21 @@ def other_configs(ctx, sp) -> dict:
     return res
 
 
-def _single_gpu(ctx, n, B, sp):
+def _single_gpu(ctx, n, B, sp, sets: int = BUFFER_SETS):
+    """One step = one batched forward NTT of B x n. Consecutive steps rotate over `sets`
+    input/output buffer pairs (>= 3 sets, 3 x 512 MiB > the 256 MiB Infinity
+    Cache), so a step never finds its operands left in the MALL by the step before."""
     w = root_of_unity(n)
-    buf_in = torch.empty(B * n, dtype=torch.int64, device="cuda")
-    buf_out = torch.empty_like(buf_in)
-    ctx.fill_random_dev(GOLD, 0x5EED0002, buf_in.data_ptr(), B * n, stream=sp)
+    bufs = []
+    for i in range(sets):
+        buf_in = torch.empty(B * n, dtype=torch.int64, device="cuda")
+        ctx.fill_random_dev(GOLD, 0x5EED0002 + i, buf_in.data_ptr(), B * n, stream=sp)
+        bufs.append((buf_in, torch.empty_like(buf_in)))
+    k = [0]
 
     def step():
+        buf_in, buf_out = bufs[k[0] % sets]
+        k[0] += 1
         ctx.ntt_batch_dev(GOLD, w, buf_in.data_ptr(), buf_out.data_ptr(), n, B, stream=sp)
 
     return step, n

@@ -120,10 +120,14 @@ struct G1 {
     r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
     return r;
   }
-  // add / dbl with the independent products paired through F::mul2 (bit-identical results):
-  // 7 product pairs for add-2008-s and 5 steps for dbl-2008-s-1 instead of 14 and 9 single
-  // products. For single-lane latency chains (the MSM's reduction trees); the throughput
+  // add / dbl for single-lane latency chains (the MSM's joins and reduction trees), with the
+  // independent products of each step interleaved in one column scan (F::mulN / F::mul2,
+  // bit-identical results): add-2008-s in 4 dependent product steps (4 + 4 + 3 + 3 products)
+  // instead of 7 pairs, dbl-2008-s-1 in 4 (2 + 3 + 3 + 1). A lane's time on these chains is
+  // its dependency latency, not its issue count (one wave per SIMD), so wider steps are
+  // shorter chains. PBF_EC_PAIRS restores the round-2 pairing for A/B. The throughput
   // kernels keep add / dbl.
+#if defined(PBF_EC_PAIRS)
   __host__ __device__ __forceinline__ static Xyzz dbl2(const Xyzz& p) {
     if (is_identity(p)) return p;
     const U256 U = dbl_f(p.Y);
@@ -163,6 +167,76 @@ struct G1 {
     F::mul2(ZZ12, PP, ZZZ12, PPP, &r.ZZ, &r.ZZZ);
     return r;
   }
+#else
+  __host__ __device__ __forceinline__ static Xyzz dbl2(const Xyzz& p) {
+    if (is_identity(p)) return p;
+    const U256 U = dbl_f(p.Y);
+    U256 V, xx, W, S, ZZ3, MM, WY, ZZZ3;
+    F::mul2(U, U, p.X, p.X, &V, &xx);
+    {
+      const U256* x[3] = {&U, &p.X, &V};
+      const U256* y[3] = {&V, &V, &p.ZZ};
+      U256* o[3] = {&W, &S, &ZZ3};
+      F::template mulN<3>(x, y, o);
+    }
+    const U256 M = F::add(dbl_f(xx), xx);
+    {
+      const U256* x[3] = {&M, &W, &W};
+      const U256* y[3] = {&M, &p.Y, &p.ZZZ};
+      U256* o[3] = {&MM, &WY, &ZZZ3};
+      F::template mulN<3>(x, y, o);
+    }
+    Xyzz r;
+    r.X = F::sub(MM, dbl_f(S));
+    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), WY);
+    r.ZZ = ZZ3;
+    r.ZZZ = ZZZ3;
+    return r;
+  }
+  __host__ __device__ __forceinline__ static Xyzz add2(const Xyzz& p, const Xyzz& q) {
+    if (is_identity(p)) return q;
+    if (is_identity(q)) return p;
+    U256 U1, U2, S1, S2;
+    {
+      const U256* x[4] = {&p.X, &q.X, &p.Y, &q.Y};
+      const U256* y[4] = {&q.ZZ, &p.ZZ, &q.ZZZ, &p.ZZZ};
+      U256* o[4] = {&U1, &U2, &S1, &S2};
+      F::template mulN<4>(x, y, o);
+    }
+    const U256 P = F::sub(U2, U1);
+    const U256 R = F::sub(S2, S1);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return dbl2(p);
+      return identity();
+    }
+    U256 PP, RR, ZZ12, ZZZ12, PPP, Q, ZZ3, Y3a, S1P, ZZZ3;
+    {
+      const U256* x[4] = {&P, &R, &p.ZZ, &p.ZZZ};
+      const U256* y[4] = {&P, &R, &q.ZZ, &q.ZZZ};
+      U256* o[4] = {&PP, &RR, &ZZ12, &ZZZ12};
+      F::template mulN<4>(x, y, o);
+    }
+    {
+      const U256* x[3] = {&P, &U1, &ZZ12};
+      const U256* y[3] = {&PP, &PP, &PP};
+      U256* o[3] = {&PPP, &Q, &ZZ3};
+      F::template mulN<3>(x, y, o);
+    }
+    Xyzz r;
+    r.X = F::sub(F::sub(RR, PPP), dbl_f(Q));
+    const U256 QX = F::sub(Q, r.X);
+    {
+      const U256* x[3] = {&R, &S1, &ZZZ12};
+      const U256* y[3] = {&QX, &PPP, &PPP};
+      U256* o[3] = {&Y3a, &S1P, &ZZZ3};
+      F::template mulN<3>(x, y, o);
+    }
+    r.Y = F::sub(Y3a, S1P);
+    r.ZZ = ZZ3;
+    r.ZZZ = ZZZ3;
+    return r;
+  }
+#endif
   // k * p for a small non-negative k (double-and-add, MSB first)
   __host__ __device__ __forceinline__ static Xyzz mul_small(const Xyzz& p, uint32_t k) {
     Xyzz r = identity();

@@ -384,6 +384,80 @@ struct Fp256 {
     *r = reduce_once(ra);
     *s = reduce_once(rb);
   }
+  // Three independent chains: three v_mad_u64_u32, then their carry folds -- each carry is
+  // read two instructions after its write (the two wait states it needs, no pad).
+  __device__ __forceinline__ static void mac3(uint64_t& a0, uint32_t& a1, uint32_t xa, uint32_t ya, uint64_t& b0,
+                                              uint32_t& b1, uint32_t xb, uint32_t yb, uint64_t& c0, uint32_t& c1,
+                                              uint32_t xc, uint32_t yc) {
+    uint64_t ca, cb, cc;
+    asm("v_mad_u64_u32 %0, %3, %9, %10, %0\n\t"
+        "v_mad_u64_u32 %1, %4, %11, %12, %1\n\t"
+        "v_mad_u64_u32 %2, %5, %13, %14, %2\n\t"
+        "v_addc_co_u32_e64 %6, %3, %6, 0, %3\n\t"
+        "v_addc_co_u32_e64 %7, %4, %7, 0, %4\n\t"
+        "v_addc_co_u32_e64 %8, %5, %8, 0, %5"
+        : "+v"(a0), "+v"(b0), "+v"(c0), "=&s"(ca), "=&s"(cb), "=&s"(cc), "+v"(a1), "+v"(b1), "+v"(c1)
+        : "v"(xa), "v"(ya), "v"(xb), "v"(yb), "v"(xc), "v"(yc));
+  }
+  // N = 3 or 4 independent Montgomery products out[j] = x[j] y[j] by one interleaved column
+  // scan, one accumulator per chain (mac3 / mac4: no wait-state pads): bit-identical to N
+  // mul() calls. Point additions on single-lane latency chains group their independent
+  // products into these (ec_bn254.hpp add2 / dbl2): 4 dependent steps per addition instead of 7.
+  template <int N>
+  __device__ __forceinline__ static void mulN(const U256* const* x, const U256* const* y, U256* const* out) {
+    static_assert(N == 3 || N == 4, "mulN: 3 or 4 chains");
+    uint32_t m[N][8];
+    U256 res[N];
+    uint64_t c0[N];
+    uint32_t c1[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) { c0[j] = 0; c1[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const int lo = k < 8 ? 0 : k - 7, hi = k < 8 ? k : 7;
+      const int nm = k < 8 ? k : 8 - lo;
+#pragma unroll
+      for (int i = lo; i <= hi; ++i) {
+        if constexpr (N == 4)
+          mac4(c0[0], c1[0], x[0]->w[i], y[0]->w[k - i], c0[1], c1[1], x[1]->w[i], y[1]->w[k - i], c0[2], c1[2],
+               x[2]->w[i], y[2]->w[k - i], c0[3], c1[3], x[3]->w[i], y[3]->w[k - i]);
+        else
+          mac3(c0[0], c1[0], x[0]->w[i], y[0]->w[k - i], c0[1], c1[1], x[1]->w[i], y[1]->w[k - i], c0[2], c1[2],
+               x[2]->w[i], y[2]->w[k - i]);
+      }
+#pragma unroll
+      for (int i = lo; i < lo + nm; ++i) {
+        if constexpr (N == 4)
+          mac4(c0[0], c1[0], m[0][i], Prm::P[k - i], c0[1], c1[1], m[1][i], Prm::P[k - i], c0[2], c1[2], m[2][i],
+               Prm::P[k - i], c0[3], c1[3], m[3][i], Prm::P[k - i]);
+        else
+          mac3(c0[0], c1[0], m[0][i], Prm::P[k - i], c0[1], c1[1], m[1][i], Prm::P[k - i], c0[2], c1[2], m[2][i],
+               Prm::P[k - i]);
+      }
+      if (k < 8) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) m[j][k] = (uint32_t)c0[j] * Prm::NP;
+        if constexpr (N == 4)
+          mac4(c0[0], c1[0], m[0][k], Prm::P[0], c0[1], c1[1], m[1][k], Prm::P[0], c0[2], c1[2], m[2][k], Prm::P[0],
+               c0[3], c1[3], m[3][k], Prm::P[0]);
+        else
+          mac3(c0[0], c1[0], m[0][k], Prm::P[0], c0[1], c1[1], m[1][k], Prm::P[0], c0[2], c1[2], m[2][k], Prm::P[0]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) res[j].w[k - 8] = (uint32_t)c0[j];
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        c0[j] = (c0[j] >> 32) | ((uint64_t)c1[j] << 32);
+        c1[j] = 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      res[j].w[7] = (uint32_t)c0[j];
+      *out[j] = reduce_once(res[j]);
+    }
+  }
 #else
   // -p^-1 mod 2^64 from the 32-bit constant's modulus by Newton's iteration (x <- x(2 - p x)
   // doubles the correct low bits; p is odd so x = p is right mod 2^3)
@@ -452,6 +526,12 @@ struct Fp256 {
   static void mul2(const U256& a, const U256& b, const U256& c, const U256& d, U256* r, U256* s) {
     *r = mul(a, b);
     *s = mul(c, d);
+  }
+  template <int N>
+  static void mulN(const U256* const* x, const U256* const* y, U256* const* out) {
+    U256 t[N];
+    for (int j = 0; j < N; ++j) t[j] = mul(*x[j], *y[j]);  // inputs may alias outputs
+    for (int j = 0; j < N; ++j) *out[j] = t[j];
   }
   // CIOS Montgomery product over 8 x 32-bit limbs (host cross-check of mul)
   static U256 mul_cios32(const U256& a, const U256& b) {

@@ -371,25 +371,28 @@ __global__ void __launch_bounds__(256) msm_fx_cd(const Xyzz* buckets, const Chun
 }
 // The same C_h / D_l sums for many windows at once (the windowed MSM: 16 x 384 trees), where
 // throughput matters more than depth: a 256-tree keeps on average a quarter of its lanes
-// busy, so each thread first adds 8 buckets in sequence. Workgroup (g, w), g < 16: C_h for
-// h = 8g .. 8g+7 (32 threads per h, 8 consecutive buckets each, then 32-lane trees);
-// g >= 16: D_l for l = 16(g-16) .. +15 (16 threads per l, 8 values of h each, then 16-lane
-// trees).
+// busy, so each thread first adds SEQ buckets in sequence. Workgroup (g, w), g < 128 / SEQ:
+// C_h for h = SEQ g .. SEQ g + SEQ - 1 (256 / SEQ threads per h, SEQ consecutive buckets
+// each, then (256 / SEQ)-lane trees); the other 128 / SEQ workgroups: D_l for 2 SEQ values
+// of l each (128 / SEQ threads per l, SEQ values of h each, then (128 / SEQ)-lane trees).
+// SEQ trades depth (SEQ + log2(lanes) additions) against waves in flight (PBF_MSM_CD_SEQ).
+template <int SEQ>
 __global__ void __launch_bounds__(256) msm_fx_cd_seq(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
                                                      const uint32_t* start, const uint32_t* end, Xyzz* cd) {
   __shared__ Xyzz red[256];
+  constexpr uint32_t CL = 256 / SEQ, DL = 128 / SEQ, CG = 128 / SEQ;  // lanes per C / D tree
   const uint32_t g = blockIdx.x, t = threadIdx.x, base = blockIdx.y * FX_NB;
   Xyzz* out = cd + (uint64_t)blockIdx.y * (FX_NH + 256);
   Xyzz acc = G1::identity();
   uint32_t lanes;
-  if (g < 16) {
-    const uint32_t h = 8 * g + t / 32, l0 = (t % 32) * 8;
-    for (uint32_t i = 0; i < 8; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * h + l0 + i, buckets, head, tail, start, end));
-    lanes = 32;
+  if (g < CG) {
+    const uint32_t h = SEQ * g + t / CL, l0 = (t % CL) * SEQ;
+    for (uint32_t i = 0; i < SEQ; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * h + l0 + i, buckets, head, tail, start, end));
+    lanes = CL;
   } else {
-    const uint32_t l = 16 * (g - 16) + t / 16, h0 = (t % 16) * 8;
-    for (uint32_t i = 0; i < 8; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * (h0 + i) + l, buckets, head, tail, start, end));
-    lanes = 16;
+    const uint32_t l = 2 * SEQ * (g - CG) + t / DL, h0 = (t % DL) * SEQ;
+    for (uint32_t i = 0; i < SEQ; ++i) acc = G1::add2(acc, fx_bucket(base + 256 * (h0 + i) + l, buckets, head, tail, start, end));
+    lanes = DL;
   }
   red[t] = acc;
   __syncthreads();
@@ -397,7 +400,7 @@ __global__ void __launch_bounds__(256) msm_fx_cd_seq(const Xyzz* buckets, const 
     if (t % lanes < st) red[t] = G1::add2(red[t], red[t + st]);
     __syncthreads();
   }
-  if (t % lanes == 0) out[g < 16 ? 8 * g + t / 32 : FX_NH + 16 * (g - 16) + t / 16] = red[t];
+  if (t % lanes == 0) out[g < CG ? SEQ * g + t / CL : FX_NH + 2 * SEQ * (g - CG) + t / DL] = red[t];
 }
 // workgroup (s, w) (128 threads): s < 8: 2^s Y_s; 8 <= s < 15: 2^s Z_(s-8); s = 15: S.
 __global__ void __launch_bounds__(128) msm_fx_subsets(const Xyzz* cd, Xyzz* sub) {
@@ -586,9 +589,15 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   }
   hipLaunchKernelGGL(msm_join_rest, dim3(NBT / 256), dim3(256), 0, s, (ChunkPart*)w.head.p,
                      (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, (const uint32_t*)w.span.p);
-  hipLaunchKernelGGL(msm_fx_cd_seq, dim3(16 + 16, MSM_NW), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
-                     (const ChunkPart*)w.head.p, (const ChunkPart*)w.tail.p, (const uint32_t*)w.start.p,
-                     (const uint32_t*)w.end.p, (Xyzz*)w.shares.p);
+  {
+    const char* e = getenv("PBF_MSM_CD_SEQ");  // read per call: an A/B knob
+    const int v = e ? atoi(e) : 8;
+    const int cd_seq = v == 2 || v == 4 || v == 16 ? v : 8;
+    auto* fn = cd_seq == 2 ? msm_fx_cd_seq<2> : cd_seq == 4 ? msm_fx_cd_seq<4> : cd_seq == 16 ? msm_fx_cd_seq<16> : msm_fx_cd_seq<8>;
+    hipLaunchKernelGGL(fn, dim3(256 / cd_seq, MSM_NW), dim3(256), 0, s, (const Xyzz*)w.buckets.p,
+                       (const ChunkPart*)w.head.p, (const ChunkPart*)w.tail.p, (const uint32_t*)w.start.p,
+                       (const uint32_t*)w.end.p, (Xyzz*)w.shares.p);
+  }
   hipLaunchKernelGGL(msm_fx_subsets, dim3(16, MSM_NW), dim3(128), 0, s, (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
   hipLaunchKernelGGL(msm_fx_total, dim3(MSM_NW), dim3(16), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
   PBF_HIP(hipGetLastError());

@@ -10,4 +10,4 @@ timeout -k 10 240 python -u scripts/r03/msm_time.py 2>&1 | grep -v amdgpu.ids ||
 export TMPDIR=/tmp
 rm -rf gpurun_out/r03/msm_prof2
 timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/r03/msm_prof2 -o k -- python scripts/r03/msm_time.py > /dev/null 2>&1 || exit 1
-scripts/r03/pmc_ab.sh
+scripts/r03/pmc_ab.sh && scripts/r03/fetch_cal.sh

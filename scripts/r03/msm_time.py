@@ -27,6 +27,12 @@ ctx.g1_mul_base_dev(t.data_ptr(), pts.data_ptr(), m, stream=sp)
 torch.cuda.synchronize()
 r0 = ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp)
 print("windowed host Horner", _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp), reps=11))
+for seq in ("2", "4", "16"):
+    os.environ["PBF_MSM_CD_SEQ"] = seq
+    rs = ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp)
+    print(f"windowed cd_seq={seq}", _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp),
+                                               reps=11), "same result", rs == r0)
+del os.environ["PBF_MSM_CD_SEQ"]
 os.environ["PBF_MSM_DEVICE_HORNER"] = "1"
 r1 = ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp)
 print("windowed device Horner", _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp), reps=11),
