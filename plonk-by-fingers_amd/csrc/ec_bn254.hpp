@@ -273,4 +273,116 @@ struct G1 {
   }
 };
 
+// ---- quad-lane point arithmetic for latency chains (the MSM's bucket-reduction tails) -----
+// The four lanes of a quad (lanes 4i .. 4i+3) hold the same operands. Each dependent product
+// step of add-2008-s / dbl-2008-s-1 (the 4 + 4 + 3 + 3 and 2 + 3 + 3 + 1 steps of add2 /
+// dbl2) computes product i on lane i and broadcasts the results across the quad with DPP
+// quad_perm moves (8 dwords per product), so a step costs one product of latency instead of
+// three or four interleaved ones. The additions and subtractions run redundantly on all four
+// lanes, and every branch depends only on quad-uniform values, so a quad never diverges. The
+// results are bit-identical to add2 / dbl2 (same formulas, same products). Callers keep all
+// four lanes of a quad active together.
+struct G1Quad {
+  typedef Fq F;
+  template <int SRC>
+  __device__ __forceinline__ static U256 bcast(const U256& v) {
+    constexpr int ctrl = SRC | (SRC << 2) | (SRC << 4) | (SRC << 6);  // quad_perm [SRC x 4]
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.w[i], ctrl, 0xF, 0xF, false);
+    return r;
+  }
+  __device__ __forceinline__ static U256 sel(uint32_t l, const U256& a, const U256& b, const U256& c, const U256& d) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = l == 0 ? a.w[i] : (l == 1 ? b.w[i] : (l == 2 ? c.w[i] : d.w[i]));
+    return r;
+  }
+  // out_i = x_i * y_i for i < N (N = 2, 3 or 4), product i on lane i of the quad
+  template <int N>
+  __device__ __forceinline__ static void mulN(const U256* const* x, const U256* const* y, U256* const* out) {
+    const uint32_t l = threadIdx.x & 3;
+    const U256 xs = sel(l, *x[0], *x[1], *x[N > 2 ? 2 : 1], *x[N > 3 ? 3 : N - 1]);
+    const U256 ys = sel(l, *y[0], *y[1], *y[N > 2 ? 2 : 1], *y[N > 3 ? 3 : N - 1]);
+    const U256 r = F::mul(xs, ys);
+    *out[0] = bcast<0>(r);
+    *out[1] = bcast<1>(r);
+    if constexpr (N > 2) *out[2] = bcast<2>(r);
+    if constexpr (N > 3) *out[3] = bcast<3>(r);
+  }
+  __device__ __forceinline__ static Xyzz dbl(const Xyzz& p) {
+    if (G1::is_identity(p)) return p;
+    const U256 U = G1::dbl_f(p.Y);
+    U256 V, xx, W, S, ZZ3, MM, WY, ZZZ3;
+    {
+      const U256* x[2] = {&U, &p.X};
+      const U256* y[2] = {&U, &p.X};
+      U256* o[2] = {&V, &xx};
+      mulN<2>(x, y, o);
+    }
+    {
+      const U256* x[3] = {&U, &p.X, &V};
+      const U256* y[3] = {&V, &V, &p.ZZ};
+      U256* o[3] = {&W, &S, &ZZ3};
+      mulN<3>(x, y, o);
+    }
+    const U256 M = F::add(G1::dbl_f(xx), xx);
+    {
+      const U256* x[3] = {&M, &W, &W};
+      const U256* y[3] = {&M, &p.Y, &p.ZZZ};
+      U256* o[3] = {&MM, &WY, &ZZZ3};
+      mulN<3>(x, y, o);
+    }
+    Xyzz r;
+    r.X = F::sub(MM, G1::dbl_f(S));
+    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), WY);
+    r.ZZ = ZZ3;
+    r.ZZZ = ZZZ3;
+    return r;
+  }
+  __device__ __forceinline__ static Xyzz add(const Xyzz& p, const Xyzz& q) {
+    if (G1::is_identity(p)) return q;
+    if (G1::is_identity(q)) return p;
+    U256 U1, U2, S1, S2;
+    {
+      const U256* x[4] = {&p.X, &q.X, &p.Y, &q.Y};
+      const U256* y[4] = {&q.ZZ, &p.ZZ, &q.ZZZ, &p.ZZZ};
+      U256* o[4] = {&U1, &U2, &S1, &S2};
+      mulN<4>(x, y, o);
+    }
+    const U256 P = F::sub(U2, U1);
+    const U256 R = F::sub(S2, S1);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return dbl(p);
+      return G1::identity();
+    }
+    U256 PP, RR, ZZ12, ZZZ12, PPP, Q, ZZ3, Y3a, S1P, ZZZ3;
+    {
+      const U256* x[4] = {&P, &R, &p.ZZ, &p.ZZZ};
+      const U256* y[4] = {&P, &R, &q.ZZ, &q.ZZZ};
+      U256* o[4] = {&PP, &RR, &ZZ12, &ZZZ12};
+      mulN<4>(x, y, o);
+    }
+    {
+      const U256* x[3] = {&P, &U1, &ZZ12};
+      const U256* y[3] = {&PP, &PP, &PP};
+      U256* o[3] = {&PPP, &Q, &ZZ3};
+      mulN<3>(x, y, o);
+    }
+    Xyzz r;
+    r.X = F::sub(F::sub(RR, PPP), G1::dbl_f(Q));
+    const U256 QX = F::sub(Q, r.X);
+    {
+      const U256* x[3] = {&R, &S1, &ZZZ12};
+      const U256* y[3] = {&QX, &PPP, &PPP};
+      U256* o[3] = {&Y3a, &S1P, &ZZZ3};
+      mulN<3>(x, y, o);
+    }
+    r.Y = F::sub(Y3a, S1P);
+    r.ZZ = ZZ3;
+    r.ZZZ = ZZZ3;
+    return r;
+  }
+};
+
 }  // namespace pbf

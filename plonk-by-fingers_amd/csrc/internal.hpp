@@ -78,6 +78,11 @@ struct NttPlan {
   int tws_w = 0;
   // round-3 schedule (ntt_ip.hpp): in-place digit slots, persistent prefetching passes;
   // ip_r = radix bits per pass (top slot first), per-pass twiddle and stage-C tables
+  // regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel): 8,8,8 passes with the general
+  // twiddles between 64-point blocks only; tables tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18),
+  // t3[f][a0][j] (2^24, n^-1 folded in for the inverse)
+  bool rg = false;
+  DevBuf rg_tc1, rg_t2, rg_t3;
   bool ip = false;
   std::vector<int> ip_r;
   std::vector<std::shared_ptr<DevBuf>> ip_tw, ip_tc;

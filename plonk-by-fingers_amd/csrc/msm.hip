@@ -133,17 +133,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
       buckets[cur] = acc;
     }
   };
-  // the next entry's key, index and point are loaded while the current addition runs
-  // (the point gathers are random: their latency would otherwise stall every step)
+  // the next entry's point and the entry after it's key and index are loaded while the
+  // current addition runs (the point gathers are random: their latency would otherwise stall
+  // every step, and a point's address is known only once its index has arrived)
   uint32_t k_nx = cur, v_nx = vals[c0];
   Affine p_nx = pts[v_nx & ~MSM_NEG];
+  uint32_t k_n2 = 0, v_n2 = 0;
+  if (c0 + 1 < c1) k_n2 = keys[c0 + 1], v_n2 = vals[c0 + 1];
   for (uint32_t j = c0; j < c1; ++j) {
     const uint32_t k = k_nx, v = v_nx;
     Affine p = p_nx;
     if (j + 1 < c1) {
-      k_nx = keys[j + 1];
-      v_nx = vals[j + 1];
+      k_nx = k_n2;
+      v_nx = v_n2;
       p_nx = pts[v_nx & ~MSM_NEG];  // a sentinel entry's index is still a valid point
+      if (j + 2 < c1) k_n2 = keys[j + 2], v_n2 = vals[j + 2];
     }
     if (k != cur) {
       flush(j);
@@ -430,6 +434,83 @@ __global__ void __launch_bounds__(16) msm_fx_total(const Xyzz* sub, Xyzz* out) {
   fx_tree(sub[blockIdx.x * 16 + threadIdx.x], out + blockIdx.x);
 }
 
+// ---- the same reduction tail on quads (G1Quad: each point addition's product steps spread
+// over the four lanes of a quad), the default: these kernels are latency chains of a few
+// hundred waves, so a chain of quad additions (one product of latency per step) finishes
+// about 3x sooner than one of single-lane additions (three or four interleaved products per
+// step). PBF_MSM_QUAD=0 restores the single-lane kernels above (A/B).
+__device__ __forceinline__ Xyzz fx_bucket_q(uint32_t k, const Xyzz* buckets, const ChunkPart* head,
+                                            const ChunkPart* tail, const uint32_t* start, const uint32_t* end) {
+  const uint32_t bs = start[k], be = end[k];
+  if (be <= bs) return G1::identity();
+  const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+  return o < e ? G1Quad::add(tail[o].acc, head[o + 1].acc) : buckets[k];
+}
+// Quad-tree sum of one value per quad (blockDim.x / 4 quads, a power of two); quad 0 returns
+// the total (the other quads' return values are partial sums).
+__device__ __forceinline__ Xyzz fx_tree_q(Xyzz v, Xyzz* red) {
+  const uint32_t t = threadIdx.x, qi = t >> 2, nq = blockDim.x >> 2;
+  if ((t & 3) == 0) red[qi] = v;
+  __syncthreads();
+  for (uint32_t st = nq / 2; st > 0; st >>= 1) {
+    if (qi < st) v = G1Quad::add(v, red[qi + st]);
+    __syncthreads();
+    if (qi < st && (t & 3) == 0) red[qi] = v;
+    __syncthreads();
+  }
+  return v;
+}
+// msm_fx_cd on quads: workgroup (g, w) of 256 threads (64 quads); g < 128: C_g, each quad
+// first adds 4 consecutive buckets; g >= 128: D_(g-128), each quad 2 values of h.
+__global__ void __launch_bounds__(256) msm_fx_cd_q(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
+                                                   const uint32_t* start, const uint32_t* end, Xyzz* cd) {
+  __shared__ Xyzz red[64];
+  const uint32_t g = blockIdx.x, qi = threadIdx.x >> 2, base = blockIdx.y * FX_NB;
+  Xyzz v = G1::identity();
+  if (g < FX_NH) {
+    for (uint32_t i = 0; i < 4; ++i)
+      v = G1Quad::add(v, fx_bucket_q(base + 256 * g + 4 * qi + i, buckets, head, tail, start, end));
+  } else {
+    for (uint32_t i = 0; i < 2; ++i)
+      v = G1Quad::add(v, fx_bucket_q(base + 256 * (2 * qi + i) + (g - FX_NH), buckets, head, tail, start, end));
+  }
+  v = fx_tree_q(v, red);
+  if (threadIdx.x == 0) cd[(uint64_t)blockIdx.y * (FX_NH + 256) + g] = v;
+}
+// msm_fx_subsets on quads: workgroup (s, w) of 512 threads (128 quads), quad i in the role of
+// thread i there; quad 0 then applies the 2^s weight.
+__global__ void __launch_bounds__(512) msm_fx_subsets_q(const Xyzz* cd, Xyzz* sub) {
+  __shared__ Xyzz red[128];
+  const uint32_t s = blockIdx.x, t = threadIdx.x >> 2;
+  const Xyzz* C = cd + (uint64_t)blockIdx.y * (FX_NH + 256);
+  const Xyzz* D = C + FX_NH;
+  Xyzz v;
+  if (s < 8) {
+    v = D[((t >> s) << (s + 1)) | (1u << s) | (t & ((1u << s) - 1))];
+  } else if (s < 15) {
+    const uint32_t k = s - 8;
+    v = t < 64 ? C[((t >> k) << (k + 1)) | (1u << k) | (t & ((1u << k) - 1))] : G1::identity();
+  } else {
+    v = C[t];
+  }
+  v = fx_tree_q(v, red);
+  if (t == 0) {
+    const uint32_t e = s < 15 ? s : 0;
+    for (uint32_t i = 0; i < e; ++i) v = G1Quad::dbl(v);
+    if (threadIdx.x == 0) sub[blockIdx.y * 16 + s] = v;
+  }
+}
+// msm_fx_total on quads: workgroup w of 64 threads (16 quads)
+__global__ void __launch_bounds__(64) msm_fx_total_q(const Xyzz* sub, Xyzz* out) {
+  __shared__ Xyzz red[16];
+  const Xyzz v = fx_tree_q(sub[blockIdx.x * 16 + (threadIdx.x >> 2)], red);
+  if (threadIdx.x == 0) out[blockIdx.x] = v;
+}
+static bool msm_quad_tail() {
+  const char* e = getenv("PBF_MSM_QUAD");  // read per call: an A/B knob
+  return !(e && atoi(e) == 0);
+}
+
 // Exact-content cache validation (snapshot_check below): diff[0] = 1 when a and b differ in
 // any of their `words` u64 (benign same-value race; vector stores only).
 __global__ void __launch_bounds__(256) k_snap_compare(const uint64_t* a, const uint64_t* b, uint64_t words, int* diff) {
@@ -598,8 +679,13 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
                        (const ChunkPart*)w.head.p, (const ChunkPart*)w.tail.p, (const uint32_t*)w.start.p,
                        (const uint32_t*)w.end.p, (Xyzz*)w.shares.p);
   }
-  hipLaunchKernelGGL(msm_fx_subsets, dim3(16, MSM_NW), dim3(128), 0, s, (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
-  hipLaunchKernelGGL(msm_fx_total, dim3(MSM_NW), dim3(16), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
+  if (msm_quad_tail()) {
+    hipLaunchKernelGGL(msm_fx_subsets_q, dim3(16, MSM_NW), dim3(512), 0, s, (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
+    hipLaunchKernelGGL(msm_fx_total_q, dim3(MSM_NW), dim3(64), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
+  } else {
+    hipLaunchKernelGGL(msm_fx_subsets, dim3(16, MSM_NW), dim3(128), 0, s, (const Xyzz*)w.shares.p, (Xyzz*)w.parts.p);
+    hipLaunchKernelGGL(msm_fx_total, dim3(MSM_NW), dim3(16), 0, s, (const Xyzz*)w.parts.p, (Xyzz*)w.sums.p);
+  }
   PBF_HIP(hipGetLastError());
   return 0;
 }
@@ -818,10 +904,18 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   }
   hipLaunchKernelGGL(msm_join_rest, dim3(FX_NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
                      (const uint32_t*)end.p, FX_NB, (const uint32_t*)spb.p);
-  hipLaunchKernelGGL(msm_fx_cd, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p, (const ChunkPart*)head.p,
-                     (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p);
-  hipLaunchKernelGGL(msm_fx_subsets, dim3(16), dim3(128), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
-  hipLaunchKernelGGL(msm_fx_total, dim3(1), dim3(16), 0, a, (const Xyzz*)parts.p, d_result);
+  if (msm_quad_tail()) {
+    hipLaunchKernelGGL(msm_fx_cd_q, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
+                       (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
+                       (const uint32_t*)end.p, (Xyzz*)shares.p);
+    hipLaunchKernelGGL(msm_fx_subsets_q, dim3(16), dim3(512), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
+    hipLaunchKernelGGL(msm_fx_total_q, dim3(1), dim3(64), 0, a, (const Xyzz*)parts.p, d_result);
+  } else {
+    hipLaunchKernelGGL(msm_fx_cd, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p, (const ChunkPart*)head.p,
+                       (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p);
+    hipLaunchKernelGGL(msm_fx_subsets, dim3(16), dim3(128), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
+    hipLaunchKernelGGL(msm_fx_total, dim3(1), dim3(16), 0, a, (const Xyzz*)parts.p, d_result);
+  }
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipEventRecord(tl.done[slot], a));
   tl.used[slot] = true;

@@ -103,6 +103,27 @@ __device__ __forceinline__ void gl_stage_b_twiddle(uint64_t* v) {
   }
 }
 
+// v[bitrev4(e)] *= w_64^(e*Q) = 2^(E64*e*Q): a twiddle on the bit-reversed outputs of a
+// 16-point register DFT
+template <int E64, int Q, int E = 1>
+__device__ __forceinline__ void gl_post_twiddle_br(uint64_t* v) {
+  if constexpr (E < 16) {
+    v[bitrev_c(E, 4)] = gl_pow2<(E64 * E * Q) % 192>(v[bitrev_c(E, 4)]);
+    gl_post_twiddle_br<E64, Q, E + 1>(v);
+  }
+}
+// RG 3 stage C: x[u*4 + r2] *= w_64^(r2 g), g = WV + 4 u (r2 = 1..3, u = 0..3)
+template <int E64, int WV, int U = 0>
+__device__ __forceinline__ void gl_rg3_c_shift(uint64_t* x) {
+  if constexpr (U < 4) {
+    constexpr int g = WV + 4 * U;
+    x[U * 4 + 1] = gl_pow2<(E64 * g) % 192>(x[U * 4 + 1]);
+    x[U * 4 + 2] = gl_pow2<(E64 * 2 * g) % 192>(x[U * 4 + 2]);
+    x[U * 4 + 3] = gl_pow2<(E64 * 3 * g) % 192>(x[U * 4 + 3]);
+    gl_rg3_c_shift<E64, WV, U + 1>(x);
+  }
+}
+
 template <int LOGR, int TILE>
 struct GlShape {
   static constexpr int R = 1 << LOGR;
@@ -189,12 +210,14 @@ constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
 // tile as one contiguous 64-KiB block instead of 64-B runs n/R apart; the first pass
 // stores 512-B runs (a wave covers 8 k x 8 j). FIRST && BLK: blocked store; !FIRST &&
 // BLK: blocked load.
-template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false>
+// RG (regrouped 2^24 plan, gl_rg2_tile below): 1 = its first pass, 3 = its last pass.
+template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false, int RG = 0>
 __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t,
                                         uint32_t next) {
   using Sh = GlShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
   static_assert(Sh::NSUB_C * C == GL_STORES, "stores per thread");
+  static_assert(RG == 0 || (LOGR == 8 && TILE == 4096 && !PERSIST && !BLK && FIRST == (RG == 1)), "RG shape");
   const FieldArgs f{};
   using G = Goldilocks;
   uint32_t poly, kb;
@@ -225,7 +248,17 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
         v[u * 4 + s1] = in[(j0 + w) + (uint64_t)r * stride];
     }
   }
-  if constexpr (!FIRST) {
+  // RG 3: the stage-B general twiddle T3[q1][a0][j] (a0 = r2 + 4 s2), loaded now (in flight
+  // during stage A) in the stage-B thread mapping
+  uint64_t t3[RG == 3 ? 16 : 1];
+  if constexpr (RG == 3) {
+    const int wave = t >> 6, q1 = wave / Sh::WPQ, rw = (wave % Sh::WPQ) * 64 + (t & 63);
+    const int r2 = rw / W, w = rw % W;
+    const uint64_t* tb = a.twpass + ((uint64_t)(q1 * 64 + r2) << 16) + j0 + w;
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) t3[s2] = tb[(uint64_t)(4 * s2) << 16];
+  }
+  if constexpr (!FIRST && RG != 3) {
     const uint64_t kmask = (1ull << a.log_ns) - 1;
     // in groups of 8 elements (loads of a group issue back to back; bounded live registers)
 #pragma unroll
@@ -281,11 +314,16 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
 #ifndef PBF_GL_NOMATH
-    switch (__builtin_amdgcn_readfirstlane(q1)) {
-      case 1: gl_stage_b_twiddle<E64, 1>(v); break;
-      case 2: gl_stage_b_twiddle<E64, 2>(v); break;
-      case 3: gl_stage_b_twiddle<E64, 3>(v); break;
-      default: break;
+    if constexpr (RG == 3) {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) v[s2] = G::mul(v[s2], t3[s2], f);
+    } else {
+      switch (__builtin_amdgcn_readfirstlane(q1)) {
+        case 1: gl_stage_b_twiddle<E64, 1>(v); break;
+        case 2: gl_stage_b_twiddle<E64, 2>(v); break;
+        case 3: gl_stage_b_twiddle<E64, 3>(v); break;
+        default: break;
+      }
     }
     dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
 #endif
@@ -323,9 +361,55 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
   }
-  {
+  if constexpr (RG == 3) {
+    // w_64^(r2 g), g = k1 >> 2 = wave + 4 u (4-wave tiles, W = 16): wave-uniform shifts
+    switch (__builtin_amdgcn_readfirstlane(t >> 6)) {
+      case 0: gl_rg3_c_shift<E64, 0>(x); break;
+      case 1: gl_rg3_c_shift<E64, 1>(x); break;
+      case 2: gl_rg3_c_shift<E64, 2>(x); break;
+      default: gl_rg3_c_shift<E64, 3>(x); break;
+    }
+  } else if constexpr (RG == 1) {
+    // tc[a2l][r2][k1] = w_4096^((a2l + 16 r2) k1), a2l = bits 12..15 of the column: every row
+    const uint64_t* tc = a.tc + ((j0 >> 12) & 15) * 256;
+#pragma unroll
+    for (int u = 0; u < Sh::NSUB_C; ++u) {
+      int k1, w;
+      c_map(u, &k1, &w);
+      uint64_t tw[C];
+#pragma unroll
+      for (int r2 = 0; r2 < C; ++r2) tw[r2] = tc[r2 * 64 + k1];
+#pragma unroll
+      for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = G::mul(x[u * C + r2], tw[r2], f);
+    }
+  } else {
     uint64_t tw[Sh::NSUB_C * C];
     const int r2lo = a.scaled ? 0 : 1;  // scaled table carries n^-1: every element multiplies
+#ifdef PBF_GL_SHFL_TW
+    // A/B build (make shfltw): wavefront-shuffle twiddle broadcast. In later passes a wave's
+    // lanes need only NSUB_C x C x 64/W distinct stage-C twiddles (k1 = idx / W: W lanes share
+    // one); lane L loads twiddle L once, and every lane takes its values from the owning lanes
+    // with ds_bpermute instead of issuing NSUB_C x C broadcast-address global loads.
+    constexpr int PERW = W <= 64 ? 64 / W : 1;
+    constexpr int CNT = Sh::NSUB_C * C * PERW;  // shapes with CNT > 64 keep the loads
+    if constexpr (!FIRST && W <= 64 && CNT <= 64) {
+      const int lane = t & 63, wbase = t & ~63;
+      uint64_t mine = 1;
+      if (lane < CNT) {
+        const int u = lane / (C * PERW), r2 = (lane / PERW) % C, d = lane % PERW;
+        mine = a.tc[r2 * 64 + (wbase + NT * u) / W + d];
+      }
+#pragma unroll
+      for (int u = 0; u < Sh::NSUB_C; ++u)
+#pragma unroll
+        for (int r2 = 0; r2 < C; ++r2) {
+          const int src = ((u * C + r2) * PERW + lane / W) * 4;
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mine);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mine >> 32));
+          tw[u * C + r2] = (r2 >= r2lo) ? (((uint64_t)hi << 32) | lo) : 1;
+        }
+    } else
+#endif
 #pragma unroll
     for (int u = 0; u < Sh::NSUB_C; ++u) {
       int k1, w;
@@ -430,13 +514,80 @@ __device__ __forceinline__ void gl_shape_checks() {
 }
 
 // One tile per workgroup.
-template <int LOGR, int E64, bool FIRST, int TILE, bool BLK = false>
+template <int LOGR, int E64, bool FIRST, int TILE, bool BLK = false, int RG = 0>
 __global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_gl_pass_kernel(GlPassArgs a) {
   gl_shape_checks<LOGR, TILE>();
   __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
   const uint32_t tiles = a.blocks_per_poly * a.batch;
-  gl_tile<LOGR, E64, FIRST, TILE, false, BLK>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
+  gl_tile<LOGR, E64, FIRST, TILE, false, BLK, RG>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
+}
+
+// ---- regrouped 2^24 plan (DESIGN.md §3.1 "Regrouped twiddles") --------------------------
+// The three radix-2^8 passes of a 2^24 transform re-cut so that every general (table)
+// twiddle sits between DFT blocks of 64 points: with the index bits in four groups of six,
+// j = a0 + 64 a1 + 4096 a2 + 2^18 a3 and k = b0 + 64 b1 + 4096 b2 + 2^18 b3, decimation in
+// frequency needs only the three twiddle layers w^(4096 a2 b0), w^(64 a1 (b0 + 64 b1)) and
+// w^(a0 (b0 + 64 b1 + 4096 b2)); each 64-point group DFT that straddles two passes is split
+// 4 x 16 or 16 x 4 with a w_64 (shift) twiddle between its halves. Per element that is 3
+// general multiplications for the whole transform instead of 4.25 (0.75 + 1.75 + 1.75):
+//   pass 1 (RG 1): DFT-64 over a3 | w_4096^(a2 b0) (a2l = bits 12..15 of the column) | DFT-4
+//   pass 2 (this kernel): w_64^(a2l c) | DFT-16 over a2l | T2[a1][K] | DFT-16 over a1h | w_64^(a1l e)
+//   pass 3 (RG 3): DFT-4 over a1l | T3[f][a0][j] | DFT-16 | w_64^(r2 g) | DFT-4
+// Pass 2 needs one LDS exchange (two 16-point stages), not two. Data stays in the Stockham
+// layout of the other passes (natural order in and out).
+// Pass 2 tile: 256 rows r = 16 a2l + a1h x W = 16 columns j (Ns = 256: j mod 256 = b0 + 64 c,
+// the first pass's output digit; bits 14..15 of j = a1l); stage X thread (a1h, w), stage Y
+// thread (d, w); LDS [d][a1h][w] with rows padded by 8 elements (the stage-Y reads of four d
+// per wave then hit every bank exactly twice).
+template <int E64>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ntt_gl_rg2_kernel(GlPassArgs a) {
+  constexpr int W = 16, PD = 16 * W + 8;
+  __shared__ __attribute__((aligned(16))) uint64_t lds[16 * PD];
+  const FieldArgs f{};
+  using G = Goldilocks;
+  const uint32_t tiles = a.blocks_per_poly * a.batch;
+  uint32_t poly, kb;
+  gl_tile_coords(a, blockIdx.x, tiles, &poly, &kb);
+  const int t = threadIdx.x, w = t % W, a1h = t / W;
+  const uint64_t j0 = (uint64_t)kb * W, j = j0 + w;
+  const uint32_t c = (uint32_t)(j0 >> 6) & 3, a1l = (uint32_t)(j0 >> 14) & 3;
+  const uint64_t* in = a.in + (uint64_t)poly * a.in_pitch;
+  const uint64_t stride = a.n >> 8;
+  uint64_t v[16], tw[16];
+#pragma unroll
+  for (int a2l = 0; a2l < 16; ++a2l) v[a2l] = in[j + (uint64_t)(a2l * 16 + a1h) * stride];
+  {
+    // T2[a1][K] = w^(64 a1 K), a1 = a1l + 4 a1h, K = b0 + 64 b1 = (j mod 256) + 256 d
+    const uint64_t* t2 = a.twpass + ((uint64_t)(a1l + 4 * a1h) << 12) + (j & 255);
+#pragma unroll
+    for (int d = 0; d < 16; ++d) tw[d] = t2[256 * d];
+  }
+  switch (__builtin_amdgcn_readfirstlane(c)) {  // w_64^(a2l c)
+    case 1: gl_stage_b_twiddle<E64, 1>(v); break;
+    case 2: gl_stage_b_twiddle<E64, 2>(v); break;
+    case 3: gl_stage_b_twiddle<E64, 3>(v); break;
+    default: break;
+  }
+  dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output d at v[bitrev4(d)]
+#pragma unroll
+  for (int d = 0; d < 16; ++d) lds[d * PD + a1h * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
+  __syncthreads();
+  const int d2 = t / W;
+#pragma unroll
+  for (int h = 0; h < 16; ++h) v[h] = lds[d2 * PD + h * W + w];
+  dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output e at v[bitrev4(e)]
+  switch (__builtin_amdgcn_readfirstlane(a1l)) {  // w_64^(a1l e)
+    case 1: gl_post_twiddle_br<E64, 1>(v); break;
+    case 2: gl_post_twiddle_br<E64, 2>(v); break;
+    case 3: gl_post_twiddle_br<E64, 3>(v); break;
+    default: break;
+  }
+  // output digit k = d + 16 e of the Stockham pass (Ns = 256)
+  uint64_t* out = a.out + (uint64_t)poly * a.out_pitch;
+  const uint64_t base = ((j >> 8) << 16) + (j & 255);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) out[base + ((uint64_t)(d2 + 16 * e) << 8)] = v[bitrev_c(e, 4)];
 }
 
 // Persistent, software-pipelined (PBF_NTT_PERSIST): each workgroup walks tiles blockIdx.x,

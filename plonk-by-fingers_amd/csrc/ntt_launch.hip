@@ -322,6 +322,33 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
       p->tc.push_back(b);
     }
   }
+  // regrouped 2^24 plan (default for 8,8,8 standard-root plans; PBF_NTT_NO_RG=1 restores the
+  // round-2 passes): three twiddle layers of order 4096, 2^18 and 2^24
+  if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && !getenv("PBF_NTT_NO_RG")) {
+    const uint64_t w4096 = hpow(w, n / 4096, m);
+    std::vector<uint64_t> tc1(4096);
+    for (uint64_t a2l = 0; a2l < 16; ++a2l)
+      for (uint64_t r2 = 0; r2 < 4; ++r2)
+        for (uint64_t k1 = 0; k1 < 64; ++k1)
+          tc1[a2l * 256 + r2 * 64 + k1] = hpow(w4096, ((a2l + 16 * r2) * k1) % 4096, m);
+    std::vector<uint64_t> t2(1ull << 18);
+    for (uint64_t a1 = 0; a1 < 64; ++a1) {
+      const uint64_t st = hpow(w, 64 * a1, m);
+      uint64_t y = 1;
+      for (uint64_t K = 0; K < 4096; ++K) { t2[(a1 << 12) + K] = y; y = hmul(y, st, m); }
+    }
+    std::vector<uint64_t> t3(1ull << 24);
+    const uint64_t scale = inverse ? p->n_inv : 1;
+    for (uint64_t fq = 0; fq < 4; ++fq)
+      for (uint64_t a0 = 0; a0 < 64; ++a0) {
+        const uint64_t st = hpow(w, a0, m);
+        uint64_t y = hmul(hpow(w, (65536 * a0 * fq) % n, m), scale, m);
+        uint64_t* row = t3.data() + ((fq * 64 + a0) << 16);
+        for (uint64_t j = 0; j < 65536; ++j) { row[j] = y; y = hmul(y, st, m); }
+      }
+    if ((rc = upload(p->rg_tc1, tc1)) || (rc = upload(p->rg_t2, t2)) || (rc = upload(p->rg_t3, t3))) return rc;
+    p->rg = true;
+  }
   // round-3 in-place schedule: opt-in (PBF_NTT_IP=1) while it measures slower than the
   // round-2 Stockham plan
   if (p->gl && getenv("PBF_NTT_IP") && !getenv("PBF_NTT_V2")) {
@@ -568,6 +595,14 @@ static GlPassFn gl_fn_blk(int logr, bool first) {
 #undef PBF_GL_B
 }
 
+// the regrouped 2^24 plan's three pass kernels
+template <int E>
+static GlPassFn gl_fn_rg(int pass) {
+  if (pass == 0) return ntt_gl_pass_kernel<8, E, true, 4096, false, 1>;
+  if (pass == 1) return ntt_gl_rg2_kernel<E>;
+  return ntt_gl_pass_kernel<8, E, false, 4096, false, 3>;
+}
+
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
@@ -666,6 +701,8 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
       while ((1ull << blk_log) < w1) ++blk_log;
     }
   }
+  const bool rg = p.rg && P == 3 && split_log == 0 && !blk && gl_pad(p) == 0 && !getenv("PBF_NTT_PERSIST") &&
+                  gl_tile(8) == 4096;
   uint32_t log_ns = 0;
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
@@ -674,6 +711,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     GlPassFn fn =
         p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile, persist) : gl_fn_e<153>(lr, log_ns == 0, tile, persist);
     if (blk) fn = p.e64 == 39 ? gl_fn_blk<39>(lr, log_ns == 0) : gl_fn_blk<153>(lr, log_ns == 0);
+    if (rg) fn = p.e64 == 39 ? gl_fn_rg<39>((int)i) : gl_fn_rg<153>((int)i);
     if (!fn) return fail(1, "no Goldilocks pass kernel for this radix");
     const uint64_t W = (uint64_t)tile >> lr;
     if ((p.n >> lr) % W) return fail(1, "transform too small for the pass tile");
@@ -705,6 +743,9 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (tiles > 0x7fffffffull) return fail(1, "batch too large");
     a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
     a.blk_log = blk_log;
+    if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
+    if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
+    if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;

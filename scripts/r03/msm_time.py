@@ -39,4 +39,12 @@ print("windowed device Horner", _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr()
       "same result", r0 == r1)
 del os.environ["PBF_MSM_DEVICE_HORNER"]
 ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp)
-print("fixed-base", _median_ms(lambda: ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp), reps=11))
+rf = ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp)
+print("fixed-base", _median_ms(lambda: ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp), reps=11),
+      "same result", rf == r0)
+os.environ["PBF_MSM_QUAD"] = "0"
+print("windowed single-lane tail", _median_ms(lambda: ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp), reps=11),
+      "same result", ctx.msm_g1_dev(pts.data_ptr(), s.data_ptr(), m, stream=sp) == r0)
+print("fixed-base single-lane tail", _median_ms(lambda: ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp), reps=11),
+      "same result", ctx.msm_g1_fixed_dev(pts.data_ptr(), m, s.data_ptr(), m, stream=sp) == r0)
+del os.environ["PBF_MSM_QUAD"]

@@ -137,6 +137,35 @@ def test_alternative_pass_plans_2p24(passes, monkeypatch, vectors):
     c2.close()
 
 
+@pytest.mark.parametrize("inverse", [False, True])
+def test_regrouped_2p24_matches_stockham(monkeypatch, inverse):
+    """The regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel: general twiddles only between
+    64-point blocks, the default for 8,8,8) against the round-2 passes (PBF_NTT_NO_RG=1), batch
+    of 2 (XCD k-major tiles sharing the 2^24-entry table), forward and inverse, bit-exact, and
+    polynomial 0 against the oracle's iterative transform."""
+    import torch
+
+    n, batch = 1 << 24, 2
+    w = root(GOLD, n)
+    host = np.stack([oracle.splitmix_field(GOLD, 900 + i, n) for i in range(batch)])
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for env in ({}, {"PBF_NTT_NO_RG": "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = pbf.Context(0)
+        d_in = torch.from_numpy(host.view(np.int64)).cuda()
+        d_out = torch.empty_like(d_in)
+        c.ntt_batch_dev(GOLD, w, d_in.data_ptr(), d_out.data_ptr(), n, batch, inverse=inverse, stream=stream)
+        torch.cuda.synchronize()
+        outs.append(d_out.cpu().numpy().view(np.uint64).copy())
+        c.close()
+        for k in env:
+            monkeypatch.delenv(k)
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0][0], oracle.ntt_gl_par(w, host[0], inverse=inverse))
+
+
 def test_batch_dev_matches_single(ctx):
     import torch
 
