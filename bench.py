@@ -154,13 +154,15 @@ def cpu_baselines_bn254() -> dict:
     return out
 
 
-def live_traffic(log_n: int, batch: int, steps: int = 6) -> dict | None:
+def live_traffic(log_n: int, batch: int, steps: int = 6, fetch_scale: float = 1.0) -> dict | None:
     """HBM bytes per step of the NTT bench workload, measured now: two rocprofv3 PMC passes
     (FETCH_SIZE, WRITE_SIZE: separate runs, MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots")
     over a child bench.py that runs only the NTT steps. Counters are KiB; the NTT kernels load
-    8 B per lane in 64-B runs, which FETCH_SIZE counts exactly on gfx950 (calibrated against
-    scripts/ubench/tile_copy moving a known byte count in the same pattern), so
-    no 2x wide-load correction applies. None if rocprofv3 is unavailable or a pass fails."""
+    8 B per lane in W-element runs. Calibrated on scripts/ubench/tile_copy moving a known byte
+    count in the same patterns (profiles/r03/fetch_cal.txt): FETCH_SIZE counts 64-B runs (the
+    2^20 plan, W = 8) exactly and 128-B runs (the 2^24 plan, W = 16) at half, so `fetch_scale`
+    (2 for the 2^24 plan) restores bytes; WRITE_SIZE is exact for both. None if rocprofv3 is
+    unavailable or a pass fails."""
     import csv
     import shutil
     import signal
@@ -193,7 +195,9 @@ def live_traffic(log_n: int, batch: int, steps: int = 6) -> dict | None:
                 total += float(r["Counter_Value"])
         out[counter] = total * 1024.0 / steps  # bytes per step (the child runs `steps` steps, no warm-up)
     shutil.rmtree(tmp, ignore_errors=True)
-    return {"hbm_bytes_per_step": out["FETCH_SIZE"] + out["WRITE_SIZE"], "fetch_bytes_per_step": out["FETCH_SIZE"],
+    fetch = out["FETCH_SIZE"] * fetch_scale
+    return {"hbm_bytes_per_step": fetch + out["WRITE_SIZE"], "fetch_bytes_per_step": fetch,
+            "fetch_counter_bytes_per_step": out["FETCH_SIZE"], "fetch_scale": fetch_scale,
             "write_bytes_per_step": out["WRITE_SIZE"], "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
             "separate passes over this bench's NTT steps, run by bench.py"}
 
@@ -338,14 +342,17 @@ def main() -> int:
                 out["roofline"]["traffic"] = tr["hbm_bytes_per_step"]
                 out["roofline"]["traffic_detail"] = dict(tr, algorithmic_bytes_per_step=alg_bytes_step)
             if "extra" in out and "ntt_2p24" in out["extra"]:
-                tr24 = live_traffic(24, 2)
+                tr24 = live_traffic(24, 2, fetch_scale=2.0)
                 if tr24:
                     r24 = out["extra"]["ntt_2p24"]["roofline"]
                     r24["traffic"] = tr24["hbm_bytes_per_step"]
                     r24["traffic_detail"] = dict(tr24, algorithmic_bytes_per_step=16.0 * (1 << 24) * 2,
-                                                 calibration="FETCH_SIZE calibrated for 64-B runs (2^20 plan); "
-                                                             "the 2^24 plan reads 128-B runs, which may be "
-                                                             "tallied at half (MI355X_MICROARCH.md, HBM)")
+                                                 calibration="tile_copy (profiles/r03/fetch_cal.txt): FETCH_SIZE "
+                                                             "= 1.00x bytes for 64-B runs, 0.50x for 128-B runs; "
+                                                             "every pass of the 2^24 plan reads 128-B runs "
+                                                             "(W = 16), so the counter is doubled; 3 passes of "
+                                                             "read + write plus the last pass's 128 MiB twiddle "
+                                                             "table = 3.3x algorithmic by construction")
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(args.log_n, args.cpu_budget)
             if "extra" in out:

@@ -132,8 +132,18 @@ struct GlShape {
   static constexpr int W = TILE / R;
   static constexpr int NT = TILE / 16;             // 16 elements per thread
   static constexpr int WPQ = NT / 256;              // waves per stage-B q1 value
-  static constexpr int YP = 65 * W;                 // Y row pitch (elements)
+  // Y rows r2: padded by W (YP = 65 W) so that the four r2 rows of one stage-B write
+  // instruction fall on both halves of the banks; for W = 16 the same spread comes from
+  // XOR-ing k1's low bit with r2's (YX: no padding, a 4096-element tile is exactly 32 KiB and
+  // five workgroups fit a CU; PBF_GL_PAD_Y builds the padded layout for A/B)
+#ifdef PBF_GL_PAD_Y
+  static constexpr bool YX = false;
+#else
+  static constexpr bool YX = W == 16 && C > 1;
+#endif
+  static constexpr int YP = (YX ? 64 : 65) * W;     // Y row pitch (elements)
   static constexpr int LDS = (C * YP > TILE) ? C * YP : TILE;
+  static constexpr bool LDS32K = LDS * 8 <= 32768;  // five workgroups per CU by LDS
   static constexpr int NSUB_C = (64 * W) / NT;      // stage-C sub-DFTs per thread
   // Y column swizzle: the first pass's stage C reads all 64 k1 of one column w per wave
   // (so its stores are 512-B runs of out[j*R + k]); w ^ ysw(k1) spreads those reads over
@@ -141,6 +151,10 @@ struct GlShape {
   // writes and later passes' reads stay permutations within a row (conflict-free).
   __host__ __device__ static constexpr int ysw(int k1) {
     return W <= 32 ? (k1 / (32 / W)) & (W - 1) : (k1 & 31);
+  }
+  // Y element (r2, k1, w)
+  __host__ __device__ static constexpr int yidx(int r2, int k1, int w) {
+    return r2 * YP + (YX ? (k1 ^ (r2 & 1)) : k1) * W + (w ^ ysw(k1));
   }
 };
 
@@ -332,7 +346,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int q2 = 0; q2 < 16; ++q2) {
       const int k1 = q1 + 4 * q2;
-      lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))] = v[bitrev_c(q2, 4)];
+      lds[Sh::yidx(r2, k1, w)] = v[bitrev_c(q2, 4)];
     }
   }
   gl_bar<PERSIST>();
@@ -359,7 +373,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     int k1, w;
     c_map(u, &k1, &w);
 #pragma unroll
-    for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
+    for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[Sh::yidx(r2, k1, w)];
   }
   if constexpr (RG == 3) {
     // w_64^(r2 g), g = k1 >> 2 = wave + 4 u (4-wave tiles, W = 16): wave-uniform shifts
@@ -515,7 +529,10 @@ __device__ __forceinline__ void gl_shape_checks() {
 
 // One tile per workgroup.
 template <int LOGR, int E64, bool FIRST, int TILE, bool BLK = false, int RG = 0>
-__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+// waves per SIMD the VGPR budget allows: 5 where the LDS allows five workgroups and the
+// kernel fits 96 VGPRs without spilling (first passes and the regrouped plan's), else 4
+__global__ void __launch_bounds__(TILE / 16)
+__attribute__((amdgpu_waves_per_eu((FIRST || RG) && !BLK && GlShape<LOGR, TILE>::LDS32K ? 5 : 4)))
 ntt_gl_pass_kernel(GlPassArgs a) {
   gl_shape_checks<LOGR, TILE>();
   __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
@@ -538,12 +555,17 @@ ntt_gl_pass_kernel(GlPassArgs a) {
 // layout of the other passes (natural order in and out).
 // Pass 2 tile: 256 rows r = 16 a2l + a1h x W = 16 columns j (Ns = 256: j mod 256 = b0 + 64 c,
 // the first pass's output digit; bits 14..15 of j = a1l); stage X thread (a1h, w), stage Y
-// thread (d, w); LDS [d][a1h][w] with rows padded by 8 elements (the stage-Y reads of four d
-// per wave then hit every bank exactly twice).
+// thread (d, w); LDS [d][a1h ^ (d mod 4)][w] (the XOR spreads the stage-Y reads of four d per
+// wave over both halves of the banks: every bank pair is hit exactly twice, the minimum).
+#ifndef PBF_RG2_WPE
+#define PBF_RG2_WPE 4
+#endif
 template <int E64>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ntt_gl_rg2_kernel(GlPassArgs a) {
-  constexpr int W = 16, PD = 16 * W + 8;
-  __shared__ __attribute__((aligned(16))) uint64_t lds[16 * PD];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_RG2_WPE))) ntt_gl_rg2_kernel(GlPassArgs a) {
+  constexpr int W = 16;
+  // 32 KiB; four waves per SIMD (PBF_RG2_WPE): at five the 96-VGPR budget spills 28 B per
+  // lane and the pass runs ~2 % slower (profiles/r03/ntt_lds_ab.log)
+  __shared__ __attribute__((aligned(16))) uint64_t lds[16 * 16 * W];
   const FieldArgs f{};
   using G = Goldilocks;
   const uint32_t tiles = a.blocks_per_poly * a.batch;
@@ -571,11 +593,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) n
   }
   dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output d at v[bitrev4(d)]
 #pragma unroll
-  for (int d = 0; d < 16; ++d) lds[d * PD + a1h * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
+  for (int d = 0; d < 16; ++d) lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
   __syncthreads();
   const int d2 = t / W;
 #pragma unroll
-  for (int h = 0; h < 16; ++h) v[h] = lds[d2 * PD + h * W + w];
+  for (int h = 0; h < 16; ++h) v[h] = lds[d2 * 256 + (h ^ (d2 & 3)) * W + w];
   dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output e at v[bitrev4(e)]
   switch (__builtin_amdgcn_readfirstlane(a1l)) {  // w_64^(a1l e)
     case 1: gl_post_twiddle_br<E64, 1>(v); break;

@@ -226,7 +226,7 @@ __device__ __forceinline__ void ip_tile_bc(const IpArgs& a, uint64_t* lds, const
 #pragma unroll
     for (int q2 = 0; q2 < 16; ++q2) {
       const int k1 = q1 + 4 * q2;
-      lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))] = v[bitrev_c(q2, 4)];
+      lds[Sh::yidx(r2, k1, w)] = v[bitrev_c(q2, 4)];
     }
   }
   ip_bar();
@@ -237,7 +237,7 @@ __device__ __forceinline__ void ip_tile_bc(const IpArgs& a, uint64_t* lds, const
     const int idx = t + NT * u;
     const int k1 = idx / W, w = idx % W;
 #pragma unroll
-    for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[r2 * YP + k1 * W + (w ^ Sh::ysw(k1))];
+    for (int r2 = 0; r2 < C; ++r2) x[u * C + r2] = lds[Sh::yidx(r2, k1, w)];
 #pragma unroll
     for (int r2 = 1; r2 < C; ++r2) x[u * C + r2] = G::mul(x[u * C + r2], tcl[r2 * 64 + k1], f);
   }
