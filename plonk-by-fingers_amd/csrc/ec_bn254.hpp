@@ -96,6 +96,29 @@ struct G1 {
     r.ZZZ = F::mul(p.ZZZ, PPP);
     return r;
   }
+  // madd-2008-s with the single-chain product (Fq::mul_tp, identical results): the MSM
+  // accumulation, which is VALU-issue-bound at four waves per SIMD
+  __host__ __device__ __forceinline__ static U256 mul_tp(const U256& a, const U256& b) { return F::mul_tp(a, b); }
+  __host__ __device__ __forceinline__ static Xyzz madd_tp(const Xyzz& p, const Affine& a) {
+    if (is_identity(p)) return from_affine(a);
+    const U256 U2 = mul_tp(a.x, p.ZZ);
+    const U256 S2 = mul_tp(a.y, p.ZZZ);
+    const U256 P = F::sub(U2, p.X);
+    const U256 R = F::sub(S2, p.Y);
+    if (F::is_zero(P)) {
+      if (F::is_zero(R)) return mdbl(a);
+      return identity();
+    }
+    const U256 PP = mul_tp(P, P);
+    const U256 PPP = mul_tp(P, PP);
+    const U256 Q = mul_tp(p.X, PP);
+    Xyzz r;
+    r.X = F::sub(F::sub(mul_tp(R, R), PPP), dbl_f(Q));
+    r.Y = F::sub(mul_tp(R, F::sub(Q, r.X)), mul_tp(p.Y, PPP));
+    r.ZZ = mul_tp(p.ZZ, PP);
+    r.ZZZ = mul_tp(p.ZZZ, PPP);
+    return r;
+  }
   // add-2008-s: p + q
   __host__ __device__ __forceinline__ static Xyzz add(const Xyzz& p, const Xyzz& q) {
     if (is_identity(p)) return q;

@@ -157,7 +157,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
       acc = G1::identity();
     }
     if (v & MSM_NEG) p.y = Fq::sub(u256_zero(), p.y);
-    acc = G1::madd(acc, p);
+#ifdef PBF_MSM_MUL2CH
+    acc = G1::madd(acc, p);  // A/B build: the two-chain product
+#else
+    acc = G1::madd_tp(acc, p);
+#endif
   }
   flush(c1);
 }
