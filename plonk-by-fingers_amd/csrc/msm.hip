@@ -384,6 +384,9 @@ __global__ void __launch_bounds__(256) msm_fx_cd(const Xyzz* buckets, const Chun
 // each, then (256 / SEQ)-lane trees); the other 128 / SEQ workgroups: D_l for 2 SEQ values
 // of l each (128 / SEQ threads per l, SEQ values of h each, then (128 / SEQ)-lane trees).
 // SEQ trades depth (SEQ + log2(lanes) additions) against waves in flight (PBF_MSM_CD_SEQ).
+// (Round 3: single-chain products in the sequential part measured no faster, 3.25-3.28 vs
+// 3.25 ms per windowed MSM, profiles/r03/msm_addtp_ab.log: two to four waves per SIMD leave
+// the interleaved products' latency hiding the better trade here.)
 template <int SEQ>
 __global__ void __launch_bounds__(256) msm_fx_cd_seq(const Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
                                                      const uint32_t* start, const uint32_t* end, Xyzz* cd) {

@@ -96,13 +96,13 @@ __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_str
     return;
   }
   U256 x = fr_pow(base, e_off + e_mult * i0);
-  if (has_c0) x = Fr::mul(x, c0);
+  if (has_c0) x = Fr::mul_tp(x, c0);
   const U256 step = fr_pow(base, 64 * e_mult);
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     const uint64_t j = in_off + in_stride * i;
-    if (j < len) u256_to_u64(Fr::mul(u256_from_u64(in + 4 * j), x), out + 4 * i);
+    if (j < len) u256_to_u64(Fr::mul_tp(u256_from_u64(in + 4 * j), x), out + 4 * i);
     else for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
-    x = Fr::mul(x, step);
+    x = Fr::mul_tp(x, step);
   }
 }
 
@@ -119,8 +119,8 @@ __device__ __forceinline__ uint64_t blk_index(const Blk& b, uint64_t p) {
 // block, recompute it where p + 64 starts a new block
 __device__ __forceinline__ U256 blk_next_x(const Blk& b, uint64_t p, const U256& x, const U256& step, const U256& g,
                                            const U256& w) {
-  if (b.G == 1 || (p + 64) / b.S == p / b.S) return Fr::mul(x, step);
-  return Fr::mul(g, fr_pow(w, blk_index(b, p + 64)));
+  if (b.G == 1 || (p + 64) / b.S == p / b.S) return Fr::mul_tp(x, step);
+  return Fr::mul_tp(g, fr_pow(w, blk_index(b, p + 64)));
 }
 
 // out[g + G m] = in[g][m] (the all-gathered stride shards of one vector, back in order)
@@ -136,11 +136,11 @@ __global__ void k_powers(uint64_t* out, uint64_t count, U256 base, U256 start) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
-  U256 x = Fr::mul(start, fr_pow(base, i0));
+  U256 x = Fr::mul_tp(start, fr_pow(base, i0));
   const U256 step = pow64(base);
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     str(out + 4 * i, x);
-    x = Fr::mul(x, step);
+    x = Fr::mul_tp(x, step);
   }
 }
 
@@ -156,8 +156,8 @@ __global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n
     return;
   }
   U256 h = u256_from_u64(hpow + 4 * (idx - 1));  // canonical; k1, k2 Montgomery: products canonical
-  if (kind == 1) h = Fr::mul(h, k1);
-  if (kind == 2) h = Fr::mul(h, k2);
+  if (kind == 1) h = Fr::mul_tp(h, k1);
+  if (kind == 2) h = Fr::mul_tp(h, k2);
   u256_to_u64(h, sigma + 4 * id);
 }
 
@@ -171,9 +171,9 @@ __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64
   const U256 ql = ld(q + 4 * i), qo = ld(q + 4 * (2 * n + i)), qm = Fr::to_mont(ld(q + 4 * (3 * n + i))),
              qc = Fr::from_mont(ld(q + 4 * (4 * n + i)));
   const U256 a = ld(abc + 4 * i), b = ld(abc + 4 * (n + i)), c = ld(abc + 4 * (2 * n + i));
-  U256 r = Fr::add(Fr::mul(ql, a), Fr::mul(ql, b));
-  r = Fr::add(r, Fr::mul(qo, c));
-  r = Fr::add(r, Fr::mul(Fr::mul(qm, a), b));
+  U256 r = Fr::add(Fr::mul_tp(ql, a), Fr::mul_tp(ql, b));
+  r = Fr::add(r, Fr::mul_tp(qo, c));
+  r = Fr::add(r, Fr::mul_tp(Fr::mul_tp(qm, a), b));
   r = Fr::add(r, qc);
   if (!Fr::is_zero(r)) *bad = 1;
   for (int col = 0; col < 3; ++col) {
@@ -196,15 +196,15 @@ __global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const u
   auto ld = [](const uint64_t* p) { return u256_from_u64(p); };
   const U256 a = ld(abc + 4 * j), b = ld(abc + 4 * (n + j)), c = ld(abc + 4 * (2 * n + j));
   const U256 w = ld(hpow + 4 * j);
-  const U256 bw = Fr::mul(beta, w);
+  const U256 bw = Fr::mul_tp(beta, w);
   U256 d1 = Fr::add(Fr::add(a, bw), gamma0);
-  U256 d2 = Fr::add(Fr::add(b, Fr::mul(bw, k1)), gamma0);
-  U256 d3 = Fr::add(Fr::add(c, Fr::mul(bw, k2)), gamma0);
-  u256_to_u64(Fr::mul(Fr::mul(d1, d2), d3), num + 4 * j);
-  U256 e1 = Fr::add(Fr::add(a, Fr::mul(beta, ld(sigma + 4 * j))), gamma0);
-  U256 e2 = Fr::add(Fr::add(b, Fr::mul(beta, ld(sigma + 4 * (n + j)))), gamma0);
-  U256 e3 = Fr::add(Fr::add(c, Fr::mul(beta, ld(sigma + 4 * (2 * n + j)))), gamma0);
-  u256_to_u64(Fr::mul(Fr::mul(e1, e2), e3), den + 4 * j);
+  U256 d2 = Fr::add(Fr::add(b, Fr::mul_tp(bw, k1)), gamma0);
+  U256 d3 = Fr::add(Fr::add(c, Fr::mul_tp(bw, k2)), gamma0);
+  u256_to_u64(Fr::mul_tp(Fr::mul_tp(d1, d2), d3), num + 4 * j);
+  U256 e1 = Fr::add(Fr::add(a, Fr::mul_tp(beta, ld(sigma + 4 * j))), gamma0);
+  U256 e2 = Fr::add(Fr::add(b, Fr::mul_tp(beta, ld(sigma + 4 * (n + j)))), gamma0);
+  U256 e3 = Fr::add(Fr::add(c, Fr::mul_tp(beta, ld(sigma + 4 * (2 * n + j)))), gamma0);
+  u256_to_u64(Fr::mul_tp(Fr::mul_tp(e1, e2), e3), den + 4 * j);
 }
 
 // out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
@@ -227,14 +227,14 @@ __global__ void __launch_bounds__(256) k_div_batch(const uint64_t* num, const ui
     const U256 d = u256_from_u64(den + 4 * (i0 + k));
     if (Fr::is_zero(d)) { *bad = 1; return; }
     pre[k] = acc;
-    acc = Fr::mul(acc, d);
+    acc = Fr::mul_tp(acc, d);
   }
   U256 inv = fr_inv(acc);  // 1 / prod
   for (int k = m - 1; k >= 0; --k) {
     const U256 d = u256_from_u64(den + 4 * (i0 + k));
-    const U256 dinv = Fr::mul(inv, pre[k]);  // 1 / d_k
-    inv = Fr::mul(inv, d);
-    str(out + 4 * (i0 + k), num ? Fr::mul(u256_from_u64(num + 4 * (i0 + k)), dinv) : dinv);
+    const U256 dinv = Fr::mul_tp(inv, pre[k]);  // 1 / d_k
+    inv = Fr::mul_tp(inv, d);
+    str(out + 4 * (i0 + k), num ? Fr::mul_tp(u256_from_u64(num + 4 * (i0 + k)), dinv) : dinv);
   }
 }
 
@@ -244,7 +244,7 @@ constexpr int SCAN_T = 256, SCAN_PER = 8, SCAN_BLK = SCAN_T * SCAN_PER;
 __device__ void block_scan_mul(U256* sh, int t) {  // inclusive Hillis-Steele over SCAN_T
   for (int off = 1; off < SCAN_T; off <<= 1) {
     U256 v = sh[t];
-    if (t >= off) v = Fr::mul(sh[t - off], v);
+    if (t >= off) v = Fr::mul_tp(sh[t - off], v);
     __syncthreads();
     sh[t] = v;
     __syncthreads();
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan1(const uint64_t* in, uint64_t* 
   for (int k = 0; k < SCAN_PER; ++k) {
     const uint64_t i = base + k;
     const U256 x = i < count ? ldr(in + 4 * i) : fr_one_m();
-    acc = Fr::mul(acc, x);
+    acc = Fr::mul_tp(acc, x);
     v[k] = acc;
   }
   sh[t] = acc;
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan1(const uint64_t* in, uint64_t* 
   const U256 pre = t ? sh[t - 1] : fr_one_m();
   for (int k = 0; k < SCAN_PER; ++k) {
     const uint64_t i = base + k;
-    if (i < count) str(out + 4 * i, Fr::mul(pre, v[k]));
+    if (i < count) str(out + 4 * i, Fr::mul_tp(pre, v[k]));
   }
   if (t == SCAN_T - 1) str(totals + 4 * blockIdx.x, sh[t]);
 }
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan2(uint64_t* totals, uint64_t nb)
   const uint64_t b0 = (uint64_t)t * per;
   U256 acc = fr_one_m();
   for (uint64_t k = 0; k < per; ++k)
-    if (b0 + k < nb) acc = Fr::mul(acc, ldr(totals + 4 * (b0 + k)));
+    if (b0 + k < nb) acc = Fr::mul_tp(acc, ldr(totals + 4 * (b0 + k)));
   sh[t] = acc;
   __syncthreads();
   block_scan_mul(sh, t);
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan2(uint64_t* totals, uint64_t nb)
     if (b0 + k >= nb) break;
     const U256 x = ldr(totals + 4 * (b0 + k));
     str(totals + 4 * (b0 + k), run);
-    run = Fr::mul(run, x);
+    run = Fr::mul_tp(run, x);
   }
 }
 
@@ -304,7 +304,7 @@ __global__ void k_scan3(const uint64_t* incl, uint64_t* out, uint64_t count, con
   if (i == 0) { str(out, fr_one_m()); return; }
   const uint64_t j = i - 1;
   const uint64_t blk = j / SCAN_BLK;
-  str(out + 4 * i, Fr::mul(ldr(totals + 4 * blk), ldr(incl + 4 * j)));
+  str(out + 4 * i, Fr::mul_tp(ldr(totals + 4 * blk), ldr(incl + 4 * j)));
 }
 
 // coeff[idx] += delta (blinding: (b_lo + b_hi x [+ b x^2]) * (x^n - 1), plonk.rs:250-252, 304)
@@ -332,14 +332,14 @@ __global__ void k_lincomb(LinComb L, uint64_t* out, uint64_t count) {
   // conversion-free: canonical inputs times Montgomery-form constants are canonical products
   U256 acc = i == 0 ? Fr::from_mont(L.c0) : u256_zero();
   for (int k = 0; k < L.k; ++k)
-    if (i < L.len[k]) acc = Fr::add(acc, Fr::mul(L.c[k], u256_from_u64(L.in[k] + 4 * i)));
+    if (i < L.len[k]) acc = Fr::add(acc, Fr::mul_tp(L.c[k], u256_from_u64(L.in[k] + 4 * i)));
   u256_to_u64(acc, out + 4 * i);
 }
 
 // out = a b for canonical a and b held at R-degree 1 (b R: mont(a, b R) = a b, canonical)
 __global__ void k_mul(const uint64_t* a, const uint64_t* b, uint64_t* out, uint64_t count) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) u256_to_u64(Fr::mul(u256_from_u64(a + 4 * i), u256_from_u64(b + 4 * i)), out + 4 * i);
+  if (i < count) u256_to_u64(Fr::mul_tp(u256_from_u64(a + 4 * i), u256_from_u64(b + 4 * i)), out + 4 * i);
 }
 
 // t(x_i) for x_i = g w_N^i on the coset (N = 4n): the numerator of plonk.rs:358-368
@@ -368,7 +368,7 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uin
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = (t / 64) * 64 * ch + (t % 64);
   if (i0 >= q.N) return;
-  U256 x = Fr::mul(q.g, fr_pow(q.wN, blk_index(q.blk, i0)));
+  U256 x = Fr::mul_tp(q.g, fr_pow(q.wN, blk_index(q.blk, i0)));
   const U256 step = pow64(q.wN);
   for (uint64_t p = i0, k = 0; k < ch && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
     const uint64_t o = 4 * p;
@@ -377,27 +377,27 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uin
     const U256 a = ld(q.a + o), b = ld(q.b + o), c = ld(q.c + o), z = ld(q.z + o);
     const U256 zw = q.zw ? ld(q.zw + o) : ld(q.z + 4 * ((i + 4) % q.N_all));  // z(w x_i): w = w_N^4
     // t1: a b q_m + a q_l + b q_r + c q_o + q_c                   (degrees -1+2, 0+1, 0)
-    U256 t1 = Fr::mul(Fr::mul(a, b), ld(q.qm + o));
-    t1 = Fr::add(t1, Fr::mul(a, ld(q.ql + o)));
-    t1 = Fr::add(t1, Fr::mul(b, ld(q.qr + o)));
-    t1 = Fr::add(t1, Fr::mul(c, ld(q.qo + o)));
+    U256 t1 = Fr::mul_tp(Fr::mul_tp(a, b), ld(q.qm + o));
+    t1 = Fr::add(t1, Fr::mul_tp(a, ld(q.ql + o)));
+    t1 = Fr::add(t1, Fr::mul_tp(b, ld(q.qr + o)));
+    t1 = Fr::add(t1, Fr::mul_tp(c, ld(q.qo + o)));
     t1 = Fr::add(t1, ld(q.qc + o));
     // t2 - t3 = (a + beta x + gamma)(b + beta k1 x + gamma)(c + beta k2 x + gamma) z
     //         - (a + beta s1 + gamma)(b + beta s2 + gamma)(c + beta s3 + gamma) z(w x)   (degree -3),
     // times alpha once (alpha at degree 4)
-    const U256 bx = Fr::mul(q.beta0, x);  // x at degree 1
-    U256 t2 = Fr::mul(Fr::add(Fr::add(a, bx), q.gamma0), Fr::add(Fr::add(b, Fr::mul(bx, q.k1)), q.gamma0));
-    t2 = Fr::mul(t2, Fr::add(Fr::add(c, Fr::mul(bx, q.k2)), q.gamma0));
-    t2 = Fr::mul(t2, z);
-    U256 t3 = Fr::mul(Fr::add(Fr::add(a, Fr::mul(q.beta0, ld(q.s1 + o))), q.gamma0),
-                      Fr::add(Fr::add(b, Fr::mul(q.beta0, ld(q.s2 + o))), q.gamma0));
-    t3 = Fr::mul(t3, Fr::add(Fr::add(c, Fr::mul(q.beta0, ld(q.s3 + o))), q.gamma0));
-    t3 = Fr::mul(t3, zw);
-    const U256 t23 = Fr::mul(Fr::sub(t2, t3), q.alpha4);
+    const U256 bx = Fr::mul_tp(q.beta0, x);  // x at degree 1
+    U256 t2 = Fr::mul_tp(Fr::add(Fr::add(a, bx), q.gamma0), Fr::add(Fr::add(b, Fr::mul_tp(bx, q.k1)), q.gamma0));
+    t2 = Fr::mul_tp(t2, Fr::add(Fr::add(c, Fr::mul_tp(bx, q.k2)), q.gamma0));
+    t2 = Fr::mul_tp(t2, z);
+    U256 t3 = Fr::mul_tp(Fr::add(Fr::add(a, Fr::mul_tp(q.beta0, ld(q.s1 + o))), q.gamma0),
+                      Fr::add(Fr::add(b, Fr::mul_tp(q.beta0, ld(q.s2 + o))), q.gamma0));
+    t3 = Fr::mul_tp(t3, Fr::add(Fr::add(c, Fr::mul_tp(q.beta0, ld(q.s3 + o))), q.gamma0));
+    t3 = Fr::mul_tp(t3, zw);
+    const U256 t23 = Fr::mul_tp(Fr::sub(t2, t3), q.alpha4);
     // t4: alpha^2 (z - 1) L1                                        (0+1-1, then +1-1)
-    const U256 t4 = Fr::mul(Fr::mul(Fr::sub(z, Fr::one_plain()), ld(q.l1 + o)), q.alpha2);
+    const U256 t4 = Fr::mul_tp(Fr::mul_tp(Fr::sub(z, Fr::one_plain()), ld(q.l1 + o)), q.alpha2);
     const U256 num = Fr::add(Fr::add(t1, t23), t4);
-    u256_to_u64(Fr::mul(num, q.zh_inv[i & 3]), out + o);
+    u256_to_u64(Fr::mul_tp(num, q.zh_inv[i & 3]), out + o);
   }
 }
 
@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* t
       u = u256_from_u64(a.p + 4 * (a.L - 1 - k));
       if (k == a.L - 1) u = Fr::sub(u, a.y);
     }
-    acc = Fr::add(u, Fr::mul(a.z, acc));
+    acc = Fr::add(u, Fr::mul_tp(a.z, acc));
     v[m] = acc;
   }
   sh[t] = acc;
@@ -446,7 +446,7 @@ __global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* t
   for (int j = 0; j < HS_LOG_T; ++j) {
     const int off = 1 << j;
     U256 x = sh[t];
-    if (t >= off) x = Fr::add(x, Fr::mul(a.zs[j], sh[t - off]));
+    if (t >= off) x = Fr::add(x, Fr::mul_tp(a.zs[j], sh[t - off]));
     __syncthreads();
     sh[t] = x;
     __syncthreads();
@@ -456,8 +456,8 @@ __global__ void __launch_bounds__(HS_T) k_hs1(HsArgs a, uint64_t* q, uint64_t* t
 #pragma unroll
   for (int m = 0; m < HS_PER; ++m) {
     const uint64_t k = k0 + m;
-    const U256 sk = Fr::add(v[m], Fr::mul(zk, carry));
-    zk = Fr::mul(zk, a.z);
+    const U256 sk = Fr::add(v[m], Fr::mul_tp(zk, carry));
+    zk = Fr::mul_tp(zk, a.z);
     if (k + 1 < a.L) u256_to_u64(sk, q + 4 * (a.L - 2 - k));
     else if (k + 1 == a.L) u256_to_u64(sk, rem);
   }
@@ -471,24 +471,24 @@ __global__ void __launch_bounds__(HS_T) k_hs2(uint64_t* totals, uint64_t nb, U25
   const uint64_t b0 = (uint64_t)t * per;
   U256 acc = u256_zero();
   for (uint64_t k = 0; k < per; ++k)
-    if (b0 + k < nb) acc = Fr::add(u256_from_u64(totals + 4 * (b0 + k)), Fr::mul(zb, acc));
+    if (b0 + k < nb) acc = Fr::add(u256_from_u64(totals + 4 * (b0 + k)), Fr::mul_tp(zb, acc));
   sh[t] = acc;
   __syncthreads();
   U256 m = fr_pow(zb, per);  // multiplier across one thread's range
   for (int off = 1; off < HS_T; off <<= 1) {
     U256 x = sh[t];
-    if (t >= off) x = Fr::add(x, Fr::mul(m, sh[t - off]));
+    if (t >= off) x = Fr::add(x, Fr::mul_tp(m, sh[t - off]));
     __syncthreads();
     sh[t] = x;
     __syncthreads();
-    m = Fr::mul(m, m);
+    m = Fr::mul_tp(m, m);
   }
   U256 c = t ? sh[t - 1] : u256_zero();
   for (uint64_t k = 0; k < per; ++k) {
     if (b0 + k >= nb) break;
     const U256 x = u256_from_u64(totals + 4 * (b0 + k));
     u256_to_u64(c, totals + 4 * (b0 + k));
-    c = Fr::add(x, Fr::mul(zb, c));
+    c = Fr::add(x, Fr::mul_tp(zb, c));
   }
 }
 // s_k += z^(k - k_b + 1) s_in(b); the remainder likewise
@@ -504,8 +504,8 @@ __global__ void __launch_bounds__(HS_T) k_hs3(uint64_t* q, uint64_t L, U256 z, c
     const uint64_t k = k0 + m;
     if (k >= L) break;
     uint64_t* dst = k + 1 < L ? q + 4 * (L - 2 - k) : rem;
-    u256_to_u64(Fr::add(u256_from_u64(dst), Fr::mul(zk, cin)), dst);
-    zk = Fr::mul(zk, z);
+    u256_to_u64(Fr::add(u256_from_u64(dst), Fr::mul_tp(zk, cin)), dst);
+    zk = Fr::mul_tp(zk, z);
   }
 }
 
@@ -534,8 +534,8 @@ __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* par
     uint64_t end = start + EV_PER;
     if (end > e.len[p]) end = e.len[p];
     // conversion-free Horner: canonical acc times Montgomery-form x stays canonical
-    for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul(acc, x), u256_from_u64(e.poly[p] + 4 * j));
-    acc = Fr::mul(acc, fr_pow(x, start));
+    for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul_tp(acc, x), u256_from_u64(e.poly[p] + 4 * j));
+    acc = Fr::mul_tp(acc, fr_pow(x, start));
   }
   sh[t] = acc;
   __syncthreads();
