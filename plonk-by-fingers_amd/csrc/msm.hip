@@ -18,6 +18,7 @@
 #include <vector>
 #include "../../include/pbf.h"
 #include "msm.hpp"
+#include "msm_l29.hpp"
 #include "msm_sort.hpp"
 
 namespace pbf {
@@ -164,6 +165,74 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
 #endif
   }
   flush(c1);
+}
+
+// msm_chunk_acc with the accumulator in 29-bit limbs (msm_l29.hpp: no carry folds in the
+// products, ~205 instead of 319 VALU each); same chunking, same flush targets, the bucket
+// sums converted back to the 32-bit Montgomery form at the flush. Default; PBF_MSM_L29=0
+// selects msm_chunk_acc (A/B).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE)))
+msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
+                  const uint32_t* end, uint32_t m, Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent,
+                  const uint32_t* m_dev) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c0 = t * MSM_CH;
+  if (c0 >= m) return;
+  head[t].key = sent;
+  tail[t].key = sent;
+  const uint32_t mv = m_dev ? *m_dev : m;
+  if (c0 >= mv) return;
+  const uint32_t c1 = c0 + MSM_CH < mv ? c0 + MSM_CH : mv;
+  uint32_t cur = keys[c0], rs = c0;
+  l29::Acc acc;
+  acc.id = true;
+  if (cur == sent) return;
+  auto flush = [&](uint32_t re) {
+    const uint32_t bs = start[cur], be = end[cur];
+    const Xyzz v = l29::to_xyzz(acc);
+    if (bs < rs) {
+      head[t].acc = v;
+      head[t].key = cur;
+    } else if (be > re) {
+      tail[t].acc = v;
+      tail[t].key = cur;
+    } else {
+      buckets[cur] = v;
+    }
+  };
+  uint32_t k_nx = cur, v_nx = vals[c0];
+  Affine p_nx = pts[v_nx & ~MSM_NEG];
+  uint32_t k_n2 = 0, v_n2 = 0;
+  if (c0 + 1 < c1) k_n2 = keys[c0 + 1], v_n2 = vals[c0 + 1];
+  for (uint32_t j = c0; j < c1; ++j) {
+    const uint32_t k = k_nx, v = v_nx;
+    Affine p = p_nx;
+    if (j + 1 < c1) {
+      k_nx = k_n2;
+      v_nx = v_n2;
+      p_nx = pts[v_nx & ~MSM_NEG];
+      if (j + 2 < c1) k_n2 = keys[j + 2], v_n2 = vals[j + 2];
+    }
+    if (k != cur) {
+      flush(j);
+      if (k == sent) return;
+      cur = k;
+      rs = j;
+      acc.id = true;
+    }
+    if (v & MSM_NEG) p.y = Fq::sub(u256_zero(), p.y);
+    if (l29::madd(acc, l29::from_u256(p.x), l29::from_u256(p.y))) {
+      // P + P (rare): the doubled point, from the point reloaded
+      Affine q = pts[v & ~MSM_NEG];
+      if (v & MSM_NEG) q.y = Fq::sub(u256_zero(), q.y);
+      acc = l29::from_xyzz(G1::mdbl(q));
+    }
+  }
+  flush(c1);
+}
+static bool msm_l29() {
+  const char* e = getenv("PBF_MSM_L29");  // read per call: an A/B knob
+  return !(e && atoi(e) == 0);
 }
 
 // ---------------------------------------------------------------- fixed-base MSM
@@ -661,7 +730,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   // the reduction reads only the buckets the accumulation wrote (fx_bucket).
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
   PBF_HIP(hipMemsetAsync(w.span.p, 0, 4, s));
-  hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
+  hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
                      (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
                      (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr);
@@ -890,7 +959,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   // ---- accumulation
   // no bucket memset: msm_fx_cd reads only the buckets the accumulation wrote (fx_bucket)
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
-  hipLaunchKernelGGL(msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
+  hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
                      (const uint32_t*)vals2.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)m,
                      (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p, FX_NB, (const uint32_t*)nullptr);
   hipLaunchKernelGGL(msm_max_span, dim3(FX_NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,

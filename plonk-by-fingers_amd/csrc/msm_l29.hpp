@@ -1,0 +1,211 @@
+// 29-bit-limb Montgomery arithmetic for the MSM accumulation (BN254 Fq, gfx950; round 3).
+//
+// The 32-bit-limb product (fp256.hpp) folds the carry of every v_mad_u64_u32 into a third
+// accumulator word: 128 of its 319 VALU are those folds. With nine 29-bit limbs a partial
+// product is < 2^58, so a column of up to 18 of them plus the carry-in stays below 2^63 and
+// NO carry is ever folded: 162 v_mad_u64_u32, 17 column shifts and the 9 Montgomery digits,
+// ~205 VALU per product (R = 2^261).
+//
+// Domains: msm_chunk_acc_l29 keeps its XYZZ accumulator as X, Y = x 2^261 and ZZ, ZZZ = x 2^266
+// (mod p) while the points arrive in the library's 32-bit Montgomery form (x 2^256): then
+// every product of madd-2008-s lands in the domain its consumer expects (U2 = x ZZ 2^(256+266
+// -261) = x ZZ 2^261, ZZ3 = ZZ PP 2^(266+261-261), ...), and only the first point of a run and
+// the flushed bucket sums change domain (products by 2^266, 2^271, 2^256, 2^251 mod p).
+// Values stay lazily reduced: products of normalised inputs below 17.3p are below 3.3p (R is
+// 128x p), differences are taken as a + M - b with M = 8p or 16p in redundant limbs (every
+// limb but the top >= 2^31 - 4: no borrows), and the accumulator is bounded by 11.3p, all
+// derived in DESIGN.md §3.5. Results are exact group elements: bit-identical after the
+// canonical conversion at the flush.
+#pragma once
+#include <stdint.h>
+
+namespace pbf {
+namespace l29 {
+
+// scripts/gen_l29_constants.py (tests/test_l29_constants.py checks this block)
+constexpr uint32_t P29[9] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u, 0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+constexpr uint32_t NP29 = 0x04866389u;
+constexpr uint32_t M8P[9] = {0x83e7ea38u, 0x882305b2u, 0x83951a74u, 0x96a91683u, 0x8c2ecbbcu, 0x96da0601u, 0x85370a04u, 0x92e1319cu, 0x0183226fu};
+constexpr uint32_t M16P[9] = {0x87cfd470u, 0x90460b68u, 0x872a34ecu, 0x8d522d0au, 0x985d977du, 0x8db40c06u, 0x8a6e140du, 0x85c2633cu, 0x030644e3u};
+constexpr uint32_t C266[9] = {0x13349ca1u, 0x1a5d84a8u, 0x0a3e5cacu, 0x100249e0u, 0x12b951e8u, 0x0e92d304u, 0x14cb95b3u, 0x041b9d3du, 0x00058003u};
+constexpr uint32_t C271[9] = {0x1d1c9c4bu, 0x08a372eeu, 0x1273abadu, 0x17c9d397u, 0x1698b0a7u, 0x09c89e50u, 0x177e12abu, 0x185f3518u, 0x001ed378u};
+constexpr uint32_t C256[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u, 0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};
+constexpr uint32_t C251[9] = {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00080000u};
+
+constexpr uint32_t MASK = (1u << 29) - 1;
+
+struct L29 {
+  uint32_t l[9];
+};
+
+__device__ __forceinline__ L29 from_u256(const U256& a) {  // re-limb a < 2^256
+  L29 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int b = 29 * i, w = b >> 5, s = b & 31;
+    uint32_t v = a.w[w] >> s;
+    if (s > 3 && w + 1 < 8) v |= a.w[w + 1] << (32 - s);
+    r.l[i] = v & MASK;
+  }
+  return r;
+}
+__device__ __forceinline__ U256 to_u256(const L29& a) {  // a normalised and < 2^256
+  U256 r;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    const int b = 32 * w, i = b / 29, s = b % 29;
+    uint32_t v = a.l[i] >> s;
+    if (i + 1 < 9) v |= a.l[i + 1] << (29 - s);
+    if (s > 29 - 32 + 29 && i + 2 < 9) v |= a.l[i + 2] << (58 - s);
+    r.w[w] = v;
+  }
+  return r;
+}
+// Montgomery product a b 2^-261 (mod p) by product scanning, one 64-bit accumulator and no
+// carry folds; normalised output. Inputs: limbs < 2^29 (values < 2^261).
+__device__ __forceinline__ L29 mul(const L29& a, const L29& b) {
+  uint32_t m[9];
+  L29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; ++k) {
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; ++i) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = lo; i < (k < 9 ? k : 9); ++i) acc += (uint64_t)m[i] * P29[k - i];
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * NP29) & MASK;
+      acc += (uint64_t)m[k] * P29[0];  // the column's low 29 bits become 0
+    } else {
+      r.l[k - 9] = (uint32_t)acc & MASK;
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+// carry-normalise limbs < 2^32 (value < 2^261)
+__device__ __forceinline__ L29 norm(L29 a) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a.l[i + 1] += a.l[i] >> 29;
+    a.l[i] &= MASK;
+  }
+  return a;
+}
+// a + M - b (limb-wise, no borrows: M's limbs exceed b's), normalised
+__device__ __forceinline__ L29 sub(const L29& a, const L29& b, const uint32_t* M) {
+  L29 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.l[i] = a.l[i] + M[i] - b.l[i];
+  return norm(r);
+}
+// value == 0 or == p (a normalised, < 2p)
+__device__ __forceinline__ bool zero_mod_p(const L29& a) {
+  uint32_t z = 0, q = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    z |= a.l[i];
+    q |= a.l[i] ^ P29[i];
+  }
+  return z == 0 || q == 0;
+}
+// canonical value of a normalised a < 2p
+__device__ __forceinline__ L29 canon(const L29& a) {
+  bool ge = true;  // a >= p, compared from the top limb
+#pragma unroll
+  for (int i = 8; i >= 0; --i) {
+    if (a.l[i] != P29[i]) {
+      ge = a.l[i] > P29[i];
+      break;
+    }
+  }
+  if (!ge) return a;
+  L29 r;
+  int32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int32_t d = (int32_t)a.l[i] - (int32_t)P29[i] - borrow;
+    borrow = d < 0 ? 1 : 0;
+    r.l[i] = (uint32_t)(d + (borrow << 29));
+  }
+  return r;
+}
+__device__ __forceinline__ L29 konst(const uint32_t* c) {
+  L29 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.l[i] = c[i];
+  return r;
+}
+
+// XYZZ accumulator in the mixed domains above; `id` marks the identity
+struct Acc {
+  L29 X, Y, ZZ, ZZZ;
+  bool id;
+};
+
+// Xyzz (32-bit Montgomery, canonical, not the identity) -> Acc
+__device__ __forceinline__ Acc from_xyzz(const Xyzz& p) {
+  Acc r;
+  r.X = mul(from_u256(p.X), konst(C266));
+  r.Y = mul(from_u256(p.Y), konst(C266));
+  r.ZZ = mul(from_u256(p.ZZ), konst(C271));
+  r.ZZZ = mul(from_u256(p.ZZZ), konst(C271));
+  r.id = false;
+  return r;
+}
+// Acc -> Xyzz (32-bit Montgomery, canonical)
+__device__ __forceinline__ Xyzz to_xyzz(const Acc& a) {
+  if (a.id) return G1::identity();
+  Xyzz r;
+  r.X = to_u256(canon(mul(a.X, konst(C256))));
+  r.Y = to_u256(canon(mul(a.Y, konst(C256))));
+  r.ZZ = to_u256(canon(mul(a.ZZ, konst(C251))));
+  r.ZZZ = to_u256(canon(mul(a.ZZZ, konst(C251))));
+  return r;
+}
+
+// acc += (x, y) (affine point, 29-bit limbs of its 32-bit Montgomery coordinates):
+// madd-2008-s. Returns true in the exceptional case P + P (the caller replaces acc by the
+// doubled point): P == 0 is detected through ZZ3 = ZZ PP == 0 (PP == 0 iff P == 0, ZZ != 0),
+// then R == 0 tells P + P from P + (-P) (the identity). Products are ordered so that every
+// input dies as early as it can (the accumulation kernel is register-bound).
+__device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
+  if (a.id) {
+    const L29 one = konst(C266);
+    a.X = mul(x, one);
+    a.Y = mul(y, one);
+    a.ZZ = one;
+    a.ZZZ = one;
+    a.id = false;
+    return false;
+  }
+  const L29 P = sub(mul(x, a.ZZ), a.X, M16P);
+  const L29 R = sub(mul(y, a.ZZZ), a.Y, M16P);
+  const L29 PP = mul(P, P);
+  const L29 ZZ3 = mul(a.ZZ, PP);
+  if (zero_mod_p(ZZ3)) {  // P == 0: doubling (R == 0) or the identity
+    L29 one{};
+    one.l[0] = 1;
+    if (zero_mod_p(mul(R, one))) return true;
+    a.id = true;
+    return false;
+  }
+  const L29 PPP = mul(P, PP);
+  const L29 YP = mul(a.Y, PPP);
+  a.ZZZ = mul(a.ZZZ, PPP);
+  const L29 Q = mul(a.X, PP);
+  const L29 RR = mul(R, R);
+  L29 X3;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X3.l[i] = RR.l[i] + M8P[i] - PPP.l[i] - 2 * Q.l[i];
+  X3 = norm(X3);
+  a.Y = sub(mul(R, sub(Q, X3, M16P)), YP, M8P);
+  a.X = X3;
+  a.ZZ = ZZ3;
+  return false;
+}
+
+}  // namespace l29
+}  // namespace pbf

@@ -71,6 +71,11 @@ struct GlPassArgs {
   // * pad, polynomials `pitch` elements apart (user buffers: pad 0, pitch n)
   uint64_t in_pitch, out_pitch;
   uint32_t in_pad, out_pad, out_rows_log;
+  // two-pass plans (default; PBF_NTT_NO_PRETW=1 for A/B): the first pass multiplies its
+  // outputs by the second pass's twiddle w^(j k) (post_tw = that pass's [r][k] table: r = this
+  // pass's column j, k its output digit) and the second pass skips its own (skip_pass_tw)
+  const uint64_t* post_tw;
+  uint32_t skip_pass_tw;
 };
 
 // x * 2^(K mod 192) (mod p), K a compile-time exponent; 2^96 = -1. Exponents in
@@ -272,7 +277,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) t3[s2] = tb[(uint64_t)(4 * s2) << 16];
   }
-  if constexpr (!FIRST && RG != 3) {
+  if constexpr (!FIRST && RG != 3) if (!a.skip_pass_tw) {
     const uint64_t kmask = (1ull << a.log_ns) - 1;
     // in groups of 8 elements (loads of a group issue back to back; bounded live registers)
 #pragma unroll
@@ -480,6 +485,13 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
         // a run of R outputs never crosses a row of the next pass (R <= n / R_next)
         const uint64_t base0 = (j0 + w) << LOGR;
         const uint64_t base = base0 + (base0 >> a.out_rows_log) * a.out_pad;
+        if (a.post_tw) {
+          uint64_t tw[C];
+#pragma unroll
+          for (int k2 = 0; k2 < C; ++k2) tw[k2] = a.post_tw[base0 + k1 + 64 * k2];
+#pragma unroll
+          for (int k2 = 0; k2 < C; ++k2) x[u * C + bitrev_c(k2, LOGC)] = G::mul(x[u * C + bitrev_c(k2, LOGC)], tw[k2], f);
+        }
 #pragma unroll
         for (int k2 = 0; k2 < C; ++k2)
           if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)

@@ -743,6 +743,15 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (tiles > 0x7fffffffull) return fail(1, "batch too large");
     a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
     a.blk_log = blk_log;
+    // two-pass plans apply the second pass's twiddle w^(j k) at the first pass's stores (the
+    // first pass hides the product under its memory phase: 2^20 x 32 0.400 -> 0.386 ms,
+    // DESIGN.md §3.1); PBF_NTT_NO_PRETW=1 restores it at the second pass's loads
+    a.post_tw = nullptr;
+    a.skip_pass_tw = 0;
+    if (P == 2 && !blk && pad == 0 && split_log == 0 && !persist && !getenv("PBF_NTT_NO_PRETW") && p.twpass[1]->p) {
+      if (i == 0) a.post_tw = (const uint64_t*)p.twpass[1]->p;
+      else a.skip_pass_tw = 1;
+    }
     if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
     if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
     if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
