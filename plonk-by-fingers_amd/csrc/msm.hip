@@ -79,6 +79,28 @@ __global__ void msm_digits(const uint64_t* scalars, const uint8_t* inf, uint32_t
   }
 }
 
+// the same digits as 16-bit codes (msm_sort.hpp RS_DIG_*; the window is the entry's row)
+__global__ void msm_digits16(const uint64_t* scalars, const uint8_t* inf, uint16_t* dig, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = scalars + 4 * i;
+    const bool skip = inf[i] != 0;
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < MSM_NW; ++w) {
+      uint32_t d = (uint32_t)((s[w / 4] >> (16 * (w % 4))) & 0xFFFF) + carry;
+      bool neg = false;
+      if (d > MSM_NB) {
+        d = (1u << MSM_C) - d;
+        neg = true;
+        carry = 1;
+      } else {
+        carry = 0;
+      }
+      dig[(uint64_t)w * n + i] = (d == 0 || skip) ? RS_DIG_NONE : (uint16_t)((d - 1) | (neg ? 0x8000u : 0u));
+    }
+  }
+}
+
 __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* start, uint32_t* end, uint32_t sent) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t k = keys[j];
@@ -338,6 +360,24 @@ __global__ void __launch_bounds__(256) msm_fx_digits(const uint64_t* scalars, co
     }
   }
 }
+
+// The same digits as msm_fx_digits as planar 16-bit codes (msm_sort.hpp RS_DIG_*): the
+// first sort pass derives key and value from the code and the entry index
+__global__ void __launch_bounds__(256) msm_fx_digits16(const uint64_t* scalars, const uint8_t* inf, uint64_t first,
+                                                       uint64_t n, uint16_t* dig) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t* s = scalars + 4 * i;
+    const bool skip = inf[first + i] != 0;
+    uint32_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < FX_NW; ++w) {
+      bool neg;
+      const uint32_t d = fx_digit(s, w, carry, neg);
+      dig[(uint64_t)w * n + i] = (d == 0 || skip) ? RS_DIG_NONE : (uint16_t)((d - 1) | (neg ? 0x8000u : 0u));
+    }
+  }
+}
+static_assert(FX_NB - 1 <= 0x7FFF, "a digit code holds |d| - 1 in 15 bits");
 
 // Boundary join (fixed-base form: ~16 n / 2^15 entries per bucket, 512 at 2^20 points, so a
 // bucket crossing chunks spans ~12 of them; windowed form: ~2 chunks). Tree over each bucket's
@@ -686,12 +726,43 @@ static MsmWork msm_work(pbf_ctx* ctx) {
 // context's scratch
 static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* vals, uint32_t* keys2, uint32_t* vals2,
                           uint64_t m, int bits, hipStream_t s) {
-  if (m > 0xFFFFFFFFull - RS_TILE) return fail(PBF_EINVAL, "too many MSM entries");
+  if (m > 0xFFFFFFFFull - RS_TILE_MAX) return fail(PBF_EINVAL, "too many MSM entries");
   DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
   const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
   int rc;
   if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
   rs_sort(keys, vals, keys2, vals2, (uint32_t*)tk.p, (uint32_t*)tv.p, (uint32_t)m, bits, (uint32_t*)hb.p, s);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
+// The MSM sorts with their first pass from planar 16-bit digit codes (dg.dig, m = 16 n entries;
+// PBF_MSM_FUSED_SORT=1): (key, value) pairs sorted by the 16-bit (fixed-base) or 20-bit
+// (windowed) key into keys2 / vals2. Pass 1 (bits 0-7) reads the codes, the later passes the
+// ping-pong scratch. Measured no faster than the pair sort so far: off by default.
+static bool msm_fused_sort() {
+  const char* e = getenv("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (default off)
+  return e && e[0] == '1';
+}
+// bits: key bits to sort (2 or 3 passes; the last lands in keys2 / vals2, the middle one in
+// the caller's keys / vals buffers, free once the codes are read)
+static int msm_sort_digits(pbf_ctx* ctx, const RsDigits& dg, uint32_t* keys2, uint32_t* vals2, uint32_t* mid_k,
+                           uint32_t* mid_v, uint64_t m, int bits, hipStream_t s) {
+  if (m > 0xFFFFFFFFull - RS_TILE_MAX) return fail(PBF_EINVAL, "too many MSM entries");
+  if ((bits != 16 && bits != 20) || dg.kw % 256 || !rs_dig_ok(dg.n))
+    return fail(PBF_EINVAL, "digit sort: 16 or 20 key bits, whole key bytes per window, n >= 256");
+  DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
+  const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
+  int rc;
+  if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
+  uint32_t *k1 = (uint32_t*)tk.p, *v1 = (uint32_t*)tv.p, *hist = (uint32_t*)hb.p;
+  rs_pass<RS_ITEMS, true>(nullptr, nullptr, k1, v1, (uint32_t)m, 0, hist, s, dg);
+  if (bits == 16) {
+    rs_pass<RS_ITEMS>(k1, v1, keys2, vals2, (uint32_t)m, 8, hist, s);
+  } else {
+    rs_pass<RS_ITEMS>(k1, v1, mid_k, mid_v, (uint32_t)m, 8, hist, s);
+    rs_pass<RS_ITEMS>(mid_k, mid_v, keys2, vals2, (uint32_t)m, 16, hist, s);
+  }
   PBF_HIP(hipGetLastError());
   return 0;
 }
@@ -716,11 +787,21 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
     return rc;
   hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, (Affine*)w.pts.p,
                      (uint8_t*)w.inf.p, n);
-  hipLaunchKernelGGL(msm_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, (const uint8_t*)w.inf.p,
-                     (uint32_t*)w.keys.p, (uint32_t*)w.vals.p, n);
-  if ((rc = msm_sort_pairs(ctx, (const uint32_t*)w.keys.p, (const uint32_t*)w.vals.p, (uint32_t*)w.keys2.p,
-                           (uint32_t*)w.vals2.p, m, MSM_BB + 5, s)))
-    return rc;
+  if (msm_fused_sort() && rs_dig_ok(n)) {
+    // 16-bit digit codes in w.keys2 (read by pass 1; only pass 3 writes w.keys2 again)
+    hipLaunchKernelGGL(msm_digits16, dim3(grid1(n)), dim3(256), 0, s, d_sc, (const uint8_t*)w.inf.p,
+                       (uint16_t*)w.keys2.p, n);
+    const RsDigits dg{(const uint16_t*)w.keys2.p, (uint32_t)n, 0, 0, 1u << MSM_BB, MSM_SENTINEL, MSM_NEG};
+    if ((rc = msm_sort_digits(ctx, dg, (uint32_t*)w.keys2.p, (uint32_t*)w.vals2.p, (uint32_t*)w.keys.p,
+                              (uint32_t*)w.vals.p, m, MSM_BB + 5, s)))
+      return rc;
+  } else {
+    hipLaunchKernelGGL(msm_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, (const uint8_t*)w.inf.p,
+                       (uint32_t*)w.keys.p, (uint32_t*)w.vals.p, n);
+    if ((rc = msm_sort_pairs(ctx, (const uint32_t*)w.keys.p, (const uint32_t*)w.vals.p, (uint32_t*)w.keys2.p,
+                             (uint32_t*)w.vals2.p, m, MSM_BB + 5, s)))
+      return rc;
+  }
   PBF_HIP(hipMemsetAsync(w.start.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
@@ -947,11 +1028,20 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
     return rc;
   const uint8_t* inf = (const uint8_t*)fb.inf.p;
   // ---- digits, sort by bucket, bucket bounds
-  hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
-                     (uint32_t*)keys.p, (uint32_t*)vals.p);
-  if ((rc = msm_sort_pairs(ctx, (const uint32_t*)keys.p, (const uint32_t*)vals.p, (uint32_t*)keys2.p,
-                           (uint32_t*)vals2.p, m, FX_C, s)))
-    return rc;
+  if (msm_fused_sort() && rs_dig_ok(n)) {
+    // keys holds the 2-byte digit codes; vals is not used
+    if ((uint64_t)FX_NW * n_table >= MSM_NEG) return fail(PBF_EINVAL, "fixed-base MSM: table too large");
+    hipLaunchKernelGGL(msm_fx_digits16, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n, (uint16_t*)keys.p);
+    const RsDigits dg{(const uint16_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, FX_NB, MSM_NEG};
+    if ((rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, nullptr, nullptr, m, FX_C, s)))
+      return rc;
+  } else {
+    hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
+                       (uint32_t*)keys.p, (uint32_t*)vals.p);
+    if ((rc = msm_sort_pairs(ctx, (const uint32_t*)keys.p, (const uint32_t*)vals.p, (uint32_t*)keys2.p,
+                             (uint32_t*)vals2.p, m, FX_C, s)))
+      return rc;
+  }
   hipLaunchKernelGGL(msm_fx_clear, dim3(FX_NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
                      (uint32_t*)spb.p);
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,

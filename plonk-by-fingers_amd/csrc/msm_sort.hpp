@@ -9,30 +9,69 @@
 //               rounds; the per-wave counts, scanned, order the waves), a locally sorted copy
 //               of the tile in LDS, then every digit's run written to its global position
 //               (consecutive lanes write consecutive addresses of a run)
+// A pass may read its input from RsDigits instead of (keys, vals): the fixed-base MSM's first
+// pass takes planar 16-bit signed digits and derives each entry's key and value from the digit
+// and the entry index, so the digit kernel writes 2 B per entry instead of 8 and the first
+// pass reads 2 B instead of 4 (histogram) and 8 (scatter).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace pbf {
 
-constexpr int RS_T = 256, RS_ITEMS = 16, RS_TILE = RS_T * RS_ITEMS;
+#ifndef PBF_RS_ITEMS
+#define PBF_RS_ITEMS 32
+#endif
+// RS_ITEMS entries per thread (a tile of 8192 entries: 64 KiB of LDS for the locally sorted
+// copy, two workgroups per CU; runs of ~32 entries per digit and tile on the store side; 2^28
+// pairs: 5.1 ms with 4096-entry tiles, 4.0 ms with 8192, scripts/ubench/sort_bench.hip).
+// RS_TILE: the smallest tile any caller may pick (it sizes the histogram scratch); RS_TILE_MAX
+// the largest (it bounds m).
+constexpr int RS_T = 256, RS_ITEMS = PBF_RS_ITEMS, RS_TILE = RS_T * 16, RS_TILE_MAX = RS_T * 64;
 
+// 16-bit signed digit code: |d| - 1 for d > 0, 0x8000 | (|d| - 1) for d < 0, RS_DIG_NONE for
+// no entry (a zero digit or an identity point)
+constexpr uint16_t RS_DIG_NONE = 0xFFFF;
+struct RsDigits {
+  const uint16_t* dig;  // dig[w * n + i]: window w's digit code of scalar i
+  uint32_t n;           // scalars
+  uint32_t n_table;     // value of entry (w, i) = w * n_table + first + i, | neg if d < 0
+  uint32_t first;
+  uint32_t kw;    // key of entry (w, i) = w * kw + (|d| - 1) (fixed base: 0; windowed: 2^15)
+  uint32_t zkey;  // key of RS_DIG_NONE (sorts last)
+  uint32_t neg;   // sign flag of the value
+};
+__device__ __forceinline__ uint32_t rs_dig_key(uint16_t c, uint32_t w, const RsDigits& dg) {
+  return c == RS_DIG_NONE ? dg.zkey : w * dg.kw + (c & 0x7FFFu);
+}
+
+template <int ITEMS, bool DIG = false>
 __global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m, uint32_t shift, uint32_t ntiles,
-                                                uint32_t* hist) {
+                                                uint32_t* hist, RsDigits dg) {
   __shared__ uint32_t h[RS_T / 64][256];  // one histogram per wave (less atomic contention)
   const int wave = threadIdx.x >> 6;
 #pragma unroll
   for (int w = 0; w < RS_T / 64; ++w) h[w][threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t base = blockIdx.x * RS_TILE;
-  uint32_t k[RS_ITEMS];
+  const uint32_t base = blockIdx.x * (RS_T * ITEMS);
+  uint32_t k[ITEMS];
+  if constexpr (DIG) {
+    // pass 1 (shift 0, kw a multiple of 256): the digit follows from the code alone
 #pragma unroll
-  for (int u = 0; u < RS_ITEMS; ++u) {
-    const uint32_t e = base + u * RS_T + threadIdx.x;
-    k[u] = e < m ? keys[e] : 0xFFFFFFFFu;
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t e = base + u * RS_T + threadIdx.x;
+      const uint16_t c = e < m ? dg.dig[e] : RS_DIG_NONE;
+      k[u] = e < m ? (c == RS_DIG_NONE ? dg.zkey : c & 0x7FFFu) : 0xFFFFFFFFu;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+      const uint32_t e = base + u * RS_T + threadIdx.x;
+      k[u] = e < m ? keys[e] : 0xFFFFFFFFu;
+    }
   }
 #pragma unroll
-  for (int u = 0; u < RS_ITEMS; ++u)
+  for (int u = 0; u < ITEMS; ++u)
     if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[wave][(k[u] >> shift) & 255], 1u);
   __syncthreads();
   uint32_t c = 0;
@@ -87,23 +126,37 @@ __global__ void __launch_bounds__(RS_T) rs_scan(uint32_t* hist, uint32_t ntiles,
 // Then the per-wave counts are scanned across the waves, every entry goes to its slot of a
 // locally sorted copy of the tile in LDS, and each digit's run is written to its global
 // position.
-constexpr int RS_WAVES = RS_T / 64, RS_WQ = RS_TILE / RS_WAVES;  // entries per wave
-__global__ void __launch_bounds__(RS_T) rs_scatter(const uint32_t* keys, const uint32_t* vals, uint32_t* okeys,
+constexpr int RS_WAVES = RS_T / 64;
+template <int ITEMS, bool DIG = false>
+__global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) rs_scatter(const uint32_t* keys, const uint32_t* vals, uint32_t* okeys,
                                                    uint32_t* ovals, uint32_t m, uint32_t shift, uint32_t ntiles,
-                                                   const uint32_t* hist, const uint32_t* total) {
+                                                   const uint32_t* hist, const uint32_t* total, RsDigits dg) {
   __shared__ uint32_t s[RS_T];
   __shared__ uint32_t gbase[256], lstart[256];
   __shared__ uint32_t wc[RS_WAVES][256];
-  __shared__ uint32_t lk[RS_TILE], lv[RS_TILE];
+  constexpr int TILE = RS_T * ITEMS, RS_WQ = TILE / RS_WAVES;  // entries per tile / per wave
+  __shared__ uint32_t lk[TILE], lv[TILE];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const uint32_t tile = blockIdx.x, base = tile * RS_TILE;
+  const uint32_t tile = blockIdx.x, base = tile * TILE;
   // this wave's entries (all loads first: their latency overlaps the setup below)
-  uint32_t key[RS_ITEMS], val[RS_ITEMS];
+  // DIG: key[r] holds the raw 16-bit code, no value registers: the digit of pass 1 (shift 0,
+  // kw a multiple of 256) follows from the code alone; key and value from the code and the
+  // entry index when the entry is placed in LDS
+  uint32_t key[ITEMS], val[DIG ? 1 : ITEMS];
+  const uint32_t e0 = base + wave * RS_WQ + lane;  // this lane's entries are 64 apart
+  if constexpr (DIG) {
 #pragma unroll
-  for (int r = 0; r < RS_ITEMS; ++r) {
-    const uint32_t e = base + wave * RS_WQ + r * 64 + lane;
-    key[r] = e < m ? keys[e] : 0;
-    val[r] = e < m ? vals[e] : 0;
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t e = e0 + r * 64;
+      key[r] = e < m ? dg.dig[e] : RS_DIG_NONE;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const uint32_t e = base + wave * RS_WQ + r * 64 + lane;
+      key[r] = e < m ? keys[e] : 0;
+      val[r] = e < m ? vals[e] : 0;
+    }
   }
   // global start of digit t's run of this tile; this tile's count of digit t (from the
   // prefixes of this tile and the next); the local start of digit t (exclusive scan)
@@ -120,11 +173,11 @@ __global__ void __launch_bounds__(RS_T) rs_scatter(const uint32_t* keys, const u
   for (int w = 0; w < RS_WAVES; ++w) wc[w][t] = 0;
   __syncthreads();
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint32_t rank[RS_ITEMS];
+  uint32_t rank[ITEMS];
 #pragma unroll
-  for (int r = 0; r < RS_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const bool valid = base + wave * RS_WQ + r * 64 + lane < m;
-    const uint32_t d = (key[r] >> shift) & 255;
+    const uint32_t d = DIG ? (key[r] == RS_DIG_NONE ? dg.zkey : key[r] & 0x7FFFu) & 255 : (key[r] >> shift) & 255;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -147,19 +200,37 @@ __global__ void __launch_bounds__(RS_T) rs_scatter(const uint32_t* keys, const u
     }
   }
   __syncthreads();
+  if constexpr (DIG) {
+    uint32_t w = e0 / dg.n, i = e0 - w * dg.n;
 #pragma unroll
-  for (int r = 0; r < RS_ITEMS; ++r) {
-    if (base + wave * RS_WQ + r * 64 + lane < m) {
-      const uint32_t d = (key[r] >> shift) & 255;
-      const uint32_t pos = lstart[d] + wc[wave][d] + rank[r];
-      lk[pos] = key[r];
-      lv[pos] = val[r];
+    for (int r = 0; r < ITEMS; ++r) {
+      if (e0 + r * 64 < m) {
+        const uint32_t c = key[r], k = rs_dig_key((uint16_t)c, w, dg);
+        const uint32_t d = k & 255;
+        const uint32_t pos = lstart[d] + wc[wave][d] + rank[r];
+        lk[pos] = k;
+        lv[pos] = (w * dg.n_table + dg.first + i) | (c != RS_DIG_NONE && (c & 0x8000u) ? dg.neg : 0u);
+      }
+      i += 64;
+      const bool wrap = i >= dg.n;
+      i -= wrap ? dg.n : 0u;
+      w += wrap ? 1u : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (e0 + r * 64 < m) {
+        const uint32_t d = (key[r] >> shift) & 255;
+        const uint32_t pos = lstart[d] + wc[wave][d] + rank[r];
+        lk[pos] = key[r];
+        lv[pos] = val[r];
+      }
     }
   }
   __syncthreads();
-  const uint32_t count = m - base < (uint32_t)RS_TILE ? m - base : (uint32_t)RS_TILE;
+  const uint32_t count = m - base < (uint32_t)TILE ? m - base : (uint32_t)TILE;
 #pragma unroll
-  for (int r = 0; r < RS_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const uint32_t i = r * RS_T + t;
     if (i < count) {
       const uint32_t k = lk[i];
@@ -171,27 +242,38 @@ __global__ void __launch_bounds__(RS_T) rs_scatter(const uint32_t* keys, const u
   }
 }
 
+// One pass: (kin, vin) (or dg) -> (kout, vout) stably sorted by key bits [shift, shift + 8).
+// hist: 256 * ntiles + 256 u32 of scratch.
+// DIG (pass 1 only, shift 0) requires dg.n >= RS_T (rs_dig_ok) and dg.kw % 256 == 0.
+inline bool rs_dig_ok(uint64_t n) { return n >= (uint64_t)RS_T; }
+template <int ITEMS = RS_ITEMS, bool DIG = false>
+inline void rs_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t m,
+                    uint32_t shift, uint32_t* hist, hipStream_t s, RsDigits dg = {}) {
+  constexpr uint32_t TILE = RS_T * ITEMS;
+  static_assert(ITEMS >= 16 && TILE <= RS_TILE_MAX, "the scratch is sized for RS_TILE .. RS_TILE_MAX");
+  const uint32_t ntiles = (m + TILE - 1) / TILE;
+  uint32_t* total = hist + 256ull * ntiles;
+  hipLaunchKernelGGL((rs_hist<ITEMS, DIG>), dim3(ntiles), dim3(RS_T), 0, s, kin, m, shift, ntiles, hist, dg);
+  hipLaunchKernelGGL(rs_scan, dim3(256), dim3(RS_T), 0, s, hist, ntiles, total);
+  hipLaunchKernelGGL((rs_scatter<ITEMS, DIG>), dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, m, shift, ntiles,
+                     (const uint32_t*)hist, (const uint32_t*)total, dg);
+}
+
 // Sort m pairs by key bits [0, bits): keys/vals -> keys2/vals2 (inputs unchanged; tmpk / tmpv:
 // m u32 each of ping-pong scratch). hist: 256 * ntiles + 256 u32 of scratch.
+template <int ITEMS = RS_ITEMS>
 inline int rs_sort(const uint32_t* keys, const uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t* tmpk,
                    uint32_t* tmpv, uint32_t m, int bits, uint32_t* hist, hipStream_t s) {
   if (m == 0) return 0;
-  const uint32_t ntiles = (m + RS_TILE - 1) / RS_TILE;
-  uint32_t* total = hist + 256ull * ntiles;
   const int passes = (bits + 7) / 8;
   // pass p reads (k_in, v_in) and writes (k_out, v_out); the last pass writes keys2 / vals2
   const uint32_t* kin = keys;
   const uint32_t* vin = vals;
   for (int p = 0; p < passes; ++p) {
-    const bool last = p + 1 == passes;
     // an even number of passes left after this one writes tmp, else keys2 (so the last lands there)
     uint32_t* kout = ((passes - 1 - p) % 2 == 0) ? keys2 : tmpk;
     uint32_t* vout = ((passes - 1 - p) % 2 == 0) ? vals2 : tmpv;
-    (void)last;
-    hipLaunchKernelGGL(rs_hist, dim3(ntiles), dim3(RS_T), 0, s, kin, m, (uint32_t)(8 * p), ntiles, hist);
-    hipLaunchKernelGGL(rs_scan, dim3(256), dim3(RS_T), 0, s, hist, ntiles, total);
-    hipLaunchKernelGGL(rs_scatter, dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, m, (uint32_t)(8 * p), ntiles,
-                       (const uint32_t*)hist, (const uint32_t*)total);
+    rs_pass<ITEMS>(kin, vin, kout, vout, m, (uint32_t)(8 * p), hist, s);
     kin = kout;
     vin = vout;
   }

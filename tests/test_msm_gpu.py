@@ -206,6 +206,29 @@ def test_fixed_base_msm_edges_and_cache(ctx):
     assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), dz.data_ptr(), len(pts)) == (0, 0)
 
 
+@pytest.mark.parametrize("n_points,n", [(300, 17), (300, 300), (70001, 70001), (70001, 69000)])
+def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n):
+    """The MSM sorts' first pass from 16-bit digit codes (msm_sort.hpp RsDigits; fixed-base and
+    windowed forms; PBF_MSM_FUSED_SORT=1) gives the same result as the (key, value) pair sort, including tiles that straddle
+    two windows (n not a multiple of the 8192-entry tile); the prover's sharded commits
+    (first point != 0) are covered by the virtual-rank prover tests."""
+    rnd = random.Random(n_points + n)
+    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(32)]
+    pts = (base * (n_points // len(base) + 1))[:n_points]
+    sc = [rnd.randrange(R) for _ in range(n)]
+    sc[::97] = [0] * len(sc[::97])  # zero scalars: every window's code is "no entry"
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    ptr = ds.data_ptr()
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
+        res[fused] = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ptr, n)
+        res["w" + fused] = ctx.msm_g1_dev(dp.data_ptr(), ptr, n)  # the windowed form's 3-pass sort
+    assert res["1"] == res["0"] == res["w1"] == res["w0"]
+    if n <= 300:
+        assert res["1"] == enc(bn254.msm_naive(pts[:n], sc))
+
+
 def test_fixed_base_msm_2p20_discrete_log(ctx):
     """Config-4 size through the fixed-base path: P_i = t_i G, result (sum s_i t_i) G."""
     import torch
