@@ -736,13 +736,12 @@ static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* va
   return 0;
 }
 
-// The MSM sorts with their first pass from planar 16-bit digit codes (dg.dig, m = 16 n entries;
-// PBF_MSM_FUSED_SORT=1): (key, value) pairs sorted by the 16-bit (fixed-base) or 20-bit
+// The MSM sorts with their first pass from planar 16-bit digit codes (dg.dig, m = 16 n entries): (key, value) pairs sorted by the 16-bit (fixed-base) or 20-bit
 // (windowed) key into keys2 / vals2. Pass 1 (bits 0-7) reads the codes, the later passes the
-// ping-pong scratch. Measured no faster than the pair sort so far: off by default.
+// ping-pong scratch. Default; PBF_MSM_FUSED_SORT=0 selects the (key, value) pair sort.
 static bool msm_fused_sort() {
-  const char* e = getenv("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (default off)
-  return e && e[0] == '1';
+  const char* e = getenv("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (=0: pair sort)
+  return !(e && e[0] == '0');
 }
 // bits: key bits to sort (2 or 3 passes; the last lands in keys2 / vals2, the middle one in
 // the caller's keys / vals buffers, free once the codes are read)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Round 3: fixed-base MSM median (HIP events) at 2^LOG points (argv[1], default 24), with the
-fixed-base sort's first pass from 16-bit digit codes (PBF_MSM_FUSED_SORT=1) and from (key,
-value) pairs (=0, the default); the two results must agree."""
+fixed-base sort's first pass from 16-bit digit codes (PBF_MSM_FUSED_SORT=1, the default) and
+from (key, value) pairs (=0); the two results must agree."""
 import os
 import sys
 

@@ -209,7 +209,7 @@ def test_fixed_base_msm_edges_and_cache(ctx):
 @pytest.mark.parametrize("n_points,n", [(300, 17), (300, 300), (70001, 70001), (70001, 69000)])
 def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n):
     """The MSM sorts' first pass from 16-bit digit codes (msm_sort.hpp RsDigits; fixed-base and
-    windowed forms; PBF_MSM_FUSED_SORT=1) gives the same result as the (key, value) pair sort, including tiles that straddle
+    windowed forms; the default) gives the same result as the (key, value) pair sort (=0), including tiles that straddle
     two windows (n not a multiple of the 8192-entry tile); the prover's sharded commits
     (first point != 0) are covered by the virtual-rank prover tests."""
     rnd = random.Random(n_points + n)
