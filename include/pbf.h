@@ -177,6 +177,11 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
  * window) digit shares one set of 2^15 buckets.                                           */
 int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
                                size_t n, uint64_t* out, void* stream);
+/* The same against points [first, first + n) of the fixed base set: out = sum_{i<n}
+ * scalars[i] * points[first + i] (one rank's point range of a sharded commitment; the
+ * window table still covers all n_points and is shared with the call above).               */
+int pbf_msm_g1_bn254_fixed_range_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, size_t first,
+                                     const uint64_t* d_scalars, size_t n, uint64_t* out, void* stream);
 /* out_i = scalars_i * G (G = (1, 2)), device pointers                               */
 int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t* d_out, size_t n,
                               void* stream);

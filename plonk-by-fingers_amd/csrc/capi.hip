@@ -110,6 +110,8 @@ int pbf_ctx_release_caches(pbf_ctx* ctx) {
   for (auto it = ctx->named.begin(); it != ctx->named.end();)
     it = it->first.compare(0, 5, "snap.") == 0 ? ctx->named.erase(it) : std::next(it);
   ctx->snap_words.clear();
+  ctx->snap_gen.clear();
+  ctx->snap_used.clear();
   return PBF_OK;
 }
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
@@ -19,6 +20,12 @@ static const uint64_t GOLDILOCKS = 0xFFFFFFFF00000001ull;
 enum FieldKind { FIELD_GOLDILOCKS = 0, FIELD_MOD32 = 1 };
 
 void set_error(const std::string& s);
+// A/B switch that is on by default: off only when the variable parses as the integer 0
+// ("0", "00"); unset, empty or any other value keeps it on. Read per call.
+inline bool env_default_on(const char* name) {
+  const char* e = getenv(name);
+  return !(e && *e && atoi(e) == 0);
+}
 int fail(int code, const std::string& s);
 
 #define PBF_HIP(expr)                                                                        \
@@ -81,8 +88,11 @@ struct NttPlan {
   // regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel): 8,8,8 passes with the general
   // twiddles between 64-point blocks only; tables tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18),
   // t3[f][a0][j] (2^24, n^-1 folded in for the inverse)
+  // rg: the plan qualifies; the tables (~130 MiB, mostly t3) are built the first time a run
+  // takes the regrouped path (ntt_launch.hip ensure_rg_tables), never for runs that cannot
   bool rg = false;
-  DevBuf rg_tc1, rg_t2, rg_t3;
+  mutable bool rg_built = false;
+  mutable DevBuf rg_tc1, rg_t2, rg_t3;
   bool ip = false;
   std::vector<int> ip_r;
   std::vector<std::shared_ptr<DevBuf>> ip_tw, ip_tc;
@@ -182,6 +192,11 @@ struct pbf_ctx {
   // snapshots of cache inputs (msm.hpp snapshot_check): device copies in buf("snap." + name),
   // their lengths in u64 words here
   std::map<std::string, uint64_t> snap_words;
+  // one snapshot per input (named after the data: "q", "copies", "g1pts"), shared by every
+  // cache derived from it; snap_gen[name] changes whenever the copy is replaced, and
+  // snap_used[consumer + "/" + name] is the generation that consumer's cache was built from
+  std::map<std::string, uint64_t> snap_gen, snap_used;
+  uint64_t snap_next_gen = 1;
   // pairing check: the G2 inputs whose prepared lines sit in buf("pc.lines") (pairing.hip)
   std::vector<uint64_t> pair_g2_key;
   // prover proving key: the preprocessed polynomials' coefficients and coset evaluations

@@ -253,8 +253,7 @@ msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
   flush(c1);
 }
 static bool msm_l29() {
-  const char* e = getenv("PBF_MSM_L29");  // read per call: an A/B knob
-  return !(e && atoi(e) == 0);
+  return env_default_on("PBF_MSM_L29");  // read per call: an A/B knob
 }
 
 // ---------------------------------------------------------------- fixed-base MSM
@@ -623,8 +622,7 @@ __global__ void __launch_bounds__(64) msm_fx_total_q(const Xyzz* sub, Xyzz* out)
   if (threadIdx.x == 0) out[blockIdx.x] = v;
 }
 static bool msm_quad_tail() {
-  const char* e = getenv("PBF_MSM_QUAD");  // read per call: an A/B knob
-  return !(e && atoi(e) == 0);
+  return env_default_on("PBF_MSM_QUAD");  // read per call: an A/B knob
 }
 
 // Exact-content cache validation (snapshot_check below): diff[0] = 1 when a and b differ in
@@ -740,8 +738,7 @@ static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* va
 // (windowed) key into keys2 / vals2. Pass 1 (bits 0-7) reads the codes, the later passes the
 // ping-pong scratch. Default; PBF_MSM_FUSED_SORT=0 selects the (key, value) pair sort.
 static bool msm_fused_sort() {
-  const char* e = getenv("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (=0: pair sort)
-  return !(e && e[0] == '0');
+  return env_default_on("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (=0: pair sort)
 }
 // bits: key bits to sort (2 or 3 passes; the last lands in keys2 / vals2, the middle one in
 // the caller's keys / vals buffers, free once the codes are read)
@@ -877,7 +874,7 @@ static void msm_finish_host(const Xyzz* sums, uint64_t* out) {
 // used before is linear over GF(2), so a chosen circuit or point set could collide with a cached
 // one). The context keeps a device copy -- a snapshot -- of every input a cache is derived from;
 // a hit requires the input to equal its snapshot word for word.
-int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bool* same) {
+int snapshot_check(pbf_ctx* ctx, const char* consumer, const SnapItem* items, int k, hipStream_t s, bool* same) {
   DevBuf& fl = ctx->buf("snap.flags");
   int rc = fl.ensure((size_t)k * sizeof(int));
   if (rc) return rc;
@@ -902,13 +899,22 @@ int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bo
   PBF_HIP(hipStreamSynchronize(s));
   *same = true;
   for (int i = 0; i < k; ++i) {
-    if (!fresh[i] && !diff[i]) continue;
+    const std::string used = std::string(consumer) + "/" + items[i].name;
+    if (!fresh[i] && !diff[i]) {
+      // the data equals the snapshot; the consumer's cache is current only if it was built from
+      // this very snapshot (another consumer may have replaced it since)
+      if (ctx->snap_used[used] != ctx->snap_gen[items[i].name]) *same = false;
+      ctx->snap_used[used] = ctx->snap_gen[items[i].name];
+      continue;
+    }
     *same = false;
     DevBuf& b = ctx->buf(std::string("snap.") + items[i].name);
     ctx->snap_words.erase(items[i].name);  // valid again only once the copy is enqueued
     if ((rc = b.ensure(items[i].words * 8 + 8))) return rc;
     if (items[i].words) PBF_HIP(hipMemcpyAsync(b.p, items[i].p, items[i].words * 8, hipMemcpyDeviceToDevice, s));
     ctx->snap_words[items[i].name] = items[i].words;
+    ctx->snap_gen[items[i].name] = ctx->snap_next_gen++;
+    ctx->snap_used[used] = ctx->snap_gen[items[i].name];
   }
   return 0;
 }
@@ -918,9 +924,9 @@ int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bo
 // kept with it (fixed_base.inf)
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
   if (n == 0 || n > 0x7FFFFFFFull / FX_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
-  const SnapItem it{"fx.pts", d_pts, 8 * n};
+  const SnapItem it{"g1pts", d_pts, 8 * n};
   bool same = false;
-  int rc = snapshot_check(ctx, &it, 1, s, &same);
+  int rc = snapshot_check(ctx, "fx", &it, 1, s, &same);
   if (rc) return rc;
   auto& fb = ctx->fixed_base;
   if (same && fb.valid && fb.n == n && fb.table.p) {
@@ -947,8 +953,9 @@ int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_
   *out = nullptr;
   auto& fb = ctx->fixed_base;
   if (!fb.valid || fb.n != n || !fb.table.p) return 0;
-  auto w = ctx->snap_words.find("fx.pts");
+  auto w = ctx->snap_words.find("g1pts");
   if (w == ctx->snap_words.end() || w->second != 8 * n) return 0;
+  if (ctx->snap_used["fx/g1pts"] != ctx->snap_gen["g1pts"]) return 0;  // replaced since the build
   DevBuf& fl = ctx->buf("snap.flags");
   int rc = fl.ensure(sizeof(int));
   if (rc) return rc;
@@ -956,7 +963,7 @@ int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_
   uint64_t blocks = (8 * n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_snap_compare, dim3((uint32_t)blocks), dim3(256), 0, s,
-                     (const uint64_t*)ctx->buf("snap.fx.pts").p, d_pts, 8 * n, (int*)fl.p);
+                     (const uint64_t*)ctx->buf("snap.g1pts").p, d_pts, 8 * n, (int*)fl.p);
   PBF_HIP(hipGetLastError());
   int diff = 0;
   PBF_HIP(hipMemcpyAsync(&diff, fl.p, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1168,8 +1175,15 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
 // points on every call)
 int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, const uint64_t* d_scalars,
                                size_t n, uint64_t* out, void* stream) {
+  return pbf_msm_g1_bn254_fixed_range_dev(ctx, d_points, n_points, 0, d_scalars, n, out, stream);
+}
+
+// out = sum_{i<n} scalars[i] * points[first + i] against the fixed base set (one rank's point
+// range of a sharded commitment)
+int pbf_msm_g1_bn254_fixed_range_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_points, size_t first,
+                                     const uint64_t* d_scalars, size_t n, uint64_t* out, void* stream) {
   if (!ctx || !out || (n && (!d_points || !d_scalars))) return fail(PBF_EINVAL, "null argument");
-  if (n > n_points) return fail(PBF_EINVAL, "more scalars than base points");
+  if (first > n_points || n > n_points - first) return fail(PBF_EINVAL, "scalar range beyond the base points");
   if (n == 0) { for (int i = 0; i < 8; ++i) out[i] = 0; return PBF_OK; }
   PBF_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
@@ -1178,7 +1192,7 @@ int pbf_msm_g1_bn254_fixed_dev(pbf_ctx* ctx, const uint64_t* d_points, size_t n_
   if (rc) return rc;
   DevBuf& res = ctx->buf("msm.fixed_result");
   if ((rc = res.ensure(sizeof(Xyzz)))) return rc;
-  if ((rc = msm_fixed_device(ctx, tbl, n_points, 0, d_scalars, n, s, (Xyzz*)res.p))) return rc;
+  if ((rc = msm_fixed_device(ctx, tbl, n_points, first, d_scalars, n, s, (Xyzz*)res.p))) return rc;
   if ((rc = msm_fixed_wait(ctx, s))) return rc;
   Xyzz r;
   PBF_HIP(hipMemcpyAsync(&r, res.p, sizeof(Xyzz), hipMemcpyDeviceToHost, s));

@@ -20,15 +20,18 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
 // before reading a d_result of msm_fixed_device on s).
 int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s);
 // Exact-content validation of context caches: *same = every item's `words` u64 equal the
-// context's snapshot named `name` (same length, word for word). Items that differ (or have no
-// snapshot yet) get their snapshot replaced by a device copy of the input, so the caller
-// rebuilds its cache from these inputs. One compare kernel per item, one stream sync in all.
+// context's snapshot named `name` (same length, word for word) AND that snapshot is the one
+// `consumer`'s cache was last built from. Snapshots are named after the data and shared by
+// every consumer (the prover's key, the verifier's key and the MSM window table all validate
+// against one copy of q / copies / the SRS points). Items that differ (or have no snapshot
+// yet) get their snapshot replaced by a device copy of the input, so the caller rebuilds its
+// cache from these inputs. One compare kernel per item, one stream sync in all.
 struct SnapItem {
   const char* name;
   const uint64_t* p;
   uint64_t words;
 };
-int snapshot_check(pbf_ctx* ctx, const SnapItem* items, int k, hipStream_t s, bool* same);
+int snapshot_check(pbf_ctx* ctx, const char* consumer, const SnapItem* items, int k, hipStream_t s, bool* same);
 // canonical affine (x, y as 4 + 4 little-endian u64; identity (0, 0)) of an XYZZ point
 void xyzz_to_affine_u64(const Xyzz& p, uint64_t* out);
 

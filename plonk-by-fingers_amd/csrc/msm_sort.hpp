@@ -187,6 +187,10 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
     const uint32_t before = __popcll(peers & below);
     rank[r] = wc[wave][d] + before;  // this wave's earlier entries of digit d, then this round's
     if (valid && before == 0) wc[wave][d] += __popcll(peers);
+    // the next round's lanes read counters this round's leader lanes wrote: order the LDS
+    // accesses across lanes explicitly (wavefront-scope fence + scheduling barrier)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   // wc[w][d] -> exclusive prefix over the waves (thread t owns digit t)

@@ -324,31 +324,7 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   }
   // regrouped 2^24 plan (default for 8,8,8 standard-root plans; PBF_NTT_NO_RG=1 restores the
   // round-2 passes): three twiddle layers of order 4096, 2^18 and 2^24
-  if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && !getenv("PBF_NTT_NO_RG")) {
-    const uint64_t w4096 = hpow(w, n / 4096, m);
-    std::vector<uint64_t> tc1(4096);
-    for (uint64_t a2l = 0; a2l < 16; ++a2l)
-      for (uint64_t r2 = 0; r2 < 4; ++r2)
-        for (uint64_t k1 = 0; k1 < 64; ++k1)
-          tc1[a2l * 256 + r2 * 64 + k1] = hpow(w4096, ((a2l + 16 * r2) * k1) % 4096, m);
-    std::vector<uint64_t> t2(1ull << 18);
-    for (uint64_t a1 = 0; a1 < 64; ++a1) {
-      const uint64_t st = hpow(w, 64 * a1, m);
-      uint64_t y = 1;
-      for (uint64_t K = 0; K < 4096; ++K) { t2[(a1 << 12) + K] = y; y = hmul(y, st, m); }
-    }
-    std::vector<uint64_t> t3(1ull << 24);
-    const uint64_t scale = inverse ? p->n_inv : 1;
-    for (uint64_t fq = 0; fq < 4; ++fq)
-      for (uint64_t a0 = 0; a0 < 64; ++a0) {
-        const uint64_t st = hpow(w, a0, m);
-        uint64_t y = hmul(hpow(w, (65536 * a0 * fq) % n, m), scale, m);
-        uint64_t* row = t3.data() + ((fq * 64 + a0) << 16);
-        for (uint64_t j = 0; j < 65536; ++j) { row[j] = y; y = hmul(y, st, m); }
-      }
-    if ((rc = upload(p->rg_tc1, tc1)) || (rc = upload(p->rg_t2, t2)) || (rc = upload(p->rg_t3, t3))) return rc;
-    p->rg = true;
-  }
+  if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && !getenv("PBF_NTT_NO_RG")) p->rg = true;
   // round-3 in-place schedule: opt-in (PBF_NTT_IP=1) while it measures slower than the
   // round-2 Stockham plan
   if (p->gl && getenv("PBF_NTT_IP") && !getenv("PBF_NTT_V2")) {
@@ -685,6 +661,41 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   return 0;
 }
 
+// The regrouped plan's twiddle tables, built on the first run that takes the regrouped path:
+// tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18), t3[f][a0][j] (2^24, n^-1 folded in for the inverse)
+static int ensure_rg_tables(const NttPlan& p) {
+  if (p.rg_built) return 0;
+  const uint64_t m = p.m, n = p.n;
+  const int inverse = p.inverse;
+  uint64_t w = p.omega;  // the transform's root: omega, or omega^-1 for the inverse (make_plan)
+  if (inverse && !hinv(p.omega, m, &w)) return fail(1, "omega not invertible");
+  int rc;
+  const uint64_t w4096 = hpow(w, n / 4096, m);
+  std::vector<uint64_t> tc1(4096);
+  for (uint64_t a2l = 0; a2l < 16; ++a2l)
+    for (uint64_t r2 = 0; r2 < 4; ++r2)
+      for (uint64_t k1 = 0; k1 < 64; ++k1)
+        tc1[a2l * 256 + r2 * 64 + k1] = hpow(w4096, ((a2l + 16 * r2) * k1) % 4096, m);
+  std::vector<uint64_t> t2(1ull << 18);
+  for (uint64_t a1 = 0; a1 < 64; ++a1) {
+    const uint64_t st = hpow(w, 64 * a1, m);
+    uint64_t y = 1;
+    for (uint64_t K = 0; K < 4096; ++K) { t2[(a1 << 12) + K] = y; y = hmul(y, st, m); }
+  }
+  std::vector<uint64_t> t3(1ull << 24);
+  const uint64_t scale = inverse ? p.n_inv : 1;
+  for (uint64_t fq = 0; fq < 4; ++fq)
+    for (uint64_t a0 = 0; a0 < 64; ++a0) {
+      const uint64_t st = hpow(w, a0, m);
+      uint64_t y = hmul(hpow(w, (65536 * a0 * fq) % n, m), scale, m);
+      uint64_t* row = t3.data() + ((fq * 64 + a0) << 16);
+      for (uint64_t j = 0; j < 65536; ++j) { row[j] = y; y = hmul(y, st, m); }
+    }
+  if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_t3, t3))) return rc;
+  p.rg_built = true;
+  return 0;
+}
+
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff) {
   const size_t P = p.logr.size();
@@ -703,6 +714,10 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
   }
   const bool rg = p.rg && P == 3 && split_log == 0 && !blk && gl_pad(p) == 0 && !getenv("PBF_NTT_PERSIST") &&
                   gl_tile(8) == 4096;
+  if (rg) {
+    const int rc = ensure_rg_tables(p);
+    if (rc) return rc;
+  }
   uint32_t log_ns = 0;
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];

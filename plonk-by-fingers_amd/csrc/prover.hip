@@ -869,9 +869,9 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* pkcoset = nullptr;
   std::vector<uint64_t> pk_key;
   if (pk_on) {
-    const SnapItem items[2] = {{"pk.q", d_q, 20 * (uint64_t)n}, {"pk.copies", d_copies, 6 * (uint64_t)n}};
+    const SnapItem items[2] = {{"q", d_q, 20 * (uint64_t)n}, {"copies", d_copies, 6 * (uint64_t)n}};
     bool same = false;
-    if ((rc = snapshot_check(ctx, items, 2, s, &same))) return rc;
+    if ((rc = snapshot_check(ctx, "pk", items, 2, s, &same))) return rc;
     if (!same) ctx->pk_key.clear();
     pk_key = {(uint64_t)n, (uint64_t)P.G, (uint64_t)P.rank};
     for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
@@ -1328,11 +1328,11 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   std::vector<uint64_t> vk_key;
   const bool vk_on = !getenv("PBF_VERIFIER_NO_VK");
   if (vk_on) {
-    const SnapItem items[3] = {{"vk.q", d_q, 20 * (uint64_t)n},
-                               {"vk.copies", d_copies, 6 * (uint64_t)n},
-                               {"vk.srs", d_srs, 8 * (uint64_t)srs_m}};
+    const SnapItem items[3] = {{"q", d_q, 20 * (uint64_t)n},
+                               {"copies", d_copies, 6 * (uint64_t)n},
+                               {"g1pts", d_srs, 8 * (uint64_t)srs_m}};
     bool same = false;
-    if ((rc = snapshot_check(ctx, items, 3, s, &same))) return rc;
+    if ((rc = snapshot_check(ctx, "vk", items, 3, s, &same))) return rc;
     if (!same) ctx->vk_key.clear();  // rebuilt below; valid again once complete
     vk_key = {(uint64_t)n, (uint64_t)srs_m};
     for (int i = 0; i < 8; ++i) vk_key.push_back(k1k2[i]);

@@ -29,6 +29,16 @@ import torch
 GOLD = 0xFFFFFFFF00000001
 
 
+def _stream_ctx(stream_ptr, like: torch.Tensor):
+    """torch.cuda.stream(stream_ptr) for device tensors (0: the device's default stream);
+    a no-op for host tensors (the gloo tests' CPU ops)."""
+    if not like.is_cuda or stream_ptr is None:
+        return contextlib.nullcontext()
+    st = (torch.cuda.ExternalStream(stream_ptr, device=like.device) if stream_ptr
+          else torch.cuda.default_stream(like.device))
+    return torch.cuda.stream(st)
+
+
 class GpuShardOps:
     """The HIP kernels of libpbf.so, enqueued on `stream` (torch's stream): u64 elements
     (Goldilocks or a 32-bit modulus), one int64 word each."""
@@ -91,6 +101,13 @@ class ShardedNtt:
             chunks -= 1
         self.chunks = max(1, chunks)
 
+    def _on_ops_stream(self):
+        """Issue (and wait for) the exchanges on the stream the kernels are enqueued on
+        (ops.stream), not on torch's current stream: torch.distributed (RCCL), LocalComm's
+        copies and DistComm's host staging all order against the CURRENT stream, so make
+        ops.stream current while they are issued (the ShardedProver callbacks do the same)."""
+        return _stream_ctx(getattr(self.ops, "stream", None), self.send)
+
     def _exchange(self, c: int):
         # equal splits along dim 0 of group c's slice: part r of `send` goes to rank r, part g
         # of `recv` came from rank g (layout [peer][polynomial of the group][kk])
@@ -102,16 +119,19 @@ class ShardedNtt:
         return slice(c * L, (c + 1) * L)
 
     def _pipeline(self, first, second):
-        """first(c) produces send[c]; the exchange fills recv[c]; second(c) consumes it."""
+        """first(c) produces send[c]; the exchange fills recv[c]; second(c) consumes it. Every
+        collective is issued and waited for on ops.stream (work.wait() orders the stream that
+        is current when it is called)."""
         works = []
-        for c in range(self.chunks):
-            first(c)
-            works.append(self._exchange(c))
-            if c >= 1:
-                works[c - 1].wait()
-                second(c - 1)
-        works[-1].wait()
-        second(self.chunks - 1)
+        with self._on_ops_stream():
+            for c in range(self.chunks):
+                first(c)
+                works.append(self._exchange(c))
+                if c >= 1:
+                    works[c - 1].wait()
+                    second(c - 1)
+            works[-1].wait()
+            second(self.chunks - 1)
 
     def forward(self, shard: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """shard[b][m] = a_b[rank + world*m]  ->  out[b][q*S + kk] = X_b[q*nl + rank*S + kk]."""
@@ -160,11 +180,13 @@ class ShardedMulNtt:
 
     def mul(self, a_shard: torch.Tensor, b_shard: torch.Tensor, c_shard: torch.Tensor) -> torch.Tensor:
         L = self.nl * self.words
-        pair = torch.cat([a_shard.reshape(-1), b_shard.reshape(-1)])
-        self.fwd.forward(pair, self.spec)
-        prod = torch.empty(L, dtype=torch.int64, device=self.spec.device)
-        self.ops.pointwise(self.modulus, self.spec[:L], self.spec[L:], prod, self.nl)
-        return self.inv.inverse(prod, c_shard)
+        # the concatenation and the allocations are stream-ordered too: ops.stream, like the kernels
+        with _stream_ctx(getattr(self.ops, "stream", None), self.spec):
+            pair = torch.cat([a_shard.reshape(-1), b_shard.reshape(-1)])
+            self.fwd.forward(pair, self.spec)
+            prod = torch.empty(L, dtype=torch.int64, device=self.spec.device)
+            self.ops.pointwise(self.modulus, self.spec[:L], self.spec[L:], prod, self.nl)
+            return self.inv.inverse(prod, c_shard)
 
 
 class BenchSharded:

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
     ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("pbf_msm_g1_bn254_fixed_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, _p64, _vp]),
+    ("pbf_msm_g1_bn254_fixed_range_dev", ctypes.c_int, [_vp, _vp, _sz, _sz, _vp, _sz, _p64, _vp]),
     ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
     ("pbf_pairing_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
     ("pbf_pairing_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
@@ -302,6 +303,15 @@ class Context:
         out = np.zeros(8, dtype=np.uint64)
         _check(self.lib.pbf_msm_g1_bn254_fixed_dev(self.h, _vp(d_points), n_points, _vp(d_scalars), n, _ptr(out),
                                                    _vp(stream) if stream else None))
+        v = limbs_to_ints(out)
+        return v[0], v[1]
+
+    def msm_g1_fixed_range_dev(self, d_points: int, n_points: int, first: int, d_scalars: int, n: int,
+                               stream: int = 0) -> tuple:
+        """sum_{i<n} s_i P_(first+i) against the fixed base set (one rank's point range)."""
+        out = np.zeros(8, dtype=np.uint64)
+        _check(self.lib.pbf_msm_g1_bn254_fixed_range_dev(self.h, _vp(d_points), n_points, first, _vp(d_scalars), n,
+                                                         _ptr(out), _vp(stream) if stream else None))
         v = limbs_to_ints(out)
         return v[0], v[1]
 

@@ -206,12 +206,13 @@ def test_fixed_base_msm_edges_and_cache(ctx):
     assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), dz.data_ptr(), len(pts)) == (0, 0)
 
 
-@pytest.mark.parametrize("n_points,n", [(300, 17), (300, 300), (70001, 70001), (70001, 69000)])
+@pytest.mark.parametrize("n_points,n", [(300, 255), (300, 256), (300, 300), (70001, 70001), (70001, 69000)])
 def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n):
     """The MSM sorts' first pass from 16-bit digit codes (msm_sort.hpp RsDigits; fixed-base and
-    windowed forms; the default) gives the same result as the (key, value) pair sort (=0), including tiles that straddle
-    two windows (n not a multiple of the 8192-entry tile); the prover's sharded commits
-    (first point != 0) are covered by the virtual-rank prover tests."""
+    windowed forms; the default) gives the same result as the (key, value) pair sort (=0),
+    including tiles that straddle two windows (n not a multiple of the 8192-entry tile).
+    n = 255 is just below the digit-code path's minimum (rs_dig_ok: n >= 256), so both settings
+    take the pair sort there; n = 256 is the smallest digit-code case."""
     rnd = random.Random(n_points + n)
     base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(32)]
     pts = (base * (n_points // len(base) + 1))[:n_points]
@@ -227,6 +228,30 @@ def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n
     assert res["1"] == res["0"] == res["w1"] == res["w0"]
     if n <= 300:
         assert res["1"] == enc(bn254.msm_naive(pts[:n], sc))
+
+
+@pytest.mark.parametrize("n_points,first,n", [(1000, 300, 256), (1000, 1, 999), (70001, 8193, 40000), (600, 599, 1)])
+def test_fixed_base_range_first_nonzero(ctx, monkeypatch, n_points, first, n):
+    """pbf_msm_g1_bn254_fixed_range_dev: scalars against points [first, first + n) of the fixed
+    base set -- the value encoding w * n_table + first + i of the digit-code sort with first > 0
+    (a sharded commitment's point range) -- equals the pair sort's result and the naive sum."""
+    rnd = random.Random(n_points * 7 + first)
+    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(37)]
+    pts = (base * (n_points // len(base) + 1))[:n_points]
+    sc = [rnd.randrange(R) for _ in range(n)]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
+        res[fused] = ctx.msm_g1_fixed_range_dev(dp.data_ptr(), n_points, first, ds.data_ptr(), n)
+    assert res["1"] == res["0"]
+    # the same range as a plain MSM over the sliced points (windowed path, no table)
+    dsl = _dev_points(pts[first:first + n])
+    assert res["1"] == ctx.msm_g1_dev(dsl.data_ptr(), ds.data_ptr(), n)
+    if n <= 1000:
+        assert res["1"] == enc(bn254.msm_naive(pts[first:first + n], sc))
+    with pytest.raises(pbf.PbfError):
+        ctx.msm_g1_fixed_range_dev(dp.data_ptr(), n_points, first, ds.data_ptr(), n_points - first + 1)
 
 
 def test_fixed_base_msm_2p20_discrete_log(ctx):

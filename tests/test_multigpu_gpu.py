@@ -235,3 +235,90 @@ def test_sharded_mul_ntt_virtual_ranks(field, G, nl):
     assert not errs, errs
     for r in range(G):
         assert out[r] == list(ref[r::G]), (field, G, r)
+
+
+@pytest.mark.parametrize("G,field", [(2, "gold"), (4, "gold"), (4, "fr")])
+def test_sharded_ntt_on_a_non_current_stream(G, field):
+    """multigpu.ShardedNtt / ShardedMulNtt issue their collectives on ops.stream, the stream the
+    kernels go to, whatever torch's current stream is. Each virtual rank runs on stream A
+    (delayed behind a queue of matmuls) while torch's current stream is B: an exchange ordered
+    on B would copy `send` before the local NTT on A wrote it."""
+    import threading
+
+    import bn254
+    from multigpu import GpuFrShardOps, GpuShardOps, LocalComm, LocalGroup, ShardedMulNtt, ShardedNtt
+
+    nl, batch = 1 << 12, 4
+    N = G * nl
+    if field == "gold":
+        M, w, Ops = GOLD, pow(7, (GOLD - 1) // N, GOLD), GpuShardOps
+        glob = np.stack([oracle.splitmix_field(GOLD, 4400 + b, N) for b in range(batch)])
+        ref = np.stack([oracle.ntt_iter(GOLD, w, glob[b]) for b in range(batch)])
+        enc = lambda v: torch.from_numpy(np.ascontiguousarray(v).reshape(-1).view(np.int64)).cuda()  # noqa: E731
+        shard_of = lambda g: enc(glob[:, g::G])  # noqa: E731
+    else:
+        M, w, Ops = bn254.R, bn254.root_of_unity(N), GpuFrShardOps
+        glob = [_fr_rand(N, 4500 + b) for b in range(batch)]
+        ctx0 = pbf.default_context()
+        ref = [ctx0.ntt_fr(w, g) for g in glob]
+        enc = lambda v: torch.from_numpy(bn254.ints_to_limbs(list(v)).view(np.int64)).cuda()  # noqa: E731
+        shard_of = lambda g: enc([x for b in range(batch) for x in glob[b][g::G]])  # noqa: E731
+    group = LocalGroup(G)
+    out, prods, errs = [None] * G, [None] * G, []
+
+    def rank_main(r):
+        try:
+            c = pbf.Context(0)
+            lib_stream, cur_stream = torch.cuda.Stream(), torch.cuda.Stream()
+            shard = shard_of(r)
+            x = torch.randn(2048, 2048, device="cuda")
+            torch.cuda.synchronize()
+            with torch.cuda.stream(lib_stream):
+                for _ in range(40):  # delays everything enqueued on lib_stream after it
+                    x = x @ x
+                    x = x / x.norm()
+            with torch.cuda.stream(cur_stream):
+                ops = Ops(c, lib_stream.cuda_stream)
+                nt = ShardedNtt(ops, LocalComm(group, r), r, G, nl, batch, modulus=M, omega=w, chunks=2)
+                res = torch.empty_like(shard)
+                nt.forward(shard, res)
+                sm = ShardedMulNtt(ops, LocalComm(group, r), r, G, nl, modulus=M, omega=w)
+                L = nl * Ops.words
+                prod = torch.empty(L, dtype=torch.int64, device="cuda")
+                sm.mul(shard[:L], shard[L:2 * L], prod)
+            lib_stream.synchronize()
+            out[r] = res.cpu().numpy().view(np.uint64)
+            prods[r] = prod.cpu().numpy().view(np.uint64)
+            c.close()
+        except Exception as e:  # reported by the main thread
+            errs.append(f"rank {r}: {e!r}")
+            group.barrier.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "rank hung"
+    assert not errs, errs
+    for r in range(G):
+        idx = ShardedNtt.output_indices(r, G, nl)
+        if field == "gold":
+            got = out[r].reshape(batch, nl)
+            assert np.array_equal(got, ref[:, idx]), (G, r)
+        else:
+            got = bn254.limbs_to_ints(out[r])
+            for b in range(batch):
+                assert got[b * nl:(b + 1) * nl] == [ref[b][i] for i in idx], (G, r, b)
+    # the product shards: mul_ntt of polynomials 0 and 1 (whole vectors), stride-sharded
+    if field == "gold":
+        spec = (ref[0].astype(object) * ref[1].astype(object)) % GOLD
+        prod_ref = [int(v) for v in oracle.ntt_iter(GOLD, w, np.asarray(spec, dtype=np.uint64), inverse=True)]
+        for r in range(G):
+            assert [int(v) for v in prods[r]] == prod_ref[r::G], (G, r)
+    else:
+        R = bn254.R
+        spec = [x * y % R for x, y in zip(ref[0], ref[1])]
+        prod_ref = pbf.default_context().ntt_fr(w, spec, inverse=True)
+        for r in range(G):
+            assert bn254.limbs_to_ints(prods[r]) == prod_ref[r::G], (G, r)

@@ -1,7 +1,12 @@
 """GPU parity of the BN254-Fr NTT and mul_ntt (BASELINE config 3) vs the Python
 big-integer oracle (oracle/bn254.py): exact at small and medium sizes, and at the
-config-3 size (a, b of 2^22 coefficients, NTT size 2^23) through size-independent
-properties (round trip, evaluation identity c(x) = a(x) b(x) at random points)."""
+config-3 size (a, b of 2^22 coefficients, NTT size 2^23) exactly too, through the SHA-256
+of the whole product that the recursion-faithful C++ oracle computed in the container
+(tests/golden/config3_mul_ntt.json, tests/golden/gen_config3_digest.py), plus
+size-independent properties (round trip, evaluation identity c(x) = a(x) b(x))."""
+import hashlib
+import json
+import os
 import random
 
 import numpy as np
@@ -80,7 +85,15 @@ def test_mul_ntt_config3_size_evaluation_identity(ctx):
     ctx.mul_ntt_fr_dev(w, da.data_ptr(), db.data_ptr(), dc.data_ptr(), n, 1,
                        stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    c = bn254.limbs_to_ints(dc.cpu().numpy().view(np.uint64))
+    host = dc.cpu().numpy().view(np.uint64)
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config3_mul_ntt.json")) as fh:
+        gold = json.load(fh)
+    assert (gold["la"], gold["lb"], gold["seeds"]) == (la, la, [301, 302])
+    # exact parity of all 2^23 product coefficients with oracle_fr_mul_ntt (fft.rs:109-132)
+    assert hashlib.sha256(host.astype("<u8").tobytes()).hexdigest() == gold["sha256_le_u64"]
+    c = bn254.limbs_to_ints(host)
+    for i, v in gold["samples"].items():
+        assert c[int(i)] == int(v)
     ai, bi = bn254.limbs_to_ints(a), bn254.limbs_to_ints(b)
     assert c[-1] == 0  # deg(a*b) = 2^23 - 2
     for x in (3, 123456789123456789):

@@ -177,3 +177,47 @@ def test_verification_key_cache(ctx, monkeypatch):
     cold = answers()
     assert warm == cold, (warm, cold)
     assert warm == [True, False, False, True, True, False, True], warm
+
+
+def test_shared_snapshots_across_caches(ctx):
+    """The proving key, the verification key and the MSM window table validate against ONE
+    device copy per input (q, copies, the SRS points; ADVICE r03: no duplicate copies). A cache
+    must still be rebuilt when ANOTHER consumer replaced the shared copy: interleave prove /
+    verify over two circuits and two SRSs with stand-alone fixed-base MSMs over other points,
+    and every answer equals the cold one."""
+    import numpy as np
+    import torch
+
+    import bn254
+
+    rng = random.Random(31337)
+    n = 64
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    s1, s2 = 1111, 2222
+    srs1, srs2 = ctx.srs_create(s1, n + 3), ctx.srs_create(s2, n + 3)
+    g2 = {s: [B.G2_GEN, ctx.g2_bn254_mul([B.G2_GEN], [s])[0]] for s in (s1, s2)}
+    A, Bc = P.mul_gates_circuit(n, 51), P.mul_gates_circuit(n, 52)
+    other = [bn254.g1_mul(bn254.G1_GEN, 5 + i) for i in range(n + 3)]  # same count as the SRS
+    sc = [rng.randrange(P.R) for _ in range(n + 3)]
+    dp = torch.from_numpy(bn254.ints_to_limbs([v for p in other for v in p]).view(np.int64)).cuda()
+    ds = torch.from_numpy(bn254.ints_to_limbs(sc).view(np.int64)).cuda()
+    msm_ref = bn254.msm_naive(other, sc)
+
+    def msm():
+        assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n + 3, ds.data_ptr(), n + 3) == msm_ref
+
+    pa1 = ctx.plonk_prove_bn254(*A, chal, rnd, srs1, mode=1)
+    ver = lambda circ, srs, s, pr: ctx.plonk_verify_bn254(circ[0], circ[1], srs, g2[s], pr[0], pr[1], chal, 5,  # noqa
+                                                          mode=1)
+    assert ver(A, srs1, s1, pa1)
+    msm()                                                       # g1pts <- other points
+    assert ctx.plonk_prove_bn254(*A, chal, rnd, srs1, mode=1) == pa1
+    pb2 = ctx.plonk_prove_bn254(*Bc, chal, rnd, srs2, mode=1)   # q, copies <- B; g1pts <- srs2
+    assert ver(A, srs1, s1, pa1)                                # vk rebuilt for A / srs1
+    assert not ver(A, srs1, s1, pb2)
+    msm()
+    assert ver(Bc, srs2, s2, pb2)
+    assert ctx.plonk_prove_bn254(*A, chal, rnd, srs1, mode=1) == pa1
+    msm()
+    assert ctx.plonk_prove_bn254(*Bc, chal, rnd, srs2, mode=1) == pb2
