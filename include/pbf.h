@@ -253,17 +253,22 @@ int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, cons
 /* Config 5 across G GPUs ("NTT sharded across 8xMI355X"): one process (or thread) per GPU
  * calls pbf_plonk_prove_bn254_sharded_dev with the same inputs (circuit, SRS, challenges,
  * blinders) and its rank. The library computes nothing collective itself: it calls back
- * into the caller's communicator (RCCL via torch.distributed in multigpu.py), always for
- * buffers it names in `comm` and stream-ordered on `stream`:
+ * into the caller's communicator (RCCL via torch.distributed in multigpu.py, or the library's
+ * own in pbf_plonk_prove_bn254_multi), always for buffers it names in `comm` and
+ * stream-ordered on `stream`:
  *   all_to_all(user, b, stream):  send[g*b .. (g+1)*b) goes to rank g, recv[g*b ..) comes from g
  *   all_gather(user, b, stream):  send[0 .. b) of rank g lands in recv[g*b .. (g+1)*b)
- * Work split: the 14 coset NTTs of size 4n of round 3 and the 4n-point
- * transforms of round 5 run as stride-sharded NTTs (one all-to-all each way), the quotient
- * and the opening divisions on this rank's evaluation blocks, t / W_z / W_zw coefficients
- * are all-gathered; every commitment is a point-range MSM whose partial sums are
- * all-gathered (64 B per rank); the O(n) steps (interpolation, accumulator, evaluations) are
- * replicated. Outputs are identical on every rank and bit-identical to the single-GPU
- * proof. send / recv: device buffers of `capacity` >= 16 * (4n / world) * 32 bytes each.   */
+ * Work split, every witness-dependent step on this rank's share: satisfies and
+ * the accumulator's terms / prefix products on rows [r n/G, (r+1) n/G) (the ranks' products
+ * all-gathered); interpolation of a b c and of the accumulator as sharded INTTs; every coset NTT
+ * of size 4n and the coset INTT of t as stride-sharded transforms; the quotient on this rank's
+ * evaluation blocks; commitments, evaluations, r(x) and the opening divisions on this rank's
+ * contiguous coefficient range (one all-to-all transposes the NTTs' stride shards into it; the
+ * divisions' and evaluations' per-range totals are all-gathered); every commitment is this
+ * rank's point range, the partial sums all-gathered once at the end. The circuit's proving key
+ * is built once per circuit on every rank. Outputs are identical on every rank and
+ * bit-identical to the single-GPU proof. n >= world^2. send / recv: device buffers of
+ * `capacity` >= 9 * (4n / world) * 32 bytes each.                                          */
 typedef struct pbf_comm {
   uint32_t world, rank;
   void* user;
@@ -277,6 +282,49 @@ int pbf_plonk_prove_bn254_sharded_dev(pbf_ctx* ctx, const pbf_comm* comm, size_t
                                       const uint64_t* d_copies, const uint64_t* d_abc, const uint64_t* chal,
                                       const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* d_srs,
                                       size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f, void* stream);
+
+/* ---- multi-GPU from ONE host process (SURVEY.md §8b pbf_ntt_u64_multi) -------------------
+ * `ctxs` = G contexts (G = 2, 4, 8), rank g = ctxs[g]. The library owns the exchange: on G
+ * distinct devices it uses RCCL (librccl loaded at run time; ncclCommInitAll, grouped
+ * ncclSend / ncclRecv for the all-to-all, ncclAllGather), on one shared device (virtual ranks)
+ * stream-ordered device copies ordered by events. The communicator and its buffers are kept
+ * per context list (pointers and creation order) until a member context is destroyed. Each
+ * rank runs in a library-owned host thread; errors name the failing rank. Outputs are
+ * bit-identical to the single-GPU entry points.
+ *
+ * pbf_ntt_u64_multi: CooleyTurkey::fft / fft_inv (fft.rs:66-78) of one host vector of n points
+ *   (n = G * nl, nl a power of two >= G), natural order in and out, with the top log2(G) levels of
+ *   the recursion (fft.rs:94-96) across the ranks: the stride shards go to the G devices, one
+ *   all-to-all, the blocks come back (pbf_ntt_shard_local_dev / _combine_dev, one rank each).
+ * _dev: per-rank device buffers and streams: d_in[g] = rank g's stride shards [batch][nl]
+ *   (forward) or blocks (inverse), d_out[g] likewise the other way round (streams may be NULL).
+ * pbf_mul_ntt_*_multi: mul_ntt (fft.rs:109-132), la + lb = G * nl; out has la + lb entries.
+ * pbf_plonk_prove_bn254_multi: Plonk::prove (plonk.rs:191-466) with the work split of
+ *   pbf_plonk_prove_bn254_sharded_dev, the host inputs uploaded to every rank's device; _dev
+ *   takes per-rank device copies (d_q[g] ... on rank g's device) and streams. The ranks'
+ *   proofs are compared (PBF_ECOMM if they differ) and returned once.
+ * pbf_multi_backend: *backend = 0 (device copies, one device) or 1 (RCCL).                   */
+int pbf_ntt_u64_multi(pbf_ctx* const* ctxs, uint32_t world, uint64_t modulus, uint64_t omega, const uint64_t* in,
+                      uint64_t* out, size_t n, int inverse);
+int pbf_ntt_u64_multi_dev(pbf_ctx* const* ctxs, uint32_t world, uint64_t modulus, uint64_t omega,
+                          const uint64_t* const* d_in, uint64_t* const* d_out, size_t nl, size_t batch, int inverse,
+                          void* const* streams);
+int pbf_ntt_fr256_multi(pbf_ctx* const* ctxs, uint32_t world, const uint64_t* omega, const uint64_t* in, uint64_t* out,
+                        size_t n, int inverse);
+int pbf_ntt_fr256_multi_dev(pbf_ctx* const* ctxs, uint32_t world, const uint64_t* omega, const uint64_t* const* d_in,
+                            uint64_t* const* d_out, size_t nl, size_t batch, int inverse, void* const* streams);
+int pbf_mul_ntt_u64_multi(pbf_ctx* const* ctxs, uint32_t world, uint64_t modulus, uint64_t omega, const uint64_t* a,
+                          size_t la, const uint64_t* b, size_t lb, uint64_t* out);
+int pbf_mul_ntt_fr256_multi(pbf_ctx* const* ctxs, uint32_t world, const uint64_t* omega, const uint64_t* a, size_t la,
+                            const uint64_t* b, size_t lb, uint64_t* out);
+int pbf_plonk_prove_bn254_multi(pbf_ctx* const* ctxs, uint32_t world, size_t n, const uint64_t* q, const uint64_t* copies,
+                                const uint64_t* abc, const uint64_t* chal, const uint64_t* rnd, const uint64_t* k1k2,
+                                const uint64_t* srs, size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f);
+int pbf_plonk_prove_bn254_multi_dev(pbf_ctx* const* ctxs, uint32_t world, size_t n, const uint64_t* const* d_q,
+                                    const uint64_t* const* d_copies, const uint64_t* const* d_abc, const uint64_t* chal,
+                                    const uint64_t* rnd, const uint64_t* k1k2, const uint64_t* const* d_srs,
+                                    size_t srs_m, int mode, uint64_t* out_pts, uint64_t* out_f, void* const* streams);
+int pbf_multi_backend(pbf_ctx* const* ctxs, uint32_t world, int* backend);
 
 /* synthetic config-5 circuit on the device (bench / tests): every gate a*b = c, a, b
  * uniform (splitmix64 of seed), every 4th gate's c copied into the next gate's a       */

@@ -1,5 +1,6 @@
 // C-ABI entry points of libpbf.so (include/pbf.h). Each cites the reference
 // function it replaces (paths relative to the adria0/plonk-by-fingers root).
+#include <atomic>
 #include <cstring>
 #include "../../include/pbf.h"
 #include "internal.hpp"
@@ -21,6 +22,7 @@ static bool all_canonical(const uint64_t* v, size_t n, uint64_t m) {
 using namespace pbf;
 void pbf_internal_drop_plans256(const void* ctx);  // ntt256.hip
 void pbf_internal_drop_tl256(const void* ctx);     // ntt256.hip
+void pbf_internal_forget_ctx(const pbf_ctx* ctx);  // group.hip
 
 int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan** out) {
   auto key = std::make_tuple(m, omega, n, inverse ? 1 : 0);
@@ -70,6 +72,8 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
   if (device < 0 || device >= count) return fail(PBF_EINVAL, "device index out of range");
   PBF_HIP(hipSetDevice(device));
   pbf_ctx* c = new pbf_ctx();
+  static std::atomic<uint64_t> next_serial{1};
+  c->serial = next_serial++;
   c->device = device;
   c->fork.device = device;
   c->msm_tail.device = device;
@@ -84,6 +88,7 @@ int pbf_ctx_create(int device, pbf_ctx** out) {
 
 void pbf_ctx_destroy(pbf_ctx* ctx) {
   if (!ctx) return;
+  pbf_internal_forget_ctx(ctx);  // multi-GPU groups with this member (group.hip)
   pbf_internal_drop_plans256(ctx);
   pbf_internal_drop_tl256(ctx);
   (void)hipSetDevice(ctx->device);

@@ -163,6 +163,7 @@ int pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2
 
 struct pbf_ctx {
   int device = 0;
+  uint64_t serial = 0;  // creation order (multi-GPU groups match contexts by pointer and serial)
   hipStream_t stream = nullptr;
   hipStream_t user_stream = nullptr;
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, int>, std::unique_ptr<pbf::NttPlan>> plans;

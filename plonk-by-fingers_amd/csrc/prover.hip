@@ -145,11 +145,14 @@ __global__ void k_powers(uint64_t* out, uint64_t count, U256 base, U256 start) {
 }
 
 // copy_constraints_to_roots (plonk.rs:181-189): sigma[col][i] = {w^j, k1 w^j, k2 w^j}[kind]
-__global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n, U256 k1, U256 k2, uint64_t* sigma,
-                        int* bad) {
-  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= 3 * n) return;
-  const uint64_t kind = copies[2 * id], idx = copies[2 * id + 1];
+// Rows [row0, row0 + rows) of every column; sigma[col][i - row0] (the whole table: 0, n)
+__global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n, uint64_t row0, uint64_t rows, U256 k1,
+                        U256 k2, uint64_t* sigma, int* bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * rows) return;
+  const uint64_t col = t / rows, id = t;
+  const uint64_t src = col * n + row0 + t % rows;
+  const uint64_t kind = copies[2 * src], idx = copies[2 * src + 1];
   if (kind > 2 || idx < 1 || idx > n) {
     *bad = 1;
     for (int k = 0; k < 4; ++k) sigma[4 * id + k] = 0;
@@ -162,9 +165,11 @@ __global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n
 }
 
 // Constrains::satisfies (constraints.rs:198-230, with its q_l * b term): gates and copies
-__global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64_t* copies, uint64_t n, int* bad) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64_t* copies, uint64_t n, uint64_t row0,
+                            uint64_t rows, int* bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows) return;
+  const uint64_t i = row0 + t;
   // every term at R-degree -1 (the zero test does not depend on the degree): canonical
   // products of two canonical values; q_m lifted to degree 1, q_c lowered to -1
   auto ld = [](const uint64_t* p) { return u256_from_u64(p); };
@@ -189,10 +194,14 @@ __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64
 // Conversion-free (R-degrees as in QuotArgs): canonical a b c w sigma, beta k1 k2 in
 // Montgomery form (degree 1), gamma0 canonical: each factor lands at degree 0, each
 // three-factor product at degree -2 -- num and den alike, and k_div_batch takes them so.
-__global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n, U256 beta,
-                             U256 gamma0, U256 k1, U256 k2, uint64_t* num, uint64_t* den) {
-  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j + 1 >= n) return;
+// Rows j = row0 + t, t < rows (and j < n - 1): num[t], den[t]; sigma as k_sigma wrote it for
+// the same rows (column stride `rows`)
+__global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const uint64_t* sigma, const uint64_t* hpow, uint64_t n,
+                                                    uint64_t row0, uint64_t rows, U256 beta, U256 gamma0, U256 k1, U256 k2,
+                                                    uint64_t* num, uint64_t* den) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t j = row0 + t;
+  if (t >= rows || j + 1 >= n) return;
   auto ld = [](const uint64_t* p) { return u256_from_u64(p); };
   const U256 a = ld(abc + 4 * j), b = ld(abc + 4 * (n + j)), c = ld(abc + 4 * (2 * n + j));
   const U256 w = ld(hpow + 4 * j);
@@ -200,11 +209,11 @@ __global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const u
   U256 d1 = Fr::add(Fr::add(a, bw), gamma0);
   U256 d2 = Fr::add(Fr::add(b, Fr::mul_tp(bw, k1)), gamma0);
   U256 d3 = Fr::add(Fr::add(c, Fr::mul_tp(bw, k2)), gamma0);
-  u256_to_u64(Fr::mul_tp(Fr::mul_tp(d1, d2), d3), num + 4 * j);
-  U256 e1 = Fr::add(Fr::add(a, Fr::mul_tp(beta, ld(sigma + 4 * j))), gamma0);
-  U256 e2 = Fr::add(Fr::add(b, Fr::mul_tp(beta, ld(sigma + 4 * (n + j)))), gamma0);
-  U256 e3 = Fr::add(Fr::add(c, Fr::mul_tp(beta, ld(sigma + 4 * (2 * n + j)))), gamma0);
-  u256_to_u64(Fr::mul_tp(Fr::mul_tp(e1, e2), e3), den + 4 * j);
+  u256_to_u64(Fr::mul_tp(Fr::mul_tp(d1, d2), d3), num + 4 * t);
+  U256 e1 = Fr::add(Fr::add(a, Fr::mul_tp(beta, ld(sigma + 4 * t))), gamma0);
+  U256 e2 = Fr::add(Fr::add(b, Fr::mul_tp(beta, ld(sigma + 4 * (rows + t)))), gamma0);
+  U256 e3 = Fr::add(Fr::add(c, Fr::mul_tp(beta, ld(sigma + 4 * (2 * rows + t)))), gamma0);
+  u256_to_u64(Fr::mul_tp(Fr::mul_tp(e1, e2), e3), den + 4 * t);
 }
 
 // out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
@@ -515,13 +524,122 @@ __global__ void k_nonzero(const uint64_t* a, uint64_t from, uint64_t to, int* ba
   if (i < to && (a[4 * i] | a[4 * i + 1] | a[4 * i + 2] | a[4 * i + 3])) *bad = 1;
 }
 
+// ---------------------------------------------------------------- sharded layouts (G > 1)
+// Coefficient vectors of a sharded prove live in one of two layouts:
+//  SS (stride shard): slot m of rank r holds global coefficient j = r + G m -- what the
+//     stride-sharded (I)NTT produces and consumes;
+//  CR (contiguous range): rank r holds j in [r Bc, r Bc + Bc) at slot j - r Bc, and the last
+//     rank also the tail [Ls, Ls + TAILC) at slots Bc.. (Ls = G Bc: n, or 2n in mode 0) -- what
+//     the commitments (point ranges of the SRS), evaluations, linear combinations and
+//     synthetic divisions use.
+// SS -> CR is one all-to-all: k_xpose_pack writes, for each destination rank d and part k, the
+// Bc / G + TF elements of d's range with j = (r - off_k) mod G (mod G), k_xpose_unpack places
+// what arrived. A "part" is a slice [off_k, off_k + len_k) of the source vector that becomes its
+// own CR vector (t(x) -> t_lo, t_mid, t_hi); Bc and Ls are multiples of G.
+constexpr uint64_t TAILC = 8;  // tail slots of a CR vector (the last rank), and of an SS vector
+struct XPose {
+  const uint64_t* ss[3];  // source SS vector of each part
+  uint64_t* cr[3];        // destination CR vector of each part (zeroed by the caller)
+  uint64_t off[3], len[3];
+  uint64_t ss_slots;      // source slots of this rank
+  uint64_t Ls, Bc, cap;   // cap = Bc / G + TF per (destination, part)
+  uint32_t G, rank, P;
+};
+__global__ void k_xpose_pack(XPose x, uint64_t* send) {
+  const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= x.ss_slots) return;
+  const uint64_t i = x.rank + (uint64_t)x.G * m;
+  for (uint32_t k = 0; k < x.P; ++k) {
+    if (i < x.off[k] || i >= x.off[k] + x.len[k]) continue;
+    const uint64_t j = i - x.off[k];
+    uint64_t d, e;
+    if (j < x.Ls) {
+      d = j / x.Bc;
+      e = (j - d * x.Bc) / x.G;
+    } else {
+      d = x.G - 1;
+      e = x.Bc / x.G + (j - x.Ls) / x.G;
+    }
+    const uint64_t* src = x.ss[k] + 4 * m;
+    uint64_t* dst = send + 4 * ((d * x.P + k) * x.cap + e);
+    for (int q = 0; q < 4; ++q) dst[q] = src[q];
+  }
+}
+__global__ void k_xpose_unpack(XPose x, const uint64_t* recv) {
+  const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (uint64_t)x.G * x.P * x.cap) return;
+  const uint64_t e = id % x.cap, k = (id / x.cap) % x.P, src = id / (x.cap * x.P);
+  const uint64_t c = (src + x.G - x.off[k] % x.G) % x.G;  // j = i - off_k with i = src (mod G)
+  uint64_t j;
+  if (e < x.Bc / x.G) {
+    j = x.rank * x.Bc + c + x.G * e;
+    if (j >= x.Ls) return;
+  } else {
+    if (x.rank != x.G - 1) return;
+    j = x.Ls + c + x.G * (e - x.Bc / x.G);
+    if (j >= x.Ls + TAILC) return;
+  }
+  if (j >= x.len[k]) return;
+  const uint64_t* sp = recv + 4 * id;
+  uint64_t* dp = x.cr[k] + 4 * (j - x.rank * x.Bc);
+  for (int q = 0; q < 4; ++q) dp[q] = sp[q];
+}
+
+// coeff[slot(idx)] += delta for the blinding indices this rank holds (plonk.rs:250-252, 304):
+// ss: SS layout (slot idx / G on rank idx mod G), else CR
+struct BlindMap {
+  Blind b;
+  uint32_t ss, G, rank;
+  uint64_t Ls, Bc;
+};
+__global__ void k_blind_map(uint64_t* coeff, BlindMap m) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int k = 0; k < m.b.count; ++k) {
+    const uint64_t j = m.b.idx[k];
+    uint64_t slot;
+    if (m.ss) {
+      if (j % m.G != m.rank) continue;
+      slot = j / m.G;
+    } else if (j < m.Ls) {
+      if (j / m.Bc != m.rank) continue;
+      slot = j % m.Bc;
+    } else {
+      if (m.rank != m.G - 1) continue;
+      slot = m.Bc + (j - m.Ls);
+    }
+    str(coeff + 4 * slot, Fr::add(ldr(coeff + 4 * slot), m.b.delta[k]));
+  }
+}
+
+// q[e] += z^(cnt - 1 - e) V for e < cnt, q[cnt - 1] starting from 0: a rank's part of a synthetic
+// division (k_hs*) completed by the contribution V of the coefficients above its range
+__global__ void k_hs_carry(uint64_t* q, uint64_t cnt, U256 z, U256 V) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t k0 = chunk_first(t);  // k = cnt - 1 - e: the power of z
+  if (k0 >= cnt) return;
+  U256 x = Fr::mul_tp(V, fr_pow(z, k0));
+  const U256 step = pow64(z);
+  for (uint64_t k = k0, c = 0; c < PV_CHUNK && k < cnt; ++c, k += 64) {
+    const uint64_t e = cnt - 1 - k;
+    const U256 base = k == 0 ? u256_zero() : u256_from_u64(q + 4 * e);
+    u256_to_u64(Fr::add(base, x), q + 4 * e);
+    x = Fr::mul_tp(x, step);
+  }
+}
+
+// out[0] = a[0] * b[0] (a rank's row-product total: last exclusive prefix times last term)
+__global__ void k_mul1(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) u256_to_u64(Fr::from_mont(Fr::mul(ldr(a), ldr(b))), out);
+}
+
 // batched Horner: partial[p][chunk] = x^(chunk start) * sum of the chunk's terms
 constexpr int EV_T = 256, EV_PER = 64;
 struct EvalArgs {
   const uint64_t* poly[12];
   uint64_t len[12];
   U256 x[12];
-  uint64_t chunks;  // per polynomial
+  uint64_t off[12];  // global index of poly[p][0] (a rank's coefficient range; 0 on one GPU)
+  uint64_t chunks;   // per polynomial
 };
 __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* partial) {
   __shared__ U256 sh[EV_T];
@@ -535,7 +653,7 @@ __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* par
     if (end > e.len[p]) end = e.len[p];
     // conversion-free Horner: canonical acc times Montgomery-form x stays canonical
     for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul_tp(acc, x), u256_from_u64(e.poly[p] + 4 * j));
-    acc = Fr::mul_tp(acc, fr_pow(x, start));
+    acc = Fr::mul_tp(acc, fr_pow(x, e.off[p] + start));
   }
   sh[t] = acc;
   __syncthreads();
@@ -686,64 +804,42 @@ struct Prover {
     for (int i = 0; i < k; ++i)
       scale(srcs[i], rank, G, lens[i], sh + 4 * nl * i, nl, bases[i], rank, G, degs ? degs[i] : 0);
     PBF_HIP(hipGetLastError());
+    return sharded_ntt_from_staging(k, out);
+  }
+  // the sharded forward NTT of the k stride shards in the staging buffer into this rank's blocks
+  int sharded_ntt_from_staging(int k, uint64_t* out) {
+    uint64_t* sh = (uint64_t*)shard->p;
     int rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, sh, (uint64_t*)comm->send, nl, k, 0, s);
     if (!rc) rc = a2a((size_t)k * S * 32);
     if (!rc) rc = pbf_ntt_fr256_shard_combine_dev(ctx, wN_plain, G, rank, (const uint64_t*)comm->recv, out, nl, k, 0, s);
     return rc;
   }
-  // coset NTT of `len` coefficients into N evaluations at g w_N^i
-  int coset_ntt(const uint64_t* coeff, uint64_t len, uint64_t* out) {
-    return coset_ntt_batch(1, &coeff, &len, &g, out);
-  }
-  // coefficients (all N of them, on every rank) of the polynomial whose coset evaluations
-  // are `ev` (this rank's blocks when sharded)
+  // coefficients of the polynomial whose N coset evaluations are `ev` (one GPU)
   int coset_intt(uint64_t* ev, uint64_t* out) {
-    if (G == 1) {
-      int rc = ntt(wN_plain, ev, ev, N, 1, 1);
-      if (rc) return rc;
-      scale(ev, 0, 1, N, out, N, g_inv, 0, 1);
-      PBF_HIP(hipGetLastError());
-      return 0;
-    }
-    uint64_t* sh = (uint64_t*)shard->p;
-    int rc = pbf_ntt_fr256_shard_combine_dev(ctx, wN_plain, G, rank, ev, (uint64_t*)comm->send, nl, 1, 1, s);
-    if (!rc) rc = a2a(S * 32);
-    if (!rc) rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, (const uint64_t*)comm->recv, sh, nl, 1, 1, s);
+    int rc = ntt(wN_plain, ev, ev, N, 1, 1);
     if (rc) return rc;
-    scale(sh, 0, 1, nl, (uint64_t*)comm->send, nl, g_inv, rank, G);  // u_j g^-j, j = rank + G m
-    PBF_HIP(hipGetLastError());
-    if ((rc = ag(nl * 32))) return rc;
-    hipLaunchKernelGGL(k_interleave, dim3(blocks_for(N)), dim3(256), 0, s, (const uint64_t*)comm->recv, out, nl, G);
+    scale(ev, 0, 1, N, out, N, g_inv, 0, 1);
     PBF_HIP(hipGetLastError());
     return 0;
   }
   // SRS::eval_at_s (plonk.rs:51-58) as a fixed-base MSM against the SRS window table
   // (msm.hpp), its XYZZ result left in device slot `slot` (finish_commits collects all of
   // them with one copy: the challenges are inputs, nothing waits on a commitment). Sharded:
-  // this rank's point range, its partial sum left in slot `slot` too; finish_commits
-  // all-gathers the partials of every commitment at once, so no commitment's tail (bucket
-  // join and reduction on the MSM side stream) is waited for before the end of the proof.
+  // commit_cr (below), this rank's point range.
   const Affine* srs_tbl = nullptr;
   uint64_t srs_n = 0;
   Xyzz* slots = nullptr;  // 9 (this rank's partial sums when sharded)
   int commit(const uint64_t* coeff, uint64_t len, int slot) {
-    if (G == 1) return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot);
-    const uint64_t base = len / G, extra = len % G;
-    const uint64_t start = rank * base + (rank < extra ? rank : extra);
-    const uint64_t cnt = base + (rank < extra ? 1 : 0);
-    if (cnt) return msm_fixed_device(ctx, srs_tbl, srs_n, start, coeff + 4 * start, cnt, s, slots + slot);
-    PBF_HIP(hipMemsetAsync(slots + slot, 0, sizeof(Xyzz), s));  // ZZ = 0: the identity
-    return 0;
+    return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot);
   }
-  // q = (p - y) / (x - z) for p of L coefficients (k_hs1..3); a nonzero remainder fails with `err`
-  int synth_div(const uint64_t* p, uint64_t L, const U256& z, const U256& y, uint64_t* q, const char* err) {
-    if (L < 2) return fail(PBF_EINVAL, "synthetic division of a constant");
+  // Horner from the top coefficient over p of L >= 2 coefficients (k_hs1..3): q = the quotient
+  // of (p - y) / (x - z) (L - 1 coefficients), *rem = p(z) - y
+  int synth_div_run(const uint64_t* p, uint64_t L, const U256& z, const U256& y, uint64_t* q, uint64_t* rem) {
     const uint64_t nb = (L + HS_BLK - 1) / HS_BLK;
     DevBuf& hb = ctx->buf("pv.hs");
-    int rc = hb.ensure((nb + 1) * 32);
+    int rc = hb.ensure(nb * 32);
     if (rc) return rc;
     uint64_t* totals = (uint64_t*)hb.p;
-    uint64_t* rem = totals + 4 * nb;
     HsArgs a;
     a.p = p;
     a.L = L;
@@ -753,9 +849,147 @@ struct Prover {
     hipLaunchKernelGGL(k_hs1, dim3((uint32_t)nb), dim3(HS_T), 0, s, a, q, totals, rem);
     hipLaunchKernelGGL(k_hs2, dim3(1), dim3(HS_T), 0, s, totals, nb, hpow64(z, HS_BLK));
     hipLaunchKernelGGL(k_hs3, dim3((uint32_t)nb), dim3(HS_T), 0, s, q, L, z, (const uint64_t*)totals, rem);
-    hipLaunchKernelGGL(k_nonzero, dim3(1), dim3(64), 0, s, (const uint64_t*)rem, 0, 1, d_bad);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  // q = (p - y) / (x - z) for p of L coefficients; a nonzero remainder fails with `err`
+  int synth_div(const uint64_t* p, uint64_t L, const U256& z, const U256& y, uint64_t* q, const char* err) {
+    if (L < 2) return fail(PBF_EINVAL, "synthetic division of a constant");
+    DevBuf& rb = ctx->buf("pv.hs_rem");
+    int rc = rb.ensure(32);
+    if (!rc) rc = synth_div_run(p, L, z, y, q, (uint64_t*)rb.p);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_nonzero, dim3(1), dim3(64), 0, s, (const uint64_t*)rb.p, 0, 1, d_bad);
     PBF_HIP(hipGetLastError());
     return check_bad(err);
+  }
+
+  // ---- sharded layouts (G > 1): rows, SS and CR vectors (see XPose)
+  uint64_t B = 0;        // rows per rank: n / G
+  uint64_t Ls = 0, Bc = 0;  // CR span (n; 2n in mode 0, whose r(x) has 2n + 2 coefficients), Ls / G
+  uint64_t crlo() const { return (uint64_t)rank * Bc; }
+  uint64_t crlen() const { return Bc + (rank == G - 1 ? TAILC : 0); }
+  uint64_t CRS() const { return Bc + TAILC; }  // CR vector stride in the rank's buffers
+  uint64_t SSS() const { return B + TAILC; }   // SS vector (of <= n + TAILC coefficients) stride
+  uint64_t cr_count(uint64_t L) const {        // coefficients j < L in this rank's range
+    const uint64_t lo = crlo();
+    return L <= lo ? 0 : std::min<uint64_t>(L - lo, crlen());
+  }
+  uint64_t ss_count(uint64_t L) const { return L <= rank ? 0 : (L - rank + G - 1) / G; }  // slots with j < L
+  BlindMap bmap(const Blind& b, bool ss) const {
+    BlindMap m;
+    m.b = b; m.ss = ss ? 1u : 0u; m.G = G; m.rank = rank; m.Ls = Ls; m.Bc = Bc;
+    return m;
+  }
+  // Every rank's *d_bad, all-gathered: any set fails every rank with `err` (so no rank waits in
+  // a collective the failed one never reaches)
+  int agree(const char* err) {
+    PBF_HIP(hipMemsetAsync(comm->send, 0, 8, s));
+    PBF_HIP(hipMemcpyAsync(comm->send, d_bad, sizeof(int), hipMemcpyDeviceToDevice, s));
+    int rc = ag(8);
+    if (rc) return rc;
+    std::vector<int> h(2 * G);
+    PBF_HIP(hipMemcpyAsync(h.data(), comm->recv, 8 * G, hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    for (uint32_t g = 0; g < G; ++g)
+      if (h[2 * g]) return fail(PBF_EINVAL, err);
+    return 0;
+  }
+  // cnt canonical field elements at d_vals from every rank: out[g * cnt + i] (Montgomery)
+  int gather(const uint64_t* d_vals, int cnt, std::vector<U256>& out) {
+    PBF_HIP(hipMemcpyAsync(comm->send, d_vals, (size_t)cnt * 32, hipMemcpyDeviceToDevice, s));
+    int rc = ag((size_t)cnt * 32);
+    if (rc) return rc;
+    std::vector<uint64_t> h((size_t)4 * cnt * G);
+    PBF_HIP(hipMemcpyAsync(h.data(), comm->recv, h.size() * 8, hipMemcpyDeviceToHost, s));
+    PBF_HIP(hipStreamSynchronize(s));
+    out.resize((size_t)cnt * G);
+    for (size_t i = 0; i < out.size(); ++i) out[i] = hm(h.data() + 4 * i);
+    return 0;
+  }
+  // SS -> CR (one all-to-all): part k of the source vectors becomes cr[k] (CRS slots, zeroed here)
+  int xpose(int P, const uint64_t* const* ss, uint64_t ss_slots, const uint64_t* off, const uint64_t* len,
+            uint64_t* const* cr) {
+    XPose x;
+    for (int k = 0; k < P; ++k) {
+      x.ss[k] = ss[k]; x.cr[k] = cr[k]; x.off[k] = off[k]; x.len[k] = len[k];
+      PBF_HIP(hipMemsetAsync(cr[k], 0, CRS() * 32, s));
+    }
+    x.ss_slots = ss_slots; x.Ls = Ls; x.Bc = Bc; x.cap = Bc / G + (TAILC + G - 1) / G;
+    x.G = G; x.rank = rank; x.P = (uint32_t)P;
+    if ((uint64_t)G * P * x.cap * 32 > comm->capacity) return fail(PBF_EINVAL, "comm buffers too small for a transpose");
+    hipLaunchKernelGGL(k_xpose_pack, dim3(blocks_for(ss_slots)), dim3(256), 0, s, x, (uint64_t*)comm->send);
+    PBF_HIP(hipGetLastError());
+    int rc = a2a((size_t)P * x.cap * 32);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_xpose_unpack, dim3(blocks_for((uint64_t)G * P * x.cap)), dim3(256), 0, s, x,
+                       (const uint64_t*)comm->recv);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  // k coset NTTs (this rank's blocks) of SS coefficient vectors of lens[i] coefficients
+  int coset_ntt_ss(int k, const uint64_t* const* ss, const uint64_t* lens, const U256* bases, uint64_t* out,
+                   const int* degs = nullptr) {
+    uint64_t* sh = (uint64_t*)shard->p;
+    for (int i = 0; i < k; ++i)
+      scale(ss[i], 0, 1, ss_count(lens[i]), sh + 4 * nl * i, nl, bases[i], rank, G, degs ? degs[i] : 0);
+    PBF_HIP(hipGetLastError());
+    return sharded_ntt_from_staging(k, out);
+  }
+  // the SS coefficients (nl slots, j = rank + G m < N) of the polynomial whose coset
+  // evaluations are this rank's blocks `ev`
+  int coset_intt_ss(const uint64_t* ev, uint64_t* ss_out) {
+    uint64_t* sh = (uint64_t*)shard->p;
+    int rc = pbf_ntt_fr256_shard_combine_dev(ctx, wN_plain, G, rank, ev, (uint64_t*)comm->send, nl, 1, 1, s);
+    if (!rc) rc = a2a(S * 32);
+    if (!rc) rc = pbf_ntt_fr256_shard_local_dev(ctx, wN_plain, G, (const uint64_t*)comm->recv, sh, nl, 1, 1, s);
+    if (rc) return rc;
+    scale(sh, 0, 1, nl, ss_out, nl, g_inv, rank, G);  // u_j g^-j, j = rank + G m
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
+  // commitment of a CR vector of L coefficients: this rank's point range of the SRS (its window
+  // table covers exactly SRS[crlo, crlo + crlen)), the partial sum left in `slot`
+  int commit_cr(const uint64_t* cr, uint64_t L, int slot) {
+    const uint64_t cnt = cr_count(L);
+    if (cnt > srs_n) return fail(PBF_EINVAL, "SRS too short for a sharded commitment");
+    if (cnt) return msm_fixed_device(ctx, srs_tbl, srs_n, 0, cr, cnt, s, slots + slot);
+    PBF_HIP(hipMemsetAsync(slots + slot, 0, sizeof(Xyzz), s));  // ZZ = 0: the identity
+    return 0;
+  }
+  // q = (p - y) / (x - z) for the CR vector p of L coefficients (global): every rank divides its
+  // range (T_r = its value at z relative to its first index), the T_r are all-gathered, the
+  // remainder sum_r T_r z^lo_r - y must be zero (checked on every rank), and each rank adds the
+  // contribution of the coefficients above its range (k_hs_carry)
+  int synth_div_cr(const uint64_t* p, uint64_t L, const U256& z, const U256& y, uint64_t* q, const char* err) {
+    const uint64_t cnt = cr_count(L);
+    DevBuf& rb = ctx->buf("pv.hs_rem");
+    int rc = rb.ensure(32);
+    if (rc) return rc;
+    uint64_t* rem = (uint64_t*)rb.p;
+    PBF_HIP(hipMemsetAsync(q, 0, CRS() * 32, s));
+    if (cnt >= 2) {
+      if ((rc = synth_div_run(p, cnt, z, u256_zero(), q, rem))) return rc;
+    } else if (cnt == 1) {
+      PBF_HIP(hipMemcpyAsync(rem, p, 32, hipMemcpyDeviceToDevice, s));
+    } else {
+      PBF_HIP(hipMemsetAsync(rem, 0, 32, s));
+    }
+    std::vector<U256> T;
+    if ((rc = gather(rem, 1, T))) return rc;
+    U256 value = u256_zero(), V = u256_zero();
+    const uint64_t hi = crlo() + cnt;
+    for (uint32_t g = 0; g < G; ++g) {
+      const uint64_t lo_g = (uint64_t)g * Bc;
+      value = Fr::add(value, Fr::mul(T[g], hpow64(z, lo_g)));
+      if (g > rank) V = Fr::add(V, Fr::mul(T[g], hpow64(z, lo_g - hi)));  // nonzero only above a full range
+    }
+    if (!Fr::is_zero(Fr::sub(value, y))) return fail(PBF_EINVAL, err);
+    if (cnt)
+      hipLaunchKernelGGL(k_hs_carry, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, q, cnt, z,
+                         Fr::from_mont(V));
+    PBF_HIP(hipGetLastError());
+    return 0;
   }
   int finish_commits(int count, uint64_t (*out)[8]) {
     std::vector<Xyzz> h((size_t)count * G);  // [rank][commitment]
@@ -788,6 +1022,369 @@ struct Prover {
 };
 
 }  // namespace
+
+// ---- Plonk::prove across G ranks (pbf_plonk_prove_bn254_sharded_dev). Every
+// witness-dependent step runs on this rank's share, with the layouts of XPose: rows
+// [r B, (r + 1) B) of H; stride shards (SS) out of and into the sharded NTTs; contiguous ranges
+// (CR) for commitments, evaluations, linear combinations and the opening divisions. Collectives
+// (comm callbacks, stream-ordered on P.s): the NTTs' all-to-alls, SS -> CR transposes, and
+// all-gathers of a few field elements (flags, scan totals, evaluation partials, division
+// totals) and of the commitments' partial sums. The proving key (circuit polynomials) is built
+// once per circuit with full-length coefficient slots on every rank and this rank's coset blocks.
+static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk_hit, const std::vector<uint64_t>& pk_key,
+                         uint64_t* const* cslot, uint64_t* const* ceslot, const uint64_t* d_q, const uint64_t* d_copies,
+                         const uint64_t* d_abc, const U256& k1, const U256& k2, const U256* bl, const U256& alpha,
+                         const U256& beta, const U256& gamma, const U256& zc, const U256& v, uint64_t* out_pts,
+                         uint64_t* out_f) {
+  pbf_ctx* ctx = P.ctx;
+  const hipStream_t s = P.s;
+  const uint64_t n = P.n, G = P.G, r = P.rank, Bn = P.B, Sn = Bn / G, NE = P.nl;
+  const uint64_t E = 32, CS = n + 8, CRS = P.CRS(), SSS = P.SSS();
+  const U256 one = fr_one_m();
+  auto C = [&](int k) { return cslot[k]; };
+  auto CE = [&](int k) { return ceslot[k]; };
+  int rc;
+  // ---- this rank's pieces
+  DevBuf& shb = ctx->buf("pv.sh");
+  const uint64_t sh_elems = 3 * Bn + 3 * SSS + 3 * CRS   // abc: blocked evaluations / INTT out, SS, CR
+                            + 3 * Bn + 3 * Bn + Bn        // sigma rows, num / den, acc rows
+                            + SSS + CRS                   // z: SS, CR
+                            + NE + 3 * CRS                // t: SS over 4n, parts CR
+                            + 4 * CRS + 2 * NE            // r, numerator, W_z, W_zw; quotient, mode-0 r_3 evaluations
+                            + (mode == 0 ? NE + CRS : 0) + (Bn / SCAN_BLK + 2) + 4;
+  if ((rc = shb.ensure(sh_elems * E))) return rc;
+  uint64_t* cur = (uint64_t*)shb.p;
+  auto take = [&](uint64_t elems) { uint64_t* p = cur; cur += 4 * elems; return p; };
+  uint64_t* X = take(3 * Bn);
+  uint64_t *abc_ss = take(3 * SSS), *abc_cr = take(3 * CRS);
+  uint64_t *sig = take(3 * Bn), *num = take(Bn), *den = take(Bn), *accr = take(Bn);
+  take(Bn);  // spare row buffer (scan input padding)
+  uint64_t *z_ss = take(SSS), *z_cr = take(CRS);
+  uint64_t *t_ss = take(NE), *t_cr = take(3 * CRS);
+  uint64_t *rx = take(CRS), *numer = take(CRS), *wz = take(CRS), *wzw = take(CRS);
+  uint64_t *Wq = take(NE), *W2 = take(NE);
+  uint64_t* r3_ss = mode == 0 ? take(NE) : nullptr;
+  uint64_t* r3_cr = mode == 0 ? take(CRS) : nullptr;
+  uint64_t* totals = take(Bn / SCAN_BLK + 2);
+  uint64_t* tot = take(1);
+  uint64_t* hpow = (uint64_t*)B.hpow.p;
+  uint64_t* l1 = (uint64_t*)B.tmp0.p;
+  uint64_t* send = (uint64_t*)P.comm->send;
+  uint64_t* recv = (uint64_t*)P.comm->recv;
+
+  // ---- satisfies (constraints.rs:198-230) on this rank's rows, agreed by every rank
+  hipLaunchKernelGGL(k_satisfies, dim3(blocks_for(Bn)), dim3(256), 0, s, d_q, d_abc, d_copies, n, r * Bn, Bn, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.agree("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
+  P.mark("satisfies (rows)");
+  // ---- h = w^i (all of H: copy labels point anywhere), l1 = n^-1 (1 + x + ... + x^(n-1))
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, P.omega, one);
+  const U256 ninv = hinvm(hm64(n));
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, n, one, ninv);
+  PBF_HIP(hipGetLastError());
+  // ---- proving key: the circuit's 8 polynomials (full coefficients on every rank) and this
+  // rank's blocks of their 9 coset evaluations; once per circuit (every proof without the key)
+  if (!pk_hit) {
+    uint64_t* sigma = (uint64_t*)B.sigma.p;
+    hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, n,
+                       (uint64_t)0, n, k1, k2, sigma, P.d_bad);
+    PBF_HIP(hipGetLastError());
+    for (int k = 3; k < 11; ++k) PBF_HIP(hipMemsetAsync(C(k), 0, CS * E, s));
+    for (int k = 0; k < 5; ++k) PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    for (int k = 0; k < 3; ++k) PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    for (int k = 3; k < 11; ++k)
+      if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
+    const uint64_t* srcs[9];
+    uint64_t lens[9];
+    U256 bases[9];
+    for (int k = 0; k < 8; ++k) { srcs[k] = C(3 + k); lens[k] = n; bases[k] = P.g; }
+    srcs[8] = l1; lens[8] = n; bases[8] = P.g;
+    if ((rc = P.coset_ntt_batch(9, srcs, lens, bases, CE(4), QUOT_DEG + 4))) return rc;
+    if ((rc = P.agree("copy constraint label out of range (plonk.rs:181-189)"))) return rc;
+    if (pk_on) {
+      ctx->pk_key = pk_key;
+      B.sigma.release();  // the full label table is only needed to build the key
+    }
+  }
+  P.mark(pk_hit ? "proving key (cached)" : "proving key (built)");
+
+  // ---- round 1: interpolate_at_h of a b c (plonk.rs:233-243) = one sharded INTT of their
+  // blocked evaluations: blocked slot q Sn + kk <- row q B + r Sn + kk of every column
+  for (int col = 0; col < 3; ++col)
+    PBF_HIP(hipMemcpy2DAsync(X + 4 * Bn * col, Sn * E, d_abc + 4 * (n * col + r * Sn), Bn * E, Sn * E, G,
+                             hipMemcpyDeviceToDevice, s));
+  if ((rc = pbf_ntt_fr256_shard_combine_dev(ctx, P.w_plain, (uint32_t)G, (uint32_t)r, X, send, Bn, 3, 1, s))) return rc;
+  if ((rc = P.a2a(3 * Sn * E))) return rc;
+  if ((rc = pbf_ntt_fr256_shard_local_dev(ctx, P.w_plain, (uint32_t)G, recv, X, Bn, 3, 1, s))) return rc;
+  PBF_HIP(hipMemsetAsync(abc_ss, 0, 3 * SSS * E, s));
+  PBF_HIP(hipMemcpy2DAsync(abc_ss, SSS * E, X, Bn * E, Bn * E, 3, hipMemcpyDeviceToDevice, s));
+  // a(x) = (b2 + b1 x)(x^n - 1) + f_a(x), likewise b, c (plonk.rs:250-252), on the SS pieces
+  for (int k = 0; k < 3; ++k) {
+    const U256 lo = bl[2 * k + 1], hi = bl[2 * k];
+    Blind b;
+    b.count = 4;
+    b.idx[0] = 0; b.delta[0] = Fr::sub(u256_zero(), lo);
+    b.idx[1] = 1; b.delta[1] = Fr::sub(u256_zero(), hi);
+    b.idx[2] = n; b.delta[2] = lo;
+    b.idx[3] = n + 1; b.delta[3] = hi;
+    hipLaunchKernelGGL(k_blind_map, dim3(1), dim3(64), 0, s, abc_ss + 4 * SSS * k, P.bmap(b, true));
+  }
+  PBF_HIP(hipGetLastError());
+  {
+    const uint64_t* ss[3] = {abc_ss, abc_ss + 4 * SSS, abc_ss + 8 * SSS};
+    uint64_t* cr[3] = {abc_cr, abc_cr + 4 * CRS, abc_cr + 8 * CRS};
+    const uint64_t off[3] = {0, 0, 0}, len[3] = {n + 2, n + 2, n + 2};
+    if ((rc = P.xpose(3, ss, SSS, off, len, cr))) return rc;
+  }
+  for (int k = 0; k < 3; ++k)
+    if ((rc = P.commit_cr(abc_cr + 4 * CRS * k, n + 2, k))) return rc;
+  P.mark("round 1 (sharded INTT, 3 MSM)");
+
+  // ---- round 2: accumulator (plonk.rs:278-313) over this rank's rows: terms, batch division,
+  // local exclusive prefix products, the ranks' totals all-gathered
+  hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * Bn)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, n, r * Bn, Bn,
+                     k1, k2, sig, P.d_bad);
+  hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(Bn)), dim3(256), 0, s, d_abc, (const uint64_t*)sig,
+                     (const uint64_t*)hpow, n, r * Bn, Bn, beta, Fr::from_mont(gamma), k1, k2, num, den);
+  const uint64_t terms = r + 1 == G ? Bn - 1 : Bn;  // ratios j < n - 1
+  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((terms + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
+                     (const uint64_t*)num, (const uint64_t*)den, num, terms, P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if (terms < Bn) {  // the last row's slot: 1 (canonical), so the local total is defined
+    const uint64_t one_c[4] = {1, 0, 0, 0};
+    PBF_HIP(hipMemcpyAsync(num + 4 * (Bn - 1), one_c, E, hipMemcpyHostToDevice, s));
+  }
+  if ((rc = P.agree("zero permutation denominator (plonk.rs:297 unwrap)"))) return rc;
+  {
+    const uint64_t nb = (Bn + SCAN_BLK - 1) / SCAN_BLK;
+    hipLaunchKernelGGL(k_scan1, dim3((uint32_t)nb), dim3(SCAN_T), 0, s, (const uint64_t*)num, den, Bn, totals);
+    hipLaunchKernelGGL(k_scan2, dim3(1), dim3(SCAN_T), 0, s, totals, nb);
+    hipLaunchKernelGGL(k_scan3, dim3(blocks_for(Bn)), dim3(256), 0, s, (const uint64_t*)den, accr, Bn,
+                       (const uint64_t*)totals);
+    hipLaunchKernelGGL(k_mul1, dim3(1), dim3(64), 0, s, (const uint64_t*)(accr + 4 * (Bn - 1)),
+                       (const uint64_t*)(num + 4 * (Bn - 1)), tot);
+    PBF_HIP(hipGetLastError());
+  }
+  {
+    std::vector<U256> T;
+    if ((rc = P.gather(tot, 1, T))) return rc;
+    U256 Ep = one;  // product of the ratios of the rows before this rank's
+    for (uint64_t g = 0; g < r; ++g) Ep = Fr::mul(Ep, T[g]);
+    // acc rows times Ep, straight into the all-to-all's send buffer: rows [r B, (r + 1) B) in
+    // order are the [dst][Sn] send layout that lands as the blocked layout of the INTT below
+    LinComb L;
+    L.k = 1;
+    L.in[0] = accr; L.len[0] = Bn; L.c[0] = Ep;
+    L.c0 = u256_zero();
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(Bn)), dim3(256), 0, s, L, send, Bn);
+    PBF_HIP(hipGetLastError());
+  }
+  if ((rc = P.a2a(Sn * E))) return rc;  // recv: this rank's blocked rows
+  if ((rc = pbf_ntt_fr256_shard_combine_dev(ctx, P.w_plain, (uint32_t)G, (uint32_t)r, recv, send, Bn, 1, 1, s))) return rc;
+  if ((rc = P.a2a(Sn * E))) return rc;
+  if ((rc = pbf_ntt_fr256_shard_local_dev(ctx, P.w_plain, (uint32_t)G, recv, X, Bn, 1, 1, s))) return rc;
+  PBF_HIP(hipMemsetAsync(z_ss, 0, SSS * E, s));
+  PBF_HIP(hipMemcpyAsync(z_ss, X, Bn * E, hipMemcpyDeviceToDevice, s));
+  {
+    Blind b;  // z(x) = (b9 + b8 x + b7 x^2)(x^n - 1) + acc(x)   (plonk.rs:309)
+    b.count = 6;
+    const U256 c0 = bl[8], c1 = bl[7], c2 = bl[6];
+    b.idx[0] = 0; b.delta[0] = Fr::sub(u256_zero(), c0);
+    b.idx[1] = 1; b.delta[1] = Fr::sub(u256_zero(), c1);
+    b.idx[2] = 2; b.delta[2] = Fr::sub(u256_zero(), c2);
+    b.idx[3] = n; b.delta[3] = c0;
+    b.idx[4] = n + 1; b.delta[4] = c1;
+    b.idx[5] = n + 2; b.delta[5] = c2;
+    hipLaunchKernelGGL(k_blind_map, dim3(1), dim3(64), 0, s, z_ss, P.bmap(b, true));
+    PBF_HIP(hipGetLastError());
+  }
+  {
+    const uint64_t* ss[1] = {z_ss};
+    uint64_t* cr[1] = {z_cr};
+    const uint64_t off[1] = {0}, len[1] = {n + 3};
+    if ((rc = P.xpose(1, ss, SSS, off, len, cr))) return rc;
+  }
+  if ((rc = P.commit_cr(z_cr, n + 3, 3))) return rc;
+  P.mark("round 2 (rows, sharded INTT, MSM)");
+
+  // ---- round 3: a b c z z(w x) on this rank's coset blocks, from their SS pieces
+  {
+    const uint64_t* ss[5] = {abc_ss, abc_ss + 4 * SSS, abc_ss + 8 * SSS, z_ss, z_ss};
+    const uint64_t lens[5] = {n + 2, n + 2, n + 2, n + 3, n + 3};
+    const U256 bases[5] = {P.g, P.g, P.g, P.g, Fr::mul(P.g, P.omega)};
+    if ((rc = P.coset_ntt_ss(5, ss, lens, bases, CE(0)))) return rc;  // slots 0 1 2 3 and 13 (after 3)
+  }
+  QuotArgs qa;
+  qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
+  qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);
+  qa.zw = CE(13);
+  qa.N = NE;
+  qa.N_all = P.N;
+  qa.blk = P.blk();
+  qa.beta0 = Fr::from_mont(beta);
+  qa.gamma0 = Fr::from_mont(gamma);
+  qa.alpha4 = Fr::to_mont(Fr::to_mont(Fr::to_mont(alpha)));
+  qa.k1 = k1; qa.k2 = k2;
+  qa.alpha2 = Fr::mul(alpha, alpha);
+  qa.g = P.g; qa.wN = P.omegaN;
+  {
+    const U256 gn = hpow64(P.g, n), w4 = hpow64(P.omegaN, n);
+    U256 x = gn;
+    for (int j = 0; j < 4; ++j) {
+      const U256 d = Fr::sub(x, one);
+      if (Fr::is_zero(d)) return fail(PBF_EINVAL, "coset meets H");
+      qa.zh_inv[j] = hinvm(d);
+      x = Fr::mul(x, w4);
+    }
+  }
+  {
+    const char* qc = getenv("PBF_QUOT_CHUNK");
+    const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
+    hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, Wq, qch);
+    PBF_HIP(hipGetLastError());
+  }
+  if ((rc = P.coset_intt_ss(Wq, t_ss))) return rc;
+  const uint64_t m = n + 2;  // coefficients per t part
+  hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)t_ss, P.ss_count(3 * m), NE,
+                     P.d_bad);
+  PBF_HIP(hipGetLastError());
+  if ((rc = P.agree("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)"))) return rc;
+  {
+    const uint64_t* ss[3] = {t_ss, t_ss, t_ss};
+    uint64_t* cr[3] = {t_cr, t_cr + 4 * CRS, t_cr + 8 * CRS};
+    const uint64_t off[3] = {0, m, 2 * m}, len[3] = {m, m, m};
+    if ((rc = P.xpose(3, ss, NE, off, len, cr))) return rc;
+  }
+  for (int k = 0; k < 3; ++k)
+    if ((rc = P.commit_cr(t_cr + 4 * CRS * k, m, 4 + k))) return rc;
+  P.mark("round 3 (sharded coset NTTs, quotient, 3 MSM)");
+
+  // ---- round 4: evaluations at z (plonk.rs:393-399) as per-rank partial sums over the CR
+  // ranges (full-length key polynomials: the same range of their coefficients), all-gathered
+  const uint64_t lo = P.crlo(), span = P.crlen();
+  auto eval = [&](int np, const uint64_t* const* polys, const bool* full, const uint64_t* lens, const U256* xs,
+                  U256* res) -> int {
+    EvalArgs e;
+    uint64_t maxlen = 1;
+    for (int i = 0; i < np; ++i) {
+      const uint64_t cnt = full[i] ? (lens[i] > lo ? std::min<uint64_t>(lens[i] - lo, span) : 0) : P.cr_count(lens[i]);
+      e.poly[i] = full[i] ? polys[i] + 4 * lo : polys[i];
+      e.len[i] = cnt; e.x[i] = xs[i]; e.off[i] = lo;
+      maxlen = std::max(maxlen, cnt);
+    }
+    e.chunks = (maxlen + EV_T * EV_PER - 1) / (EV_T * EV_PER);
+    int rc2 = B.partial.ensure(np * e.chunks * 32);
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(k_eval_partial, dim3((uint32_t)(np * e.chunks)), dim3(EV_T), 0, s, e, (uint64_t*)B.partial.p);
+    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, s, (const uint64_t*)B.partial.p, e.chunks, (uint64_t)np,
+                       (uint64_t*)B.evals.p);
+    PBF_HIP(hipGetLastError());
+    std::vector<U256> parts;
+    if ((rc2 = P.gather((const uint64_t*)B.evals.p, np, parts))) return rc2;
+    for (int i = 0; i < np; ++i) {
+      res[i] = u256_zero();
+      for (uint64_t g = 0; g < G; ++g) res[i] = Fr::add(res[i], parts[g * np + i]);
+    }
+    return 0;
+  };
+  const U256 zw = Fr::mul(zc, P.omega);
+  U256 ev[10];
+  {
+    const uint64_t* polys[10] = {abc_cr, abc_cr + 4 * CRS, abc_cr + 8 * CRS, C(8), C(9), t_cr, t_cr + 4 * CRS,
+                                 t_cr + 8 * CRS, z_cr, l1};
+    const bool full[10] = {false, false, false, true, true, false, false, false, false, true};
+    const uint64_t lens[10] = {n + 2, n + 2, n + 2, n, n, m, m, m, n + 3, n};
+    const U256 xs[10] = {zc, zc, zc, zc, zc, zc, zc, zc, zw, zc};
+    if ((rc = eval(10, polys, full, lens, xs, ev))) return rc;
+  }
+  const U256 a_z = ev[0], b_z = ev[1], c_z = ev[2], s1_z = ev[3], s2_z = ev[4], zw_z = ev[8], l1_z = ev[9];
+  const U256 t_z = Fr::add(Fr::add(ev[5], Fr::mul(hpow64(zc, m), ev[6])), Fr::mul(hpow64(zc, 2 * m), ev[7]));
+  const U256 K2 = Fr::mul(Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, zc)), gamma),
+                                          Fr::add(Fr::add(b_z, Fr::mul(Fr::mul(beta, k1), zc)), gamma)),
+                                  Fr::add(Fr::add(c_z, Fr::mul(Fr::mul(beta, k2), zc)), gamma)),
+                          alpha);
+  const U256 K3 = Fr::mul(Fr::mul(Fr::add(Fr::add(a_z, Fr::mul(beta, s1_z)), gamma),
+                                  Fr::add(Fr::add(b_z, Fr::mul(beta, s2_z)), gamma)),
+                          alpha);
+  const U256 K4 = Fr::mul(l1_z, qa.alpha2);
+  const uint64_t rlen = mode == 0 ? 2 * n + 2 : n + 3;
+  // linear combinations over this rank's CR range: full-length inputs from offset lo
+  auto lincomb = [&](int k, const uint64_t* const* in, const bool* full, const uint64_t* lens, const U256* c,
+                     const U256& c0, uint64_t* out) -> int {
+    LinComb L;
+    L.k = k;
+    for (int i = 0; i < k; ++i) {
+      L.in[i] = full[i] ? in[i] + 4 * lo : in[i];
+      L.len[i] = full[i] ? (lens[i] > lo ? std::min<uint64_t>(lens[i] - lo, span) : 0) : P.cr_count(lens[i]);
+      L.c[i] = c[i];
+    }
+    L.c0 = r == 0 ? c0 : u256_zero();  // the constant term is coefficient 0: rank 0's
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(CRS)), dim3(256), 0, s, L, out, CRS);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  };
+  // r(x) = q_m a_z b_z + q_l a_z + q_r b_z + q_o c_z + q_c + (K2 + K4) z(x) + r_3(x)
+  if (mode == 0) {  // r_3(x) = z(x) s_sigma_3(x) (beta z_w(z)) K3 (plonk.rs:414-416): on the coset
+    hipLaunchKernelGGL(k_mul, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)CE(3), (const uint64_t*)CE(11), W2,
+                       NE);
+    PBF_HIP(hipGetLastError());
+    if ((rc = P.coset_intt_ss(W2, r3_ss))) return rc;
+    const uint64_t* ss[1] = {r3_ss};
+    uint64_t* cr[1] = {r3_cr};
+    const uint64_t off[1] = {0}, len[1] = {2 * n + 2};
+    if ((rc = P.xpose(1, ss, NE, off, len, cr))) return rc;
+  }
+  {
+    const uint64_t* in[7] = {C(6), C(3), C(4), C(5), C(7), z_cr, mode == 1 ? C(10) : r3_cr};
+    const bool full[7] = {true, true, true, true, true, false, mode == 1};
+    const uint64_t lens[7] = {n, n, n, n, n, n + 3, mode == 1 ? n : 2 * n + 2};
+    const U256 c[7] = {Fr::mul(a_z, b_z), a_z, b_z, c_z, one, Fr::add(K2, K4),
+                       mode == 1 ? Fr::sub(u256_zero(), Fr::mul(Fr::mul(beta, zw_z), K3))
+                                 : Fr::mul(Fr::mul(beta, zw_z), K3)};
+    if ((rc = lincomb(7, in, full, lens, c, u256_zero(), rx))) return rc;
+  }
+  U256 r_z;
+  {
+    const uint64_t* polys[1] = {rx};
+    const bool full[1] = {false};
+    const uint64_t lens[1] = {rlen};
+    const U256 xs[1] = {zc};
+    if ((rc = eval(1, polys, full, lens, xs, &r_z))) return rc;
+  }
+  P.mark("round 4 (evaluation partials, r(x))");
+
+  // ---- round 5: the opening quotients (plonk.rs:430-442) on the CR ranges
+  U256 vp[7];
+  vp[0] = one;
+  for (int i = 1; i < 7; ++i) vp[i] = Fr::mul(vp[i - 1], v);
+  {
+    const uint64_t* in[9] = {t_cr, t_cr + 4 * CRS, t_cr + 8 * CRS, rx, abc_cr, abc_cr + 4 * CRS, abc_cr + 8 * CRS,
+                             C(8), C(9)};
+    const bool full[9] = {false, false, false, false, false, false, false, true, true};
+    const uint64_t lens[9] = {m, m, m, rlen, n + 2, n + 2, n + 2, n, n};
+    const U256 c[9] = {one, hpow64(zc, n + 2), hpow64(zc, 2 * n + 4), vp[1], vp[2], vp[3], vp[4], vp[5], vp[6]};
+    U256 cst = Fr::add(t_z, Fr::mul(vp[1], r_z));
+    cst = Fr::add(cst, Fr::mul(vp[2], a_z));
+    cst = Fr::add(cst, Fr::mul(vp[3], b_z));
+    cst = Fr::add(cst, Fr::mul(vp[4], c_z));
+    cst = Fr::add(cst, Fr::mul(vp[5], s1_z));
+    cst = Fr::add(cst, Fr::mul(vp[6], s2_z));
+    if ((rc = lincomb(9, in, full, lens, c, Fr::sub(u256_zero(), cst), numer))) return rc;
+  }
+  const uint64_t lnum = rlen > m ? rlen : m;
+  const uint64_t wlen = lnum - 1;
+  if ((rc = P.synth_div_cr(numer, lnum, zc, u256_zero(), wz, "W_z division left a remainder (plonk.rs:438)"))) return rc;
+  if ((rc = P.commit_cr(wz, wlen, 7))) return rc;
+  if ((rc = P.synth_div_cr(z_cr, n + 3, zw, zw_z, wzw, "W_zw division left a remainder (plonk.rs:442)"))) return rc;
+  if ((rc = P.commit_cr(wzw, n + 2, 8))) return rc;
+  uint64_t pts[9][8];
+  if ((rc = P.finish_commits(9, pts))) return rc;
+  P.mark("round 5 (sharded divisions, 2 MSM)");
+  for (int i = 0; i < 9; ++i) memcpy(out_pts + 8 * i, pts[i], 64);
+  const U256 fo[7] = {a_z, b_z, c_z, s1_z, s2_z, r_z, zw_z};
+  for (int i = 0; i < 7; ++i) hout(out_f + 4 * i, fo[i]);
+  return 0;
+}
 
 // Plonk::prove; comm == null (or world 1): one GPU; else this rank's part of the multi-GPU
 // split (pbf.h pbf_plonk_prove_bn254_sharded_dev)
@@ -829,15 +1426,19 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     if (G != 2 && G != 4 && G != 8) return fail(PBF_EINVAL, "world size must be 2, 4 or 8");
     if (comm->rank >= G) return fail(PBF_EINVAL, "rank out of range");
     if (!comm->send || !comm->recv || !comm->all_to_all || !comm->all_gather) return fail(PBF_EINVAL, "incomplete comm");
-    if (4 * (uint64_t)n < (uint64_t)G * G) return fail(PBF_EINVAL, "4n must be at least world^2");
+    if ((uint64_t)n < (uint64_t)G * G) return fail(PBF_EINVAL, "n must be at least world^2 (sharded layouts)");
     P.comm = comm;
     P.G = G;
     P.rank = comm->rank;
     P.nl = 4 * (uint64_t)n / G;
     P.S = P.nl / G;
-    if (comm->capacity < 16 * P.nl * 32) return fail(PBF_EINVAL, "comm buffers below 16 * (4n / world) * 32 bytes");
+    P.B = n / G;
+    P.Ls = mode == 0 ? 2 * (uint64_t)n : (uint64_t)n;  // mode 0's r(x) and W_z reach x^(2n+1)
+    P.Bc = P.Ls / G;
+    // the largest exchange: the proving key's 9 coset NTTs of 4n / world points per rank
+    if (comm->capacity < 9 * P.nl * 32) return fail(PBF_EINVAL, "comm buffers below 9 * (4n / world) * 32 bytes");
     P.shard = &ctx->buf("pv.shard");
-    int rc0 = P.shard->ensure(16 * P.nl * 32);
+    int rc0 = P.shard->ensure(9 * P.nl * 32);
     if (rc0) return rc0;
   }
   const hipStream_t s = P.s;
@@ -883,11 +1484,16 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     pk_hit = ctx->pk_key == pk_key;
     if (!pk_hit) ctx->pk_key.clear();  // the slots are rewritten below; valid again once complete
   }
-  if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure(3 * n * E)) || (rc = B.coef.ensure(11 * (n + 8) * E)) ||
-      (rc = B.acc.ensure((n + 8) * E)) || (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure(n * E)) ||
+  // sharded: full-length scratch only where the proving key is built (the circuit's polynomials
+  // on every rank); the witness-dependent vectors live in this rank's SS / CR pieces ("pv.sh")
+  const bool sharded = P.G > 1;
+  const uint64_t n_full = sharded ? 0 : n;
+  if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure((sharded && pk_hit ? 0 : 3 * n) * E)) ||
+      (rc = B.coef.ensure((sharded ? (pk_on ? 0 : 11) : 11) * (n + 8) * E)) || (rc = B.acc.ensure((n_full + 8) * E)) ||
+      (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure((n_full + 8) * E)) ||
       (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure((pk_on ? 5 : 14) * P.count() * E)) ||
-      (rc = B.t.ensure(N * E)) || (rc = B.work.ensure(3 * N * E)) || (rc = B.flag.ensure(64)) ||
-      (rc = B.evals.ensure(16 * E)))
+      (rc = B.t.ensure((sharded ? 8 : N) * E)) || (rc = B.work.ensure((sharded ? 8 : 3 * N) * E)) ||
+      (rc = B.flag.ensure(64)) || (rc = B.evals.ensure(16 * E)))
     return rc;
   P.d_bad = (int*)B.flag.p;
   PBF_HIP(hipMemsetAsync(P.d_bad, 0, sizeof(int), s));
@@ -895,8 +1501,15 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     DevBuf& sl = ctx->buf("pv.commits");
     if ((rc = sl.ensure(9 * sizeof(Xyzz)))) return rc;
     P.slots = (Xyzz*)sl.p;
-    P.srs_n = srs_m;
-    if ((rc = msm_fixed_table(ctx, d_srs, srs_m, s, &P.srs_tbl))) return rc;  // built once per SRS
+    if (!sharded) {
+      P.srs_n = srs_m;
+      if ((rc = msm_fixed_table(ctx, d_srs, srs_m, s, &P.srs_tbl))) return rc;  // built once per SRS
+    } else {
+      // this rank's point range SRS[crlo, crlo + crlen) (contiguous: the CR ranges)
+      if (P.crlo() >= srs_m) return fail(PBF_EINVAL, "SRS too short for this n, mode and world size");
+      P.srs_n = std::min<uint64_t>(P.crlen(), srs_m - P.crlo());
+      if ((rc = msm_fixed_table(ctx, d_srs + 8 * P.crlo(), P.srs_n, s, &P.srs_tbl))) return rc;
+    }
   }
   uint64_t* hpow = (uint64_t*)B.hpow.p;
   uint64_t* sigma = (uint64_t*)B.sigma.p;
@@ -909,18 +1522,23 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   const uint64_t NE = P.count();  // coset evaluations held here (N; nl = N / G when sharded)
   uint64_t* ceslot[14];
   for (int k = 0; k < 14; ++k)
-    ceslot[k] = (pk_on && k >= 4 && k <= 12) ? pkcoset + 4 * NE * (k - 4)
-                : (pk_on && k == 13)        ? coset + 4 * NE * 4  // z(w x) after a b c z
-                                            : coset + 4 * NE * k;
+    ceslot[k] = (pk_on && k >= 4 && k <= 12)  ? pkcoset + 4 * NE * (k - 4)
+                : ((pk_on || sharded) && k == 13) ? coset + 4 * NE * 4        // z(w x) after a b c z
+                : (sharded && k >= 4 && k <= 12)  ? coset + 4 * NE * (k + 1)  // no key: circuit slots after
+                                                  : coset + 4 * NE * k;
   auto CE = [&](int k) { return ceslot[k]; };
   // coset slots: 0 a 1 b 2 c 3 z 4 ql 5 qr 6 qo 7 qm 8 qc 9 s1 10 s2 11 s3 12 l1 [13 z(w x), sharded]
+  if (sharded)
+    return prove_sharded(P, B, mode, pk_on, pk_hit, pk_key, cslot, ceslot, d_q, d_copies, d_abc, k1, k2, bl, alpha, beta,
+                         gamma, zc, v, out_pts, out_f);
   uint64_t* work = (uint64_t*)B.work.p;
   uint64_t* W0 = work;
   uint64_t* W1 = work + 4 * N;
   uint64_t* W2 = work + 8 * N;
 
   // ---- satisfies (constraints.rs:198-230)
-  hipLaunchKernelGGL(k_satisfies, dim3(blocks_for(n)), dim3(256), 0, s, d_q, d_abc, d_copies, (uint64_t)n, P.d_bad);
+  hipLaunchKernelGGL(k_satisfies, dim3(blocks_for(n)), dim3(256), 0, s, d_q, d_abc, d_copies, (uint64_t)n, (uint64_t)0,
+                     (uint64_t)n, P.d_bad);
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
   P.mark("satisfies");
@@ -929,7 +1547,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
                      P.omega, one);
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, (uint64_t)n,
-                     k1, k2, sigma, P.d_bad);
+                     (uint64_t)0, (uint64_t)n, k1, k2, sigma, P.d_bad);
   PBF_HIP(hipGetLastError());
   // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
   PBF_HIP(hipMemsetAsync(coef, 0, (pk_on ? 3 : 11) * CS * E, s));
@@ -971,7 +1589,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* den = (uint64_t*)B.tmp1.p;
   PBF_HIP(hipMemsetAsync(acc, 0, CS * E, s));
   hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(n)), dim3(256), 0, s, d_abc, (const uint64_t*)sigma,
-                     (const uint64_t*)hpow, (uint64_t)n, beta, Fr::from_mont(gamma), k1, k2, num, den);
+                     (const uint64_t*)hpow, (uint64_t)n, (uint64_t)0, (uint64_t)n, beta, Fr::from_mont(gamma), k1, k2, num,
+                     den);
   hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((n - 1 + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
                      (const uint64_t*)num, (const uint64_t*)den, num, (uint64_t)(n - 1), P.d_bad);
   PBF_HIP(hipGetLastError());
@@ -1033,12 +1652,12 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
       const uint64_t* ps[5] = {srcs[0], srcs[1], srcs[2], srcs[3], srcs[13]};
       const uint64_t pl[5] = {lens[0], lens[1], lens[2], lens[3], lens[13]};
       const U256 pb[5] = {bases[0], bases[1], bases[2], bases[3], bases[13]};
-      if ((rc = P.coset_ntt_batch(P.G > 1 ? 5 : 4, ps, pl, pb, CE(0)))) return rc;
+      if ((rc = P.coset_ntt_batch(4, ps, pl, pb, CE(0)))) return rc;
       if (!pk_hit) {
         if ((rc = P.coset_ntt_batch(9, srcs + 4, lens + 4, bases + 4, CE(4), QUOT_DEG + 4))) return rc;
         ctx->pk_key = pk_key;
       }
-    } else if ((rc = P.coset_ntt_batch(P.G > 1 ? 14 : 13, srcs, lens, bases, CE(0), QUOT_DEG))) {
+    } else if ((rc = P.coset_ntt_batch(13, srcs, lens, bases, CE(0), QUOT_DEG))) {
       return rc;
     }
   }
@@ -1046,7 +1665,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   QuotArgs qa;
   qa.a = CE(0); qa.b = CE(1); qa.c = CE(2); qa.z = CE(3); qa.ql = CE(4); qa.qr = CE(5); qa.qo = CE(6);
   qa.qm = CE(7); qa.qc = CE(8); qa.s1 = CE(9); qa.s2 = CE(10); qa.s3 = CE(11); qa.l1 = CE(12);
-  qa.zw = P.G > 1 ? CE(13) : nullptr;
+  qa.zw = nullptr;
   qa.N = NE;
   qa.N_all = N;
   qa.blk = P.blk();
@@ -1093,7 +1712,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     EvalArgs e;
     uint64_t maxlen = 0;
     for (int i = 0; i < np; ++i) {
-      e.poly[i] = polys[i]; e.len[i] = lens[i]; e.x[i] = xs[i];
+      e.poly[i] = polys[i]; e.len[i] = lens[i]; e.x[i] = xs[i]; e.off[i] = 0;
       if (lens[i] > maxlen) maxlen = lens[i];
     }
     e.chunks = (maxlen + EV_T * EV_PER - 1) / (EV_T * EV_PER);
@@ -1349,7 +1968,7 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
                      (uint64_t)n, omega, one);
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hp.p, (uint64_t)n,
-                     k1, k2, (uint64_t*)sg.p, (int*)fl.p);
+                     (uint64_t)0, (uint64_t)n, k1, k2, (uint64_t*)sg.p, (int*)fl.p);
   PBF_HIP(hipGetLastError());
   uint64_t* c = (uint64_t*)cf.p;
   // slots: 0 q_m 1 q_l 2 q_r 3 q_o 4 q_c 5 s1 6 s2 7 s3  (q columns: q_l q_r q_o q_m q_c)

@@ -67,7 +67,6 @@ SIGNATURES = [
     ("pbf_msm_g1_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _p64, _vp]),
     ("pbf_g1_bn254_mul_base_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     ("pbf_msm_g1_bn254_fixed_dev", ctypes.c_int, [_vp, _vp, _sz, _vp, _sz, _p64, _vp]),
-    ("pbf_msm_g1_bn254_fixed_range_dev", ctypes.c_int, [_vp, _vp, _sz, _sz, _vp, _sz, _p64, _vp]),
     ("pbf_srs_create_bn254", ctypes.c_int, [_vp, _p64, _sz, _p64]),
     ("pbf_pairing_bn254", ctypes.c_int, [_vp, _p64, _p64, _sz, _p64]),
     ("pbf_pairing_bn254_dev", ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
@@ -95,6 +94,18 @@ SIGNATURES = [
                                                _vp]),
     ("pbf_ntt_shard_combine_dev", ctypes.c_int, [_vp, _u64, _u64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, _sz,
                                                  _sz, ctypes.c_int, _vp]),
+    ("pbf_ntt_u64_multi", ctypes.c_int, [_vp, ctypes.c_uint32, _u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
+    ("pbf_ntt_u64_multi_dev", ctypes.c_int, [_vp, ctypes.c_uint32, _u64, _u64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
+    ("pbf_ntt_fr256_multi", ctypes.c_int, [_vp, ctypes.c_uint32, _p64, _p64, _p64, _sz, ctypes.c_int]),
+    ("pbf_ntt_fr256_multi_dev", ctypes.c_int, [_vp, ctypes.c_uint32, _p64, _vp, _vp, _sz, _sz, ctypes.c_int, _vp]),
+    ("pbf_mul_ntt_u64_multi", ctypes.c_int, [_vp, ctypes.c_uint32, _u64, _u64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_mul_ntt_fr256_multi", ctypes.c_int, [_vp, ctypes.c_uint32, _p64, _p64, _sz, _p64, _sz, _p64]),
+    ("pbf_plonk_prove_bn254_multi", ctypes.c_int, [_vp, ctypes.c_uint32, _sz, _p64, _p64, _p64, _p64, _p64, _p64, _p64,
+                                                   _sz, ctypes.c_int, _p64, _p64]),
+    ("pbf_plonk_prove_bn254_multi_dev", ctypes.c_int, [_vp, ctypes.c_uint32, _sz, _vp, _vp, _vp, _p64, _p64, _p64, _vp,
+                                                       _sz, ctypes.c_int, _p64, _p64, _vp]),
+    ("pbf_multi_backend", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int)]),
+    ("pbf_msm_g1_bn254_fixed_range_dev", ctypes.c_int, [_vp, _vp, _sz, _sz, _vp, _sz, _p64, _vp]),
 ]
 
 _lib = None
@@ -520,6 +531,98 @@ def ints_to_limbs(values) -> np.ndarray:
 def limbs_to_ints(a: np.ndarray) -> list:
     a = np.asarray(a, dtype=np.uint64).reshape(-1, 4)
     return [int(r[0]) | (int(r[1]) << 64) | (int(r[2]) << 128) | (int(r[3]) << 192) for r in a]
+
+
+# ---- multi-GPU from one process (pbf_*_multi): a list of Contexts, rank g = ctxs[g] -----------
+def _ctx_array(ctxs):
+    arr = (_vp * len(ctxs))(*[c.h for c in ctxs])
+    return arr, len(ctxs)
+
+
+def _ptr_array(ptrs):
+    return (_vp * len(ptrs))(*[_vp(p) if p else None for p in ptrs])
+
+
+def multi_backend(ctxs) -> str:
+    arr, w = _ctx_array(ctxs)
+    b = ctypes.c_int(-1)
+    _check(load_library().pbf_multi_backend(arr, w, ctypes.byref(b)))
+    return {0: "device-copies", 1: "rccl"}[b.value]
+
+
+def ntt_multi(ctxs, modulus: int, omega: int, values, inverse: bool = False) -> np.ndarray:
+    """pbf_ntt_u64_multi: fft.rs:66-78 of one vector with its top log2(G) levels across the ranks."""
+    arr, w = _ctx_array(ctxs)
+    a = _as_u64(values)
+    out = np.empty_like(a)
+    _check(load_library().pbf_ntt_u64_multi(arr, w, modulus, omega, _ptr(a), _ptr(out), a.size, int(inverse)))
+    return out
+
+
+def ntt_multi_dev(ctxs, modulus: int, omega: int, d_in, d_out, nl: int, batch: int, inverse: bool = False,
+                  streams=None) -> None:
+    arr, w = _ctx_array(ctxs)
+    _check(load_library().pbf_ntt_u64_multi_dev(arr, w, modulus, omega, _ptr_array(d_in), _ptr_array(d_out), nl, batch,
+                                                int(inverse), _ptr_array(streams) if streams else None))
+
+
+def ntt_fr_multi(ctxs, omega: int, values, inverse: bool = False) -> list:
+    arr, w = _ctx_array(ctxs)
+    a = ints_to_limbs(values)
+    out = np.empty_like(a)
+    _check(load_library().pbf_ntt_fr256_multi(arr, w, _ptr(ints_to_limbs([omega])), _ptr(a), _ptr(out), len(values),
+                                              int(inverse)))
+    return limbs_to_ints(out)
+
+
+def mul_ntt_multi(ctxs, modulus: int, omega: int, a, b) -> np.ndarray:
+    arr, w = _ctx_array(ctxs)
+    a = _as_u64(a)
+    b = _as_u64(b)
+    out = np.empty(a.size + b.size, dtype=np.uint64)
+    _check(load_library().pbf_mul_ntt_u64_multi(arr, w, modulus, omega, _ptr(a), a.size, _ptr(b), b.size, _ptr(out)))
+    return out
+
+
+def mul_ntt_fr_multi(ctxs, omega: int, a, b) -> list:
+    arr, w = _ctx_array(ctxs)
+    al, bl = ints_to_limbs(a), ints_to_limbs(b)
+    out = np.empty((len(a) + len(b)) * 4, dtype=np.uint64)
+    _check(load_library().pbf_mul_ntt_fr256_multi(arr, w, _ptr(ints_to_limbs([omega])), _ptr(al), len(a), _ptr(bl),
+                                                  len(b), _ptr(out)))
+    return limbs_to_ints(out)
+
+
+def plonk_prove_bn254_multi(ctxs, q, copies, abc, chal, rnd, srs, k1k2=(2, 3), mode=1):
+    """pbf_plonk_prove_bn254_multi (host inputs; same conventions as Context.plonk_prove_bn254)."""
+    arr, w = _ctx_array(ctxs)
+    n = len(abc[0])
+    qa = ints_to_limbs([x for col in q for x in col])
+    ca = np.array([v for col in copies for (k, i) in col for v in (k, i)], dtype=np.uint64)
+    aa = ints_to_limbs([x for col in abc for x in col])
+    sa = _g1_limbs(srs)
+    pts = np.zeros(72, dtype=np.uint64)
+    fs = np.zeros(28, dtype=np.uint64)
+    _check(load_library().pbf_plonk_prove_bn254_multi(arr, w, n, _ptr(qa), _ptr(ca), _ptr(aa), _ptr(ints_to_limbs(chal)),
+                                                      _ptr(ints_to_limbs(rnd)), _ptr(ints_to_limbs(k1k2)), _ptr(sa),
+                                                      len(srs), mode, _ptr(pts), _ptr(fs)))
+    pv = limbs_to_ints(pts)
+    return [None if pv[2 * i] == 0 and pv[2 * i + 1] == 0 else (pv[2 * i], pv[2 * i + 1]) for i in range(9)], \
+        limbs_to_ints(fs)
+
+
+def plonk_prove_bn254_multi_dev(ctxs, n, d_q, d_copies, d_abc, chal, rnd, d_srs, srs_m, k1k2=(2, 3), mode=1,
+                                streams=None):
+    """pbf_plonk_prove_bn254_multi_dev: per-rank device inputs (lists of pointers); returns the
+    proof as limb arrays (9 x 8 u64 points, 7 x 4 u64 fields)."""
+    arr, w = _ctx_array(ctxs)
+    pts = np.zeros(72, dtype=np.uint64)
+    fs = np.zeros(28, dtype=np.uint64)
+    _check(load_library().pbf_plonk_prove_bn254_multi_dev(
+        arr, w, n, _ptr_array(d_q), _ptr_array(d_copies), _ptr_array(d_abc), _ptr(ints_to_limbs(chal)),
+        _ptr(ints_to_limbs(rnd)), _ptr(ints_to_limbs(k1k2)), _ptr_array(d_srs), srs_m, mode, _ptr(pts), _ptr(fs),
+        _ptr_array(streams) if streams else None))
+    return pts, fs
 
 
 _default_ctx: Context | None = None

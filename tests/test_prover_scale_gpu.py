@@ -148,3 +148,47 @@ def test_prove_2p24_gates(ctx):
     bad_p[[4, 6]] = bad_p[[6, 4]]  # t_lo <-> t_hi
     assert not verify(bad_p.reshape(-1), fs)
     ctx.release_caches()  # ~24 GB of proving key; later tests start from a clean context
+
+
+def test_prove_2p24_gates_8_virtual_ranks():
+    """Config 5 in its specified form -- 2^24 gates with the work split over 8 ranks -- as 8
+    virtual ranks on this one GPU (pbf_plonk_prove_bn254_multi_dev, device-copy exchanges),
+    bit-exact against the single-GPU proof of the same inputs. Prints the device bytes in use
+    with the 8 ranks' contexts alive (what 8 real GPUs would each hold is about 1/8 of it plus
+    the shared inputs)."""
+    import torch
+
+    import pbf
+
+    n, G = 1 << 24, 8
+    rng = random.Random(0x5EED0024)
+    single = pbf.Context(0)
+    sp = torch.cuda.current_stream().cuda_stream
+    dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
+    dc = torch.empty(3 * n * 2, dtype=torch.int64, device="cuda")
+    dabc = torch.empty(3 * n * 4, dtype=torch.int64, device="cuda")
+    single.plonk_synth_circuit_dev(n, 0x5EED0024, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), stream=sp)
+    s = rng.randrange(2, P.R)
+    srs_m = n + 3
+    dsrs = torch.empty(srs_m * 8, dtype=torch.int64, device="cuda")
+    single.srs_create_dev(s, srs_m - 1, dsrs.data_ptr(), stream=sp)
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    ref = single.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(),
+                                       srs_m, mode=1, stream=sp)
+    torch.cuda.synchronize()
+    single.close()
+    free0, total = torch.cuda.mem_get_info()
+    ranks = [pbf.Context(0) for _ in range(G)]
+    try:
+        pts, fs = pbf.plonk_prove_bn254_multi_dev(ranks, n, [dq.data_ptr()] * G, [dc.data_ptr()] * G,
+                                                  [dabc.data_ptr()] * G, chal, rnd, [dsrs.data_ptr()] * G, srs_m,
+                                                  mode=1)
+        free1, _ = torch.cuda.mem_get_info()
+        print(f"\n[2^24 x 8 virtual ranks] device bytes in use: {(total - free1) / 2**30:.1f} GiB of "
+              f"{total / 2**30:.1f} GiB (inputs + SRS {(total - free0) / 2**30:.1f} GiB); per rank "
+              f"{(free0 - free1) / G / 2**30:.1f} GiB")
+        assert np.array_equal(pts, ref[0]) and np.array_equal(fs, ref[1])
+    finally:
+        for c in ranks:
+            c.close()

@@ -5,7 +5,8 @@ commitments, checked bit-exact against the single-GPU proof of the same inputs (
 bit-exact against the literal oracle, tests/test_prover_gpu.py).
 
 * virtual ranks: G = 2, 4, 8 host threads, each with its own context and stream on this GPU,
-  exchanging through multigpu.LocalComm (device copies);
+  exchanging through multigpu.LocalComm (device copies); n >= G^2 (the sharded layouts);
+  too small an n is refused;
 * two processes over torch.distributed/gloo (host-staged exchanges, multigpu.DistComm),
   both on cuda:0: the same code path the driver's RCCL run takes, with a real process group.
 """
@@ -49,7 +50,8 @@ def _inputs(n, seed, mode):
     return ctx, (dq, dc, dabc, dsrs, srs_m, chal, rnd), ref
 
 
-@pytest.mark.parametrize("G,log_n,mode", [(2, 10, 1), (4, 10, 1), (8, 10, 1), (2, 12, 0), (8, 5, 1), (8, 17, 1)])
+@pytest.mark.parametrize("G,log_n,mode", [(2, 10, 1), (4, 10, 1), (8, 10, 1), (2, 12, 0), (4, 11, 0), (8, 6, 1),
+                                         (8, 17, 1)])
 def test_sharded_prove_virtual_ranks(G, log_n, mode):
     import torch
 
@@ -136,6 +138,20 @@ def test_sharded_prove_on_a_non_current_stream(G):
     for r in range(G):
         pts, fs = out[r]
         assert np.array_equal(pts, pts0) and np.array_equal(fs, fs0), f"rank {r} proof differs from one GPU's"
+    ctx0.close()
+
+
+def test_sharded_prove_rejects_n_below_world_squared():
+    import torch
+
+    import pbf
+    from multigpu import LocalComm, LocalGroup, ShardedProver
+
+    n, G = 32, 8
+    ctx0, (dq, dc, dabc, dsrs, srs_m, chal, rnd), _ = _inputs(n, 5, 1)
+    sp = ShardedProver(ctx0, LocalComm(LocalGroup(1), 0), 0, G, n, stream=torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(pbf.PbfError):
+        sp.prove(dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(), srs_m, mode=1)
     ctx0.close()
 
 
