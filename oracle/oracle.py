@@ -49,6 +49,11 @@ _SIG = [
     ("oracle_gt_pow", None, [_p64, _u64, _p64]),
     ("oracle_pairing", ctypes.c_int, [_p64, _p64, _p64]),
     ("oracle_fr_mul_ntt", ctypes.c_int, [_p64, _sz, _p64, _sz, _p64, _p64]),
+    ("oracle_fr_mul_ntt_par", ctypes.c_int, [_p64, _sz, _p64, _sz, _p64, ctypes.c_int, _p64]),
+    ("oracle_synth_circuit", ctypes.c_int, [_sz, ctypes.c_uint64, _p64, _p64, _p64, ctypes.c_int]),
+    ("oracle_commitment_scalars", ctypes.c_int, [_sz, _p64, _p64, _p64, _p64, _p64, _p64, _p64, ctypes.c_int, _p64]),
+    ("oracle_plonk_prove_cpu", ctypes.c_int, [_sz, _p64, _p64, _p64, _p64, _p64, _p64, _p64, _sz, ctypes.c_int,
+                                              ctypes.c_int, _p64, _p64]),
     ("oracle_g1_msm_naive", ctypes.c_int, [_p64, _p64, _sz, _p64]),
     ("oracle_g1_msm_pippenger", ctypes.c_int, [_p64, _p64, _sz, ctypes.c_int, _p64]),
     ("oracle_g1_mul_gen", ctypes.c_int, [_p64, _sz, _p64]),
@@ -337,3 +342,62 @@ def g1_progression(k0: int, d: int, n: int) -> np.ndarray:
     out = np.zeros((n, 8), dtype=np.uint64)
     lib().oracle_g1_progression(_p(_limbs([k0])), _p(_limbs([d])), n, _p(out))
     return out
+
+
+# ---------------------------------------------------------------- config 5 on the host (prover_cpu.cpp)
+def _threads(t):
+    import os
+
+    return t or (os.cpu_count() or 1)
+
+
+def fr_mul_ntt_par(a_limbs: np.ndarray, b_limbs: np.ndarray, omega: int, threads: int = 0) -> np.ndarray:
+    """mul_ntt (fft.rs:109-132) over Fr, iterative NTT on `threads` host threads (0 = all)."""
+    a = np.ascontiguousarray(a_limbs, dtype=np.uint64).reshape(-1, 4)
+    b = np.ascontiguousarray(b_limbs, dtype=np.uint64).reshape(-1, 4)
+    out = np.zeros((len(a) + len(b), 4), dtype=np.uint64)
+    if lib().oracle_fr_mul_ntt_par(_p(a), len(a), _p(b), len(b), _p(_limbs([omega])), _threads(threads), _p(out)):
+        raise ValueError("la + lb must be a power of two")
+    return out
+
+
+def synth_circuit(n: int, seed: int, threads: int = 0):
+    """k_synth_circuit (prover.hip) restated: (q 5n x 4, copies 3n x 2, abc 3n x 4) u64 arrays."""
+    q = np.zeros(5 * n * 4, dtype=np.uint64)
+    c = np.zeros(3 * n * 2, dtype=np.uint64)
+    abc = np.zeros(3 * n * 4, dtype=np.uint64)
+    lib().oracle_synth_circuit(n, seed, _p(q), _p(c), _p(abc), _threads(threads))
+    return q, c, abc
+
+
+def commitment_scalars_cpu(n, q, copies, abc, chal, rnd, s, k1k2=(2, 3), threads: int = 0) -> dict:
+    """plonk_bn254.commitment_scalars in C++ (limb arrays in): {mode: {a b c z t wz wzw fields}}."""
+    out = np.zeros(2 * 14 * 4, dtype=np.uint64)
+    rc = lib().oracle_commitment_scalars(n, _p(np.ascontiguousarray(q, dtype=np.uint64)),
+                                         _p(np.ascontiguousarray(copies, dtype=np.uint64)),
+                                         _p(np.ascontiguousarray(abc, dtype=np.uint64)), _p(_limbs(chal)),
+                                         _p(_limbs(rnd)), _p(_limbs([s])), _p(_limbs(k1k2)), _threads(threads), _p(out))
+    if rc:
+        raise ValueError("s or z lies in H")
+    v = _ints(out)
+    res = {}
+    for md, name in ((0, "reference"), (1, "paper")):
+        x = v[14 * md:14 * (md + 1)]
+        res[name] = dict(zip(("a", "b", "c", "z", "t", "wz", "wzw"), x[:7]))
+        res[name]["fields"] = x[7:]
+    return res
+
+
+def plonk_prove_cpu(n, q, copies, abc, chal, rnd, srs_limbs, k1k2=(2, 3), mode=1, threads: int = 0):
+    """The generalised prover on the host (the config-5 CPU baseline): limb arrays in (srs:
+    srs_m x 8), returns (9 x 8 point limbs, 7 x 4 field limbs)."""
+    srs = np.ascontiguousarray(srs_limbs, dtype=np.uint64).reshape(-1, 8)
+    pts = np.zeros(72, dtype=np.uint64)
+    fs = np.zeros(28, dtype=np.uint64)
+    rc = lib().oracle_plonk_prove_cpu(n, _p(np.ascontiguousarray(q, dtype=np.uint64)),
+                                      _p(np.ascontiguousarray(copies, dtype=np.uint64)),
+                                      _p(np.ascontiguousarray(abc, dtype=np.uint64)), _p(_limbs(chal)), _p(_limbs(rnd)),
+                                      _p(_limbs(k1k2)), _p(srs), len(srs), mode, _threads(threads), _p(pts), _p(fs))
+    if rc:
+        raise ValueError(f"oracle_plonk_prove_cpu rc={rc}")
+    return pts, fs
