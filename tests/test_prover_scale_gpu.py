@@ -111,13 +111,33 @@ def test_prove_2p20_gates(ctx, log_n):
         assert all(res.values()), (md, res)
 
 
+def test_synth_circuit_matches_host_restatement(ctx):
+    """pbf_plonk_synth_circuit_bn254_dev equals its host restatement (oracle/prover_cpu.cpp
+    oracle_synth_circuit), which generates the 2^24-gate fixture's circuit."""
+    import torch
+
+    import oracle
+
+    n = 1 << 12
+    dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
+    dc = torch.empty(3 * n * 2, dtype=torch.int64, device="cuda")
+    dabc = torch.empty(3 * n * 4, dtype=torch.int64, device="cuda")
+    ctx.plonk_synth_circuit_dev(n, 0x5EED0024, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr())
+    torch.cuda.synchronize()
+    q, c, abc = oracle.synth_circuit(n, 0x5EED0024)
+    for dev, host in ((dq, q), (dc, c), (dabc, abc)):
+        assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+
+
 def test_prove_2p24_gates(ctx):
-    """BASELINE config 5 at its own size on one GPU: 2^24 gates, paper mode. The prover's
-    built-in checks (constraints satisfied, the accumulator's product = 1, t(x) divisible by
-    Z_H with coefficients 3n+6.. zero, zero remainders of W_z / W_zw: plonk.rs:199, 307,
-    370, 438, 442) pass, the proof verifies, and a changed evaluation or two swapped
-    commitments are rejected. (The O(n) Python checker of test_prove_2p20_gates is not run
-    at this size: 16x its ~30 s.)"""
+    """BASELINE config 5 at its own size on one GPU: 2^24 gates, paper mode. The proof is
+    pinned exactly: its 7 field elements and all 9 commitments against the scalars the O(n)
+    checker computed in the container for the same seeded circuit, SRS secret, challenges and
+    blinders (tests/golden/prove_2p24.json, tests/golden/gen_prove_2p24.py:
+    oracle_commitment_scalars = oracle/plonk_bn254.py commitment_scalars restated in C++).
+    The prover's built-in checks (constraints satisfied, t(x) divisible by Z_H with
+    coefficients 3n+6.. zero, zero remainders of W_z / W_zw: plonk.rs:199, 370, 438, 442) pass,
+    the proof verifies, and a changed evaluation or two swapped commitments are rejected."""
     import torch
 
     n = 1 << 24
@@ -138,6 +158,19 @@ def test_prove_2p24_gates(ctx):
     pts, fs = ctx.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(),
                                         srs_m, mode=1, stream=sp)
     torch.cuda.synchronize()
+    import json
+    import os
+
+    import pbf
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "prove_2p24.json")) as fh:
+        gold = json.load(fh)
+    assert (gold["log_n"], gold["seed"], int(gold["s"])) == (24, 0x5EED0024, s)
+    assert [int(x) for x in gold["chal"]] == chal and [int(x) for x in gold["rnd"]] == rnd
+    assert pbf.limbs_to_ints(fs) == [int(x) for x in gold["paper"]["fields"]]
+    cs = {k: int(v) for k, v in gold["paper"].items() if k != "fields"}
+    res = P.commitments_match(n, _points(pts), cs, s, chal[3])
+    assert all(res.values()), res
     verify = lambda p, f: ctx.plonk_verify_bn254_dev(  # noqa: E731
         n, dq.data_ptr(), dc.data_ptr(), dsrs.data_ptr(), srs_m, g2s, p, f, chal, u, mode=1, stream=sp)
     assert verify(pts, fs)
