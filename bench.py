@@ -29,12 +29,13 @@ import pbf  # noqa: E402
 
 GOLD = pbf.GOLDILOCKS
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# BN254 Fq Montgomery products/s of the whole chip at the instruction level: a product is
-# 136 v_mad_u64_u32 + 136 carry folds (csrc/fp256.hpp), 4 cycles per wave-instruction each
-# (profiles/r02/valu_rates.log), 64 lanes, 1024 SIMDs at 2.4 GHz. (scripts/ubench/
-# pairing_lat.hip k_tput measures 1.0e11 with two chains per lane; the MSM accumulation
-# reaches 1.2e11, so the measured figure is not the ceiling.)
-FQ_MUL_PEAK = 1024 * 2.4e9 * 64 / (272 * 4)
+# Ceiling of 254-bit Montgomery products/s on the chip, from the hardware, not from our own
+# kernels' instruction counts: v_mad_u64_u32 (32 x 32 + 64 -> 64) issues once per 4 cycles per
+# SIMD (profiles/r02/valu_rates.log), 1024 SIMDs x 64 lanes at 2.4 GHz = 3.93e13 mads/s, and a
+# Montgomery product of 8 x 32-bit limbs needs at least 136 of them (64 for a b, 64 for m p,
+# 8 for the m digits), every other instruction free: 2.89e11 products/s.
+MAD_RATE = 1024 * 64 * 2.4e9 / 4
+FQ_MUL_PEAK = MAD_RATE / 136
 
 
 BUFFER_SETS = 3  # input/output pairs the NTT steps rotate over
@@ -92,9 +93,14 @@ def cpu_baselines_bn254() -> dict:
       config 4: SRS::eval_at_s (plonk.rs:51-58), the naive fold of affine double-and-add
                 products, on 2^12 points, one core -> linear to 2^20 (x256); and an all-core
                 Pippenger at the full 2^20 points (not extrapolated);
-      config 5: Plonk::prove (plonk.rs:191-466, literal: O(n^2) Vandermonde interpolation, long
-                division) in the Python restatement at n = 8, not extrapolated (its cost grows
-                as n^3; no C++ restatement of the whole prover exists yet)."""
+      config 3 (all cores): the same product with the iterative radix-2 NTT on all the job's
+                cores, measured at the full 2^22 x 2^22 (oracle_fr_mul_ntt_par);
+      config 4 (pairing): the 2-pair KZG pairing check of plonk.rs:646-650 in the Python
+                restatement (oracle/bn254_pairing.py, optimal ate, one core);
+      config 5: the generalised C++ prover (oracle/prover_cpu.cpp oracle_plonk_prove_cpu: the GPU
+                prover's O(n log n) algorithms, 4 x u64 Montgomery, every step per proof) at 2^14
+                gates on one core and on all cores, extrapolated n log n to 2^20 (x91.4) and 2^24
+                (x1755); and the literal Python Plonk::prove (O(n^3) interpolation) at n = 8."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import random as _r
 
@@ -139,6 +145,45 @@ def cpu_baselines_bn254() -> dict:
     out["config4_msm_2p20_pippenger_all_cores"] = {
         "ms": t * 1e3, "unit": "ms (measured at 2^20 points)", "cores": threads, "kind": "port",
         "sample": "Pippenger, 16-bit windows, XYZZ buckets, one window per thread, oracle_g1_msm_pippenger"}
+    # config 3, all cores, at its own size (iterative NTT)
+    la3 = 1 << 22
+    a3, b3 = rand_fr(la3), rand_fr(la3)
+    w3 = bn254.root_of_unity(2 * la3)
+    t0 = time.perf_counter()
+    oracle.fr_mul_ntt_par(a3, b3, w3, threads=threads)
+    t = time.perf_counter() - t0
+    out["config3_polymul_2p22_all_cores"] = {"ms": t * 1e3, "unit": "ms (measured at 2^22 x 2^22)", "cores": threads,
+                                             "kind": "port",
+                                             "sample": "oracle_fr_mul_ntt_par: iterative radix-2 NTT, butterflies of "
+                                                       "each stage split over the threads"}
+    del a3, b3
+    # config 4: the 2-pair pairing check, Python restatement, one core
+    import bn254_pairing as BP
+
+    G2 = BP.G2_GEN
+    t0 = time.perf_counter()
+    ok = BP.pairing_check([(BP.G1_GEN, G2), (BP.g1_neg(BP.G1_GEN), G2)])
+    t = time.perf_counter() - t0
+    out["config4_pairing_check"] = {"ms": t * 1e3, "unit": "ms (measured)", "cores": 1, "kind": "port", "ok": ok,
+                                    "sample": "e(G, H) e(-G, H) == 1 by oracle/bn254_pairing.py pairing_check "
+                                              "(Python big integers: optimal-ate Miller loops + one final exp)"}
+    # config 5: the generalised C++ prover at 2^14 gates, 1 core and all cores
+    n5 = 1 << 14
+    q5, c5, abc5 = oracle.synth_circuit(n5, 0x5EED0005, threads=threads)
+    srs5 = oracle.g1_progression(0x5EED0005C0FFEE, 0x1234567, n5 + 3)  # any points: timing only
+    chal5 = [0x1111 * (i + 3) for i in range(5)]
+    rnd5 = [0x2222 * (i + 5) for i in range(9)]
+    f20 = (20 * (1 << 20)) / (14 * n5)
+    f24 = (24 * (1 << 24)) / (14 * n5)
+    for label, th in (("1_core", 1), ("all_cores", threads)):
+        t0 = time.perf_counter()
+        oracle.plonk_prove_cpu(n5, q5, c5, abc5, chal5, rnd5, srs5, mode=1, threads=th)
+        t = time.perf_counter() - t0
+        out[f"config5_prove_cpp_{label}"] = {
+            "ms_2p14": t * 1e3, "ms_2p20": t * f20 * 1e3, "ms_2p24": t * f24 * 1e3, "cores": th, "kind": "port",
+            "unit": "ms per proof (2^14 measured; 2^20 / 2^24 extrapolated n log n: x91.4 / x1755)",
+            "sample": "oracle/prover_cpu.cpp oracle_plonk_prove_cpu (NTT interpolation and quotient, prefix-product "
+                      "accumulator, synthetic-division openings, Pippenger commitments; no proving key), mode 1"}
     prov = {}
     r2 = _r.Random(0x5EED0003)
     for n in (8,):
@@ -510,8 +555,8 @@ def other_configs(ctx, sp) -> dict:
         ach = fq_products / (ms / 1e3)
         return {"bound": "valu (Fq products)", "achieved": ach, "peak": FQ_MUL_PEAK, "unit": "Fq products/s",
                 "frac": ach / FQ_MUL_PEAK, "fq_products": fq_products,
-                "peak_source": "instruction count: 272 four-cycle VALU per Fq product, 1024 SIMDs x 64 lanes "
-                               "at 2.4 GHz (k_tput measures 1.0e11; the accumulation kernel alone reaches 1.2e11)"}
+                "peak_source": "hardware: v_mad_u64_u32 at 1 per 4 cycles per SIMD (1024 SIMDs x 64 lanes x "
+                               "2.4 GHz = 3.93e13 mads/s) / 136 mads, the minimum of an 8 x 32-bit Montgomery product"}
 
     res["config4_bn254_msm_2p20"] = dict(t, points_per_s=m / (t["ms"] / 1e3), roofline=msm_roof(t["ms"]),
                                          note="Pippenger c=16, 16 windows (bucket accumulation, window sums, "

@@ -268,7 +268,7 @@ int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t* d_q, cons
  * rank's point range, the partial sums all-gathered once at the end. The circuit's proving key
  * is built once per circuit on every rank. Outputs are identical on every rank and
  * bit-identical to the single-GPU proof. n >= world^2. send / recv: device buffers of
- * `capacity` >= 9 * (4n / world) * 32 bytes each.                                          */
+ * `capacity` >= 5 * (4n / world) * 32 bytes each.                                          */
 typedef struct pbf_comm {
   uint32_t world, rank;
   void* user;

@@ -530,7 +530,7 @@ int pbf_plonk_prove_bn254_multi_dev(pbf_ctx* const* ctxs, uint32_t world, size_t
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
-  if ((rc = g->ensure((size_t)9 * (4 * n / world) * 32))) return rc;
+  if ((rc = g->ensure((size_t)5 * (4 * n / world) * 32))) return rc;
   std::vector<uint64_t> pts((size_t)world * 72), fs((size_t)world * 28);
   rc = g->run([&](uint32_t r) {
     const pbf_comm c = g->comm(r);

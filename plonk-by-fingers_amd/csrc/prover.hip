@@ -164,6 +164,26 @@ __global__ void k_sigma(const uint64_t* copies, const uint64_t* hpow, uint64_t n
   u256_to_u64(h, sigma + 4 * id);
 }
 
+// k_sigma for the blocked rows of a sharded NTT's rank r: out[col][q Sn + kk] = sigma of row
+// q B + r Sn + kk (B = n / G, Sn = B / G), the evaluation layout pbf_ntt_fr256_shard_* use
+__global__ void k_sigma_blk(const uint64_t* copies, const uint64_t* hpow, uint64_t n, uint64_t B, uint64_t Sn,
+                            uint64_t r, U256 k1, U256 k2, uint64_t* out, int* bad) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * B) return;
+  const uint64_t col = t / B, p = t % B;
+  const uint64_t row = (p / Sn) * B + r * Sn + p % Sn;
+  const uint64_t kind = copies[2 * (col * n + row)], idx = copies[2 * (col * n + row) + 1];
+  if (kind > 2 || idx < 1 || idx > n) {
+    *bad = 1;
+    for (int k = 0; k < 4; ++k) out[4 * t + k] = 0;
+    return;
+  }
+  U256 h = u256_from_u64(hpow + 4 * (idx - 1));
+  if (kind == 1) h = Fr::mul_tp(h, k1);
+  if (kind == 2) h = Fr::mul_tp(h, k2);
+  u256_to_u64(h, out + 4 * t);
+}
+
 // Constrains::satisfies (constraints.rs:198-230, with its q_l * b term): gates and copies
 __global__ void k_satisfies(const uint64_t* q, const uint64_t* abc, const uint64_t* copies, uint64_t n, uint64_t row0,
                             uint64_t rows, int* bad) {
@@ -1077,34 +1097,59 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   PBF_HIP(hipGetLastError());
   if ((rc = P.agree("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
   P.mark("satisfies (rows)");
-  // ---- h = w^i (all of H: copy labels point anywhere), l1 = n^-1 (1 + x + ... + x^(n-1))
+  // ---- h = w^i (all of H: copy labels point anywhere)
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, P.omega, one);
-  const U256 ninv = hinvm(hm64(n));
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, n, one, ninv);
   PBF_HIP(hipGetLastError());
-  // ---- proving key: the circuit's 8 polynomials (full coefficients on every rank) and this
-  // rank's blocks of their 9 coset evaluations; once per circuit (every proof without the key)
+  const U256 ninv = hinvm(hm64(n));
+  // ---- proving key, sharded like the witness (once per circuit; every proof without the key):
+  // the 8 circuit polynomials by one sharded INTT of their blocked evaluations (q columns, sigma
+  // labels of the blocked rows), their coset blocks from the SS coefficients, their CR ranges by
+  // transposes; l1 = n^-1 (1 + x + ... + x^(n-1)) is n^-1 in every slot of both layouts
   if (!pk_hit) {
-    uint64_t* sigma = (uint64_t*)B.sigma.p;
-    hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, n,
-                       (uint64_t)0, n, k1, k2, sigma, P.d_bad);
+    DevBuf& pkb = ctx->buf("pv.pkb");
+    if ((rc = pkb.ensure(2 * 8 * Bn * E))) return rc;
+    uint64_t* Xk = (uint64_t*)pkb.p;
+    uint64_t* Yk = Xk + 4 * 8 * Bn;
+    for (int k = 0; k < 5; ++k)
+      PBF_HIP(hipMemcpy2DAsync(Xk + 4 * Bn * k, Sn * E, d_q + 4 * (n * k + r * Sn), Bn * E, Sn * E, G,
+                               hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_sigma_blk, dim3(blocks_for(3 * Bn)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, n, Bn,
+                       Sn, r, k1, k2, Xk + 4 * Bn * 5, P.d_bad);
     PBF_HIP(hipGetLastError());
-    for (int k = 3; k < 11; ++k) PBF_HIP(hipMemsetAsync(C(k), 0, CS * E, s));
-    for (int k = 0; k < 5; ++k) PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
-    for (int k = 0; k < 3; ++k) PBF_HIP(hipMemcpyAsync(C(8 + k), sigma + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
-    for (int k = 3; k < 11; ++k)
-      if ((rc = P.ntt(P.w_plain, C(k), C(k), n, 1, 1))) return rc;
-    const uint64_t* srcs[9];
-    uint64_t lens[9];
-    U256 bases[9];
-    for (int k = 0; k < 8; ++k) { srcs[k] = C(3 + k); lens[k] = n; bases[k] = P.g; }
-    srcs[8] = l1; lens[8] = n; bases[8] = P.g;
-    if ((rc = P.coset_ntt_batch(9, srcs, lens, bases, CE(4), QUOT_DEG + 4))) return rc;
     if ((rc = P.agree("copy constraint label out of range (plonk.rs:181-189)"))) return rc;
-    if (pk_on) {
-      ctx->pk_key = pk_key;
-      B.sigma.release();  // the full label table is only needed to build the key
+    if ((rc = pbf_ntt_fr256_shard_combine_dev(ctx, P.w_plain, (uint32_t)G, (uint32_t)r, Xk, send, Bn, 8, 1, s))) return rc;
+    if ((rc = P.a2a(8 * Sn * E))) return rc;
+    if ((rc = pbf_ntt_fr256_shard_local_dev(ctx, P.w_plain, (uint32_t)G, recv, Yk, Bn, 8, 1, s))) return rc;
+    uint64_t* l1_ss = Xk;  // the blocked evaluations are consumed
+    hipLaunchKernelGGL(k_powers, dim3(blocks_for((Bn + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1_ss, Bn, one,
+                       ninv);
+    PBF_HIP(hipGetLastError());
+    const uint64_t lens[5] = {n, n, n, n, n};
+    const U256 bases[5] = {P.g, P.g, P.g, P.g, P.g};
+    const uint64_t* ss1[5] = {Yk, Yk + 4 * Bn, Yk + 8 * Bn, Yk + 12 * Bn, Yk + 16 * Bn};  // q_l q_r q_o q_m q_c
+    if ((rc = P.coset_ntt_ss(5, ss1, lens, bases, CE(4), QUOT_DEG + 4))) return rc;
+    const uint64_t* ss2[4] = {Yk + 20 * Bn, Yk + 24 * Bn, Yk + 28 * Bn, l1_ss};  // s1 s2 s3 l1
+    if ((rc = P.coset_ntt_ss(4, ss2, lens, bases, CE(9), QUOT_DEG + 9))) return rc;
+    for (int k0 = 0; k0 < 8; k0 += 3) {
+      const int np = std::min(3, 8 - k0);
+      const uint64_t* ss[3];
+      uint64_t* cr[3];
+      uint64_t off[3], len[3];
+      for (int i = 0; i < np; ++i) {
+        ss[i] = Yk + 4 * Bn * (k0 + i); cr[i] = C(3 + k0 + i); off[i] = 0; len[i] = n;
+      }
+      if ((rc = P.xpose(np, ss, Bn, off, len, cr))) return rc;
     }
+    pkb.release();
+    if (pk_on) ctx->pk_key = pk_key;
+  }
+  {  // l1's CR range: n^-1 for j < n
+    PBF_HIP(hipMemsetAsync(l1, 0, CRS * E, s));
+    const uint64_t cnt = P.cr_count(n);
+    if (cnt)
+      hipLaunchKernelGGL(k_powers, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, cnt, one,
+                         ninv);
+    PBF_HIP(hipGetLastError());
   }
   P.mark(pk_hit ? "proving key (cached)" : "proving key (built)");
 
@@ -1292,7 +1337,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   {
     const uint64_t* polys[10] = {abc_cr, abc_cr + 4 * CRS, abc_cr + 8 * CRS, C(8), C(9), t_cr, t_cr + 4 * CRS,
                                  t_cr + 8 * CRS, z_cr, l1};
-    const bool full[10] = {false, false, false, true, true, false, false, false, false, true};
+    const bool full[10] = {false, false, false, false, false, false, false, false, false, false};
     const uint64_t lens[10] = {n + 2, n + 2, n + 2, n, n, m, m, m, n + 3, n};
     const U256 xs[10] = {zc, zc, zc, zc, zc, zc, zc, zc, zw, zc};
     if ((rc = eval(10, polys, full, lens, xs, ev))) return rc;
@@ -1336,7 +1381,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   }
   {
     const uint64_t* in[7] = {C(6), C(3), C(4), C(5), C(7), z_cr, mode == 1 ? C(10) : r3_cr};
-    const bool full[7] = {true, true, true, true, true, false, mode == 1};
+    const bool full[7] = {false, false, false, false, false, false, false};
     const uint64_t lens[7] = {n, n, n, n, n, n + 3, mode == 1 ? n : 2 * n + 2};
     const U256 c[7] = {Fr::mul(a_z, b_z), a_z, b_z, c_z, one, Fr::add(K2, K4),
                        mode == 1 ? Fr::sub(u256_zero(), Fr::mul(Fr::mul(beta, zw_z), K3))
@@ -1360,7 +1405,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   {
     const uint64_t* in[9] = {t_cr, t_cr + 4 * CRS, t_cr + 8 * CRS, rx, abc_cr, abc_cr + 4 * CRS, abc_cr + 8 * CRS,
                              C(8), C(9)};
-    const bool full[9] = {false, false, false, false, false, false, false, true, true};
+    const bool full[9] = {false, false, false, false, false, false, false, false, false};
     const uint64_t lens[9] = {m, m, m, rlen, n + 2, n + 2, n + 2, n, n};
     const U256 c[9] = {one, hpow64(zc, n + 2), hpow64(zc, 2 * n + 4), vp[1], vp[2], vp[3], vp[4], vp[5], vp[6]};
     U256 cst = Fr::add(t_z, Fr::mul(vp[1], r_z));
@@ -1435,10 +1480,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     P.B = n / G;
     P.Ls = mode == 0 ? 2 * (uint64_t)n : (uint64_t)n;  // mode 0's r(x) and W_z reach x^(2n+1)
     P.Bc = P.Ls / G;
-    // the largest exchange: the proving key's 9 coset NTTs of 4n / world points per rank
-    if (comm->capacity < 9 * P.nl * 32) return fail(PBF_EINVAL, "comm buffers below 9 * (4n / world) * 32 bytes");
+    // the largest exchange: 5 coset NTTs of 4n / world points per rank (a b c z z(w x); the key's
+    // 9 go as 5 + 4)
+    if (comm->capacity < 5 * P.nl * 32) return fail(PBF_EINVAL, "comm buffers below 5 * (4n / world) * 32 bytes");
     P.shard = &ctx->buf("pv.shard");
-    int rc0 = P.shard->ensure(9 * P.nl * 32);
+    int rc0 = P.shard->ensure(5 * P.nl * 32);
     if (rc0) return rc0;
   }
   const hipStream_t s = P.s;
@@ -1478,7 +1524,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
     DevBuf& kc = ctx->buf("pk.coef");
     DevBuf& ks = ctx->buf("pk.coset");
-    if ((rc = kc.ensure(8 * CS * E)) || (rc = ks.ensure(9 * P.count() * E))) return rc;
+    if ((rc = kc.ensure(8 * (P.G > 1 ? P.CRS() : CS) * E)) || (rc = ks.ensure(9 * P.count() * E))) return rc;
     pkcoef = (uint64_t*)kc.p;
     pkcoset = (uint64_t*)ks.p;
     pk_hit = ctx->pk_key == pk_key;
@@ -1488,9 +1534,10 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // on every rank); the witness-dependent vectors live in this rank's SS / CR pieces ("pv.sh")
   const bool sharded = P.G > 1;
   const uint64_t n_full = sharded ? 0 : n;
-  if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure((sharded && pk_hit ? 0 : 3 * n) * E)) ||
-      (rc = B.coef.ensure((sharded ? (pk_on ? 0 : 11) : 11) * (n + 8) * E)) || (rc = B.acc.ensure((n_full + 8) * E)) ||
-      (rc = B.tmp0.ensure(n * E)) || (rc = B.tmp1.ensure((n_full + 8) * E)) ||
+  if ((rc = B.hpow.ensure(n * E)) || (rc = B.sigma.ensure((sharded ? 0 : 3 * n) * E)) ||
+      (rc = B.coef.ensure(sharded ? (pk_on ? 0 : 11 * P.CRS() * E) : 11 * (n + 8) * E)) ||
+      (rc = B.acc.ensure((n_full + 8) * E)) || (rc = B.tmp0.ensure((sharded ? P.CRS() : n) * E)) ||
+      (rc = B.tmp1.ensure((n_full + 8) * E)) ||
       (rc = B.tmp2.ensure((n / SCAN_BLK + 2) * E)) || (rc = B.coset.ensure((pk_on ? 5 : 14) * P.count() * E)) ||
       (rc = B.t.ensure((sharded ? 8 : N) * E)) || (rc = B.work.ensure((sharded ? 8 : 3 * N) * E)) ||
       (rc = B.flag.ensure(64)) || (rc = B.evals.ensure(16 * E)))
@@ -1516,7 +1563,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* coef = (uint64_t*)B.coef.p;
   // slots: 0 a, 1 b, 2 c, 3 q_l, 4 q_r, 5 q_o, 6 q_m, 7 q_c, 8 s1, 9 s2, 10 s3 (3.. in the proving key)
   uint64_t* cslot[11];
-  for (int k = 0; k < 11; ++k) cslot[k] = (pk_on && k >= 3) ? pkcoef + 4 * CS * (k - 3) : coef + 4 * CS * k;
+  const uint64_t cstride = sharded ? P.CRS() : CS;  // sharded: the circuit polynomials' CR ranges
+  for (int k = 0; k < 11; ++k) cslot[k] = (pk_on && k >= 3) ? pkcoef + 4 * cstride * (k - 3) : coef + 4 * cstride * k;
   auto C = [&](int k) { return cslot[k]; };
   uint64_t* coset = (uint64_t*)B.coset.p;
   const uint64_t NE = P.count();  // coset evaluations held here (N; nl = N / G when sharded)

@@ -351,7 +351,7 @@ class ShardedProver:
         self.ctx, self.comm, self.rank, self.world, self.n = ctx, comm, rank, world, n
         self.stream = stream
         nl = 4 * n // world
-        self.words = 9 * nl * 4  # 9 * nl Fr elements of 4 int64 words (pbf.h: the key's 9 coset NTTs)
+        self.words = 5 * nl * 4  # 5 * nl Fr elements of 4 int64 words (pbf.h: 5 coset NTTs per exchange)
         self.send = torch.empty(self.words, dtype=torch.int64, device=device)
         self.recv = torch.empty(self.words, dtype=torch.int64, device=device)
         cb = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
