@@ -134,7 +134,67 @@ def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True, no_k
     return out
 
 
+def throughput(log_n: int, streams: int, proofs: int = 8, mode: int = 1) -> dict:
+    """Proofs/s with `streams` proofs in flight: one context, torch stream and host thread each
+    (a prover serving many witnesses of one circuit), all reading the same device-resident
+    circuit, witness and SRS. Every context warms up first (plans, proving key, SRS window
+    table); then each thread runs `proofs` proofs back to back, and the wall time from the
+    common start to the last proof's completion gives the rate. The proofs of all threads must
+    be identical (same inputs)."""
+    import threading
+
+    n = 1 << log_n
+    base = pbf.Context(0)
+    sp = torch.cuda.current_stream().cuda_stream
+    dq = torch.empty(5 * n * 4, dtype=torch.int64, device="cuda")
+    dc = torch.empty(3 * n * 2, dtype=torch.int64, device="cuda")
+    dabc = torch.empty(3 * n * 4, dtype=torch.int64, device="cuda")
+    base.plonk_synth_circuit_dev(n, 0x5EED0005, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), stream=sp)
+    srs_m = (n + 3) if mode == 1 else (2 * n + 2)
+    dsrs = torch.empty(srs_m * 8, dtype=torch.int64, device="cuda")
+    base.srs_create_dev(0x5EED0005C0FFEE, srs_m - 1, dsrs.data_ptr(), stream=sp)
+    torch.cuda.synchronize()
+    base.close()
+    chal = [0x1111 * (i + 3) for i in range(5)]
+    rnd = [0x2222 * (i + 5) for i in range(9)]
+    ctxs = [pbf.Context(0) for _ in range(streams)]
+    sts = [torch.cuda.Stream() for _ in range(streams)]
+    results = [None] * streams
+    go = threading.Barrier(streams + 1)
+
+    def prove(k):
+        return ctxs[k].plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd,
+                                             dsrs.data_ptr(), srs_m, mode=mode, stream=sts[k].cuda_stream)
+
+    def worker(k):
+        prove(k)  # warm-up
+        sts[k].synchronize()
+        go.wait()
+        for _ in range(proofs):
+            results[k] = prove(k)  # returns after the proof's points and fields reached the host
+        sts[k].synchronize()
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(streams)]
+    for t in ts:
+        t.start()
+    go.wait()
+    t0 = time.perf_counter()
+    for t in ts:
+        t.join()
+    wall = time.perf_counter() - t0
+    same = all(np.array_equal(results[0][0], r[0]) and np.array_equal(results[0][1], r[1]) for r in results)
+    for c in ctxs:
+        c.close()
+    return {"log_n": log_n, "streams": streams, "proofs": streams * proofs, "wall_s": wall,
+            "proofs_per_s": streams * proofs / wall, "ms_per_proof": wall / (streams * proofs) * 1e3,
+            "identical_proofs": bool(same)}
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--throughput":  # --throughput LOG_N K [K ...]
+        for k in sys.argv[3:]:
+            print(json.dumps(throughput(int(sys.argv[2]), int(k))), flush=True)
+        sys.exit(0)
     ctx = pbf.Context(0)
     for a in sys.argv[1:]:
         print(json.dumps(run(ctx, int(a))), flush=True)
