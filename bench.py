@@ -606,6 +606,12 @@ def other_configs(ctx, sp) -> dict:
     # W_z commitment); its honest proofs do not verify, so no verify here
     res["config5_prove_2p20_mode0"] = bench_prover.run(ctx, 20, reps=5, mode=0, verify=False, no_key=False)
     ctx.release_caches()
+    # proofs/s with four proofs in flight (one context + stream + host thread each)
+    try:
+        res["config5_prove_2p20_4_streams"] = bench_prover.throughput(20, 4)
+    except Exception as e:
+        res["config5_prove_2p20_4_streams"] = {"error": repr(e)}
+    torch.cuda.empty_cache()
     torch.cuda.empty_cache()
     # config 5 at its own size on one GPU (the 8-GPU sharded run is the driver's N > 1 bench)
     try:

@@ -173,6 +173,7 @@ struct pbf_ctx {
   struct FixedBase {
     bool valid = false;  // built from the points in snapshot "fx.pts" (msm.hip snapshot_check)
     uint64_t n = 0;
+    int c = 16;  // window bits of the table (msm.hip FxGeom): ceil(255 / c) windows of n points
     pbf::DevBuf table;
     pbf::DevBuf inf;  // per point: 1 = the identity (contributes nothing)
   } fixed_base;

@@ -119,7 +119,10 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
 constexpr uint32_t MSM_CH = PBF_MSM_CH;  // sorted entries per accumulation thread
 
 struct ChunkPart {
-  Xyzz acc;
+  union {
+    Xyzz acc;
+    uint32_t raw[36];  // msm_chunk_acc_l29r's unconverted accumulator (msm_l29_finish converts it)
+  };
   uint32_t key;  // the sentinel key: no partial
   uint32_t pad[3];
 };
@@ -131,12 +134,14 @@ struct ChunkPart {
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE))) msm_chunk_acc(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
                                                      const uint32_t* start, const uint32_t* end, uint32_t m,
                                                      Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent,
-                                                     const uint32_t* m_dev) {
+                                                     const uint32_t* m_dev, uint32_t* hkey, uint32_t* tkey) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c0 = t * MSM_CH;
   if (c0 >= m) return;  // past the chunks of the m-entry list
   head[t].key = sent;
   tail[t].key = sent;
+  hkey[t] = sent;
+  tkey[t] = sent;
   // m_dev: the valid length, known on the device only (counting sort: no sentinel entries)
   const uint32_t mv = m_dev ? *m_dev : m;
   if (c0 >= mv) return;
@@ -149,9 +154,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
     if (bs < rs) {  // continues a bucket of an earlier chunk (possibly spanning this one)
       head[t].acc = acc;
       head[t].key = cur;
+      hkey[t] = cur;
     } else if (be > re) {  // starts here, ends in a later chunk
       tail[t].acc = acc;
       tail[t].key = cur;
+      tkey[t] = cur;
     } else {
       buckets[cur] = acc;
     }
@@ -196,12 +203,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MS
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE)))
 msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
                   const uint32_t* end, uint32_t m, Xyzz* buckets, ChunkPart* head, ChunkPart* tail, uint32_t sent,
-                  const uint32_t* m_dev) {
+                  const uint32_t* m_dev, uint32_t* hkey, uint32_t* tkey) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c0 = t * MSM_CH;
   if (c0 >= m) return;
   head[t].key = sent;
   tail[t].key = sent;
+  hkey[t] = sent;
+  tkey[t] = sent;
   const uint32_t mv = m_dev ? *m_dev : m;
   if (c0 >= mv) return;
   const uint32_t c1 = c0 + MSM_CH < mv ? c0 + MSM_CH : mv;
@@ -215,9 +224,11 @@ msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
     if (bs < rs) {
       head[t].acc = v;
       head[t].key = cur;
+      hkey[t] = cur;
     } else if (be > re) {
       tail[t].acc = v;
       tail[t].key = cur;
+      tkey[t] = cur;
     } else {
       buckets[cur] = v;
     }
@@ -252,8 +263,105 @@ msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
   }
   flush(c1);
 }
+// msm_chunk_acc_l29 with the flush deferred (round 4, default; PBF_MSM_RAWFLUSH=0 selects the
+// kernel above): a flush stores the raw 29-bit-limb accumulator (l29::store_raw, 144 B, no
+// products) -- into braw[key] for a run complete in this chunk, head[t].raw / tail[t].raw for
+// a partial -- and msm_l29_finish converts them afterwards. Lanes of a wave reach their run
+// boundaries at different entries; with the conversion (4 products) inside the loop, a wave
+// executed it at every entry where any lane flushed: with ~100 entries per bucket (wide
+// fixed-base windows, the windowed form) that is most entries. hkey[t] / tkey[t]: the key of
+// chunk t's head / tail partial (the sentinel: none), compact for the join and the finish.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE)))
+msm_chunk_acc_l29r(const Affine* pts, const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
+                   const uint32_t* end, uint32_t m, uint32_t* braw, ChunkPart* head, ChunkPart* tail, uint32_t sent,
+                   const uint32_t* m_dev, uint32_t* hkey, uint32_t* tkey) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c0 = t * MSM_CH;
+  if (c0 >= m) return;
+  hkey[t] = sent;
+  tkey[t] = sent;
+  const uint32_t mv = m_dev ? *m_dev : m;
+  if (c0 >= mv) return;
+  const uint32_t c1 = c0 + MSM_CH < mv ? c0 + MSM_CH : mv;
+  uint32_t cur = keys[c0], rs = c0;
+  l29::Acc acc;
+  acc.id = true;
+  if (cur == sent) return;
+  auto flush = [&](uint32_t re) {
+    const uint32_t bs = start[cur], be = end[cur];
+    uint32_t* dst;
+    if (bs < rs) {
+      dst = head[t].raw;
+      hkey[t] = cur;
+    } else if (be > re) {
+      dst = tail[t].raw;
+      tkey[t] = cur;
+    } else {
+      dst = braw + 36ull * cur;
+    }
+    l29::store_raw(acc, dst);
+  };
+  uint32_t k_nx = cur, v_nx = vals[c0];
+  Affine p_nx = pts[v_nx & ~MSM_NEG];
+  uint32_t k_n2 = 0, v_n2 = 0;
+  if (c0 + 1 < c1) k_n2 = keys[c0 + 1], v_n2 = vals[c0 + 1];
+  for (uint32_t j = c0; j < c1; ++j) {
+    const uint32_t k = k_nx, v = v_nx;
+    Affine p = p_nx;
+    if (j + 1 < c1) {
+      k_nx = k_n2;
+      v_nx = v_n2;
+      p_nx = pts[v_nx & ~MSM_NEG];
+      if (j + 2 < c1) k_n2 = keys[j + 2], v_n2 = vals[j + 2];
+    }
+    if (k != cur) {
+      flush(j);
+      if (k == sent) return;
+      cur = k;
+      rs = j;
+      acc.id = true;
+    }
+    if (v & MSM_NEG) p.y = Fq::sub(u256_zero(), p.y);
+    if (l29::madd(acc, l29::from_u256(p.x), l29::from_u256(p.y))) {
+      Affine q = pts[v & ~MSM_NEG];
+      if (v & MSM_NEG) q.y = Fq::sub(u256_zero(), q.y);
+      acc = l29::from_xyzz(G1::mdbl(q));
+    }
+  }
+  flush(c1);
+}
+// The conversions msm_chunk_acc_l29r deferred, one per stored sum, every lane busy: buckets
+// complete inside one chunk (start and end in the same chunk: the ones fx_bucket reads from
+// `buckets`), then every head and tail partial with a key, converted in place.
+__global__ void __launch_bounds__(256) msm_l29_finish(const uint32_t* braw, Xyzz* buckets, ChunkPart* head,
+                                                      ChunkPart* tail, const uint32_t* hkey, const uint32_t* tkey,
+                                                      const uint32_t* start, const uint32_t* end, uint32_t nb,
+                                                      uint32_t nchunks, uint32_t sent) {
+  const uint64_t items = (uint64_t)nb + 2ull * nchunks;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i < nb) {
+      const uint32_t bs = start[i], be = end[i];
+      if (be > bs && bs / MSM_CH == (be - 1) / MSM_CH) buckets[i] = l29::raw_to_xyzz(braw + 36 * i);
+    } else if (i < (uint64_t)nb + nchunks) {
+      const uint64_t t = i - nb;
+      if (hkey[t] != sent) head[t].acc = l29::raw_to_xyzz(head[t].raw);
+    } else {
+      const uint64_t t = i - nb - nchunks;
+      if (tkey[t] != sent) tail[t].acc = l29::raw_to_xyzz(tail[t].raw);
+    }
+  }
+}
 static bool msm_l29() {
   return env_default_on("PBF_MSM_L29");  // read per call: an A/B knob
+}
+// deferred flush conversion: the default where runs are short (the windowed form, fixed-base
+// windows wider than 16 bits: ~30-200 entries per bucket); the c = 16 fixed-base form (~500+
+// per bucket) flushes rarely, and the separate conversion pass costs it more than it saves
+// (2^24 points: 32.5 against 32.0 ms). PBF_MSM_RAWFLUSH=0/1 forces either (A/B).
+static bool msm_rawflush(bool short_runs = true) {
+  const char* e = getenv("PBF_MSM_RAWFLUSH");  // read per call: an A/B knob
+  if (e) return atoi(e) != 0;
+  return short_runs;
 }
 
 // ---------------------------------------------------------------- fixed-base MSM
@@ -272,11 +380,46 @@ static bool msm_l29() {
 constexpr int FX_C = 16, FX_NW = 16;
 constexpr uint32_t FX_NB = 1u << (FX_C - 1);  // buckets (|d| - 1, |d| <= 2^(FX_C-1))
 static_assert(FX_C * FX_NW >= 255, "windows must cover a 254-bit scalar plus the recoding carry");
+// Round 4: the window width of a table is chosen by its size (FxGeom, fx_geom). c-bit signed
+// digits need ceil(255 / c) windows (a 254-bit scalar plus the recoding carry) and 2^(c-1)
+// buckets, so the accumulation performs ceil(255 / c) n mixed additions: 16 n at c = 16,
+// 13 n at c = 20, 12 n at c = 22. The wider windows pay for it with a third sort pass, more
+// buckets to reduce (2^(c-1)) and fewer entries per bucket (more flushes), which a large table
+// amortises and a small one does not.
+struct FxGeom {
+  int c = FX_C, nw = FX_NW;  // window bits, windows
+  uint32_t nb = FX_NB;       // buckets, 2^(c-1)
+  int lb = 8, hb = 7;        // bucket b = 2^lb h + l (l < 2^lb, h < 2^hb), lb + hb = c - 1
+};
+static FxGeom fx_geom_of(int c) {
+  FxGeom g;
+  g.c = c;
+  g.nw = (255 + c - 1) / c;
+  g.nb = 1u << (c - 1);
+  g.lb = c / 2;
+  g.hb = c - 1 - g.lb;
+  return g;
+}
+// default window width of a table of n points; PBF_MSM_FX_C=16/18/20/22 forces one (A/B; read at
+// the table build). Measured (profiles/r04/msm_window_*): a 2^20-point MSM is fastest at c = 16
+// (2.27 ms; c = 20: 2.69), 2^22 points at c = 20 (7.60 against 7.71 ms; in the 2^22-gate proof
+// 87.6 against 92.0 ms), 2^24 points at c = 22 (27.2 against 29.0 ms; the 2^24-gate proof 327
+// against 350 ms). Boundaries at the geometric midpoints.
+static int fx_default_c(uint64_t n) {
+  const char* e = getenv("PBF_MSM_FX_C");
+  if (e) {
+    const int v = atoi(e);
+    if (v == 16 || v == 18 || v == 20 || v == 22) return v;
+  }
+  if (n >= 3ull << 22) return 22;
+  if (n >= 3ull << 20) return 20;
+  return 16;
+}
 
 // table window w from window w-1: FX_C doublings in XYZZ, then affine through a
 // block-wide batch inversion of the ZZZ (prefix and suffix products in LDS, one Fermat
 // inversion per block); the identity (0, 0) stays (0, 0)
-__global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affine* next, uint64_t n) {
+__global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affine* next, uint64_t n, int c) {
   __shared__ U256 pre[256], suf[256];
   __shared__ U256 tinv;
   const uint32_t t = threadIdx.x;
@@ -289,7 +432,7 @@ __global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affi
     id = Fq::is_zero(a.x) && Fq::is_zero(a.y);
     if (!id) {
       acc = G1::mdbl(a);
-      for (int k = 1; k < FX_C; ++k) acc = G1::dbl(acc);
+      for (int k = 1; k < c; ++k) acc = G1::dbl(acc);
     }
   }
   const U256 z = id ? one : acc.ZZZ;
@@ -326,14 +469,14 @@ __global__ void __launch_bounds__(256) msm_table_window(const Affine* prev, Affi
 
 // window w's signed digit of a scalar (FX_C bits; d > 2^(FX_C-1) -> d - 2^FX_C, carry 1 upward):
 // calls in window order carry through `carry`. Returns |d| (0: no entry), sets neg.
-__device__ __forceinline__ uint32_t fx_digit(const uint64_t* s, int w, uint32_t& carry, bool& neg) {
-  const int bit = FX_C * w, limb = bit >> 6, off = bit & 63;
+__device__ __forceinline__ uint32_t fx_digit(const uint64_t* s, int w, int c, uint32_t& carry, bool& neg) {
+  const int bit = c * w, limb = bit >> 6, off = bit & 63;
   uint64_t v = limb < 4 ? s[limb] >> off : 0;
-  if (off + FX_C > 64 && limb + 1 < 4) v |= s[limb + 1] << (64 - off);
-  uint32_t d = (uint32_t)(v & ((1u << FX_C) - 1)) + carry;
+  if (off + c > 64 && limb + 1 < 4) v |= s[limb + 1] << (64 - off);
+  uint32_t d = (uint32_t)(v & ((1u << c) - 1)) + carry;
   neg = false;
-  if (d > FX_NB) {
-    d = (1u << FX_C) - d;
+  if (d > (1u << (c - 1))) {
+    d = (1u << c) - d;
     neg = true;
     carry = 1;
   } else {
@@ -345,38 +488,41 @@ __device__ __forceinline__ uint32_t fx_digit(const uint64_t* s, int w, uint32_t&
 // one (key, value) per (point, window): key = |d| - 1 (FX_NB: zero digit or identity
 // point, sorts last), value = index of table[w][first + i] | sign
 __global__ void __launch_bounds__(256) msm_fx_digits(const uint64_t* scalars, const uint8_t* inf, uint64_t n_table,
-                                                     uint64_t first, uint64_t n, uint32_t* keys, uint32_t* vals) {
+                                                     uint64_t first, uint64_t n, uint32_t* keys, uint32_t* vals,
+                                                     int c, int nw) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = scalars + 4 * i;
     const bool skip = inf[first + i] != 0;
     uint32_t carry = 0;
-#pragma unroll
-    for (int w = 0; w < FX_NW; ++w) {
+    for (int w = 0; w < nw; ++w) {
       bool neg;
-      const uint32_t d = fx_digit(s, w, carry, neg);
-      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? FX_NB : d - 1;
+      const uint32_t d = fx_digit(s, w, c, carry, neg);
+      keys[(uint64_t)w * n + i] = (d == 0 || skip) ? (1u << (c - 1)) : d - 1;
       vals[(uint64_t)w * n + i] = (uint32_t)((uint64_t)w * n_table + first + i) | (neg ? MSM_NEG : 0u);
     }
   }
 }
 
-// The same digits as msm_fx_digits as planar 16-bit codes (msm_sort.hpp RS_DIG_*): the
-// first sort pass derives key and value from the code and the entry index
-__global__ void __launch_bounds__(256) msm_fx_digits16(const uint64_t* scalars, const uint8_t* inf, uint64_t first,
-                                                       uint64_t n, uint16_t* dig) {
+// The same digits as msm_fx_digits as planar codes (msm_sort.hpp RsDigitsT: 16-bit for c <= 16,
+// 32-bit above): the first sort pass derives key and value from the code and the entry index
+template <typename C, int C_FIX = 0>
+__global__ void __launch_bounds__(256) msm_fx_digits_code(const uint64_t* scalars, const uint8_t* inf, uint64_t first,
+                                                          uint64_t n, C* dig, int c_rt, int nw_rt) {
+  const int c = C_FIX ? C_FIX : c_rt, nw = C_FIX ? (255 + C_FIX - 1) / C_FIX : nw_rt;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t* s = scalars + 4 * i;
     const bool skip = inf[first + i] != 0;
     uint32_t carry = 0;
 #pragma unroll
-    for (int w = 0; w < FX_NW; ++w) {
+    for (int w = 0; w < (C_FIX ? (255 + C_FIX - 1) / C_FIX : 16); ++w) {
+      if (!C_FIX && w >= nw) break;
       bool neg;
-      const uint32_t d = fx_digit(s, w, carry, neg);
-      dig[(uint64_t)w * n + i] = (d == 0 || skip) ? RS_DIG_NONE : (uint16_t)((d - 1) | (neg ? 0x8000u : 0u));
+      const uint32_t d = fx_digit(s, w, c, carry, neg);
+      dig[(uint64_t)w * n + i] = (d == 0 || skip) ? (C)rs_none<C>() : (C)((d - 1) | (neg ? rs_sign<C>() : 0u));
     }
   }
 }
-static_assert(FX_NB - 1 <= 0x7FFF, "a digit code holds |d| - 1 in 15 bits");
+static_assert(FX_NB - 1 <= 0x7FFF, "a 16-bit digit code holds |d| - 1 in 15 bits");
 
 // Boundary join (fixed-base form: ~16 n / 2^15 entries per bucket, 512 at 2^20 points, so a
 // bucket crossing chunks spans ~12 of them; windowed form: ~2 chunks). Tree over each bucket's
@@ -398,9 +544,12 @@ __global__ void __launch_bounds__(256) msm_max_span(const uint32_t* start, const
   __syncthreads();
   if (threadIdx.x == 0 && bmax) atomicMax(span, bmax);
 }
+// cap: buckets spanning more than `cap` chunks are left to msm_join_chunks (the fixed-base form;
+// ~0u: none), so the pair slots per bucket follow min(largest span, cap), not the largest span
 __global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint32_t* start, const uint32_t* end,
-                                                     uint32_t nb, uint32_t step, const uint32_t* span) {
-  const uint32_t sp = *span;
+                                                     uint32_t nb, uint32_t step, const uint32_t* span,
+                                                     uint32_t cap) {
+  const uint32_t sp0 = *span, sp = sp0 < cap ? sp0 : cap;
   if (step >= sp) return;  // every bucket's continuations already summed
   const uint32_t per = (sp + 2 * step - 1) / (2 * step);  // pair slots per bucket
   const uint64_t items = (uint64_t)nb * per;
@@ -410,6 +559,7 @@ __global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint
     const uint32_t bs = start[k], be = end[k];
     if (be <= bs) continue;
     const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+    if (e - o > cap) continue;  // a heavy bucket: msm_join_chunks
     const uint32_t u = o + 1 + 2 * step * j;
     if (u + step <= e) head[u].acc = G1::add2(head[u].acc, head[u + step].acc);
   }
@@ -436,6 +586,37 @@ __global__ void __launch_bounds__(256) msm_join_rest(ChunkPart* head, const uint
   if (e - o <= FX_JOIN_GROUP) return;
   Xyzz acc = head[o + 1].acc;
   for (uint32_t u = o + 1 + FX_JOIN_GROUP; u <= e; u += FX_JOIN_GROUP) acc = G1::add2(acc, head[u].acc);
+  head[o + 1].acc = acc;
+}
+
+// The same tree for the heavy buckets (spanning more than `cap` chunks; round 4, the fixed-base
+// form), indexed by continuation chunk: work item u < nchunks is chunk u's head partial (hkey[u]:
+// its bucket, or the sentinel), so a step costs O(chunks) however few buckets are heavy. Without
+// it the per-bucket grid gives every bucket the pair slots of the LARGEST span: a narrow top
+// window puts all n of its entries into few buckets (c = 18: 2 bits, 4 buckets; c = 22: 12
+// bits), and the steps took up to ~8 ms each. Exits at once when no bucket is heavy.
+__global__ void __launch_bounds__(256) msm_join_chunks(ChunkPart* head, const uint32_t* hkey, const uint32_t* start,
+                                                       const uint32_t* end, uint32_t nchunks, uint32_t step,
+                                                       const uint32_t* span, uint32_t sent, uint32_t cap) {
+  const uint32_t sp = *span;
+  if (step >= sp || sp <= cap) return;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < nchunks; u += gridDim.x * blockDim.x) {
+    const uint32_t k = hkey[u];
+    if (k == sent) continue;
+    const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH, rel = u - (o + 1);
+    if (e - o > cap && rel % (2 * step) == 0 && u + step <= e) head[u].acc = G1::add2(head[u].acc, head[u + step].acc);
+  }
+}
+// msm_join_rest for a group size `group` (the steps launched: 1 .. group / 2)
+__global__ void __launch_bounds__(256) msm_join_rest_g(ChunkPart* head, const uint32_t* start, const uint32_t* end,
+                                                       uint32_t nb, const uint32_t* span, uint32_t group) {
+  if (*span <= group) return;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nb || end[k] <= start[k]) return;
+  const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH;
+  if (e - o <= group) return;
+  Xyzz acc = head[o + 1].acc;
+  for (uint32_t u = o + 1 + group; u <= e; u += group) acc = G1::add2(acc, head[u].acc);
   head[o + 1].acc = acc;
 }
 
@@ -624,6 +805,133 @@ __global__ void __launch_bounds__(64) msm_fx_total_q(const Xyzz* sub, Xyzz* out)
 static bool msm_quad_tail() {
   return env_default_on("PBF_MSM_QUAD");  // read per call: an A/B knob
 }
+// the fixed-base join indexed by chunk (msm_join_chunks, default) or by bucket (=0: A/B)
+static bool fx_chunk_join() {
+  return env_default_on("PBF_MSM_CHUNK_JOIN");  // read per call: an A/B knob
+}
+constexpr uint32_t FX_JOIN_GROUP_C = 4096;  // per-chunk steps 1 .. 2048, the rest sequential
+constexpr uint32_t FX_SEQ_CAP = 4;  // wide windows: spans <= 4 chunks summed in fx_bucket_into
+
+// ---- the fixed-base tail for any window width (FxGeom: 2^(lb + hb) buckets, b = 2^lb h + l):
+//   C_h = sum_l B_(2^lb h + l) (2^hb values), D_l = sum_h B_(2^lb h + l) (2^lb values),
+//   T = sum_b (b + 1) B_b = sum_{k < hb} 2^(k + lb) Z_k + sum_{k < lb} 2^k Y_k + S,
+//   Z_k = sum_{h: bit k of h} C_h, Y_k = sum_{l: bit k of l} D_l, S = sum_h C_h
+// (the c = 16 kernels above with 256 -> 2^lb, 128 -> 2^hb). Workgroups of QW quads; every quad
+// first adds its share of the values in sequence, then a quad tree. At c = 16 the sequences
+// and trees are those of msm_fx_cd_q / msm_fx_subsets_q.
+template <int QW>
+__global__ void __launch_bounds__(4 * QW) msm_fxg_cd_q(const Xyzz* buckets, const ChunkPart* head,
+                                                       const ChunkPart* tail, const uint32_t* start,
+                                                       const uint32_t* end, Xyzz* cd, int lb, int hb) {
+  __shared__ Xyzz red[QW];
+  const uint32_t g = blockIdx.x, qi = threadIdx.x >> 2, L = 1u << lb, NH = 1u << hb;
+  Xyzz v = G1::identity();
+  if (g < NH) {  // C_g: L consecutive buckets, L / QW per quad
+    const uint32_t per = (L + QW - 1) / QW;
+    for (uint32_t i = 0; i < per; ++i) {
+      const uint32_t l = per * qi + i;  // quad-uniform
+      if (l < L) v = G1Quad::add(v, fx_bucket_q(L * g + l, buckets, head, tail, start, end));
+    }
+  } else {  // D_l: NH buckets L apart
+    const uint32_t l = g - NH, per = (NH + QW - 1) / QW;
+    for (uint32_t i = 0; i < per; ++i) {
+      const uint32_t h = per * qi + i;
+      if (h < NH) v = G1Quad::add(v, fx_bucket_q(L * h + l, buckets, head, tail, start, end));
+    }
+  }
+  v = fx_tree_q(v, red);
+  if (threadIdx.x == 0) cd[g] = v;
+}
+// The C_h / D_l sums of msm_fxg_cd_q on single lanes (wide windows: 2^18 .. 2^21 buckets, a
+// throughput job; a quad addition costs four lanes for one sum): each lane adds per = count /
+// lanes values in sequence, then a `lanes`-lane LDS tree. Workgroup g < gC: C_h for vc = 256 /
+// lc values of h (lc = min(256, L / SEQ) lanes each); then D_l for vd values of l.
+// Bucket k's parts added into acc: its whole sum (buckets[k]) when it lies in one chunk; its
+// chunk-o tail run and its continuations head[o+1 .. e] one by one when it spans at most cap
+// chunks (the wide-window tails skip the join for those: ~2 chunks per bucket); else the tail
+// run and the joined continuations head[o+1].
+__device__ __forceinline__ Xyzz fx_bucket_into(Xyzz acc, uint32_t k, const Xyzz* buckets, const ChunkPart* head,
+                                               const ChunkPart* tail, const uint32_t* start, const uint32_t* end,
+                                               uint32_t cap) {
+  const uint32_t bs = start[k], be = end[k];
+  if (be <= bs) return acc;
+  const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+  if (o == e) return G1::add2(acc, buckets[k]);
+  acc = G1::add2(acc, tail[o].acc);
+  if (e - o > cap) return G1::add2(acc, head[o + 1].acc);
+  for (uint32_t u = o + 1; u <= e; ++u) acc = G1::add2(acc, head[u].acc);
+  return acc;
+}
+template <int SEQ>
+__global__ void __launch_bounds__(256) msm_fxg_cd_seq(const Xyzz* buckets, const ChunkPart* head,
+                                                      const ChunkPart* tail, const uint32_t* start,
+                                                      const uint32_t* end, Xyzz* cd, int lb, int hb, uint32_t cap) {
+  __shared__ Xyzz red[256];
+  const uint32_t L = 1u << lb, NH = 1u << hb, t = threadIdx.x, g = blockIdx.x;
+  const uint32_t lc = L / SEQ < 256 ? L / SEQ : 256, vc = 256 / lc, gC = NH / vc;
+  const uint32_t ld = NH / SEQ < 256 ? NH / SEQ : 256, vd = 256 / ld;
+  Xyzz acc = G1::identity();
+  uint32_t lanes, outi;
+  if (g < gC) {
+    const uint32_t h = g * vc + t / lc, per = L / lc, l0 = (t % lc) * per;
+    for (uint32_t i = 0; i < per; ++i) acc = fx_bucket_into(acc, L * h + l0 + i, buckets, head, tail, start, end, cap);
+    lanes = lc;
+    outi = h;
+  } else {
+    const uint32_t l = (g - gC) * vd + t / ld, per = NH / ld, h0 = (t % ld) * per;
+    for (uint32_t i = 0; i < per; ++i) acc = fx_bucket_into(acc, L * (h0 + i) + l, buckets, head, tail, start, end, cap);
+    lanes = ld;
+    outi = NH + l;
+  }
+  red[t] = acc;
+  __syncthreads();
+  for (uint32_t st = lanes / 2; st > 0; st >>= 1) {
+    if (t % lanes < st) red[t] = G1::add2(red[t], red[t + st]);
+    __syncthreads();
+  }
+  if (t % lanes == 0) cd[outi] = red[t];
+}
+static uint32_t fxg_cd_seq_groups(const FxGeom& g, uint32_t seq) {
+  const uint32_t L = 1u << g.lb, NH = 1u << g.hb;
+  const uint32_t lc = L / seq < 256 ? L / seq : 256, ld = NH / seq < 256 ? NH / seq : 256;
+  return NH / (256 / lc) + L / (256 / ld);
+}
+// workgroup s < lb: 2^s Y_s; lb <= s < lb + hb: 2^s Z_(s - lb); s = lb + hb: S
+template <int QW>
+__global__ void __launch_bounds__(4 * QW) msm_fxg_subsets_q(const Xyzz* cd, Xyzz* sub, int lb, int hb) {
+  __shared__ Xyzz red[QW];
+  const uint32_t s = blockIdx.x, t = threadIdx.x >> 2, L = 1u << lb, NH = 1u << hb;
+  const Xyzz* C = cd;
+  const Xyzz* D = cd + NH;
+  const uint32_t cnt = s < (uint32_t)lb ? L / 2 : s < (uint32_t)(lb + hb) ? NH / 2 : NH;
+  const uint32_t per = (cnt + QW - 1) / QW;
+  Xyzz v = G1::identity();
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t u = t * per + i;  // the u-th index with bit k set
+    if (u >= cnt) break;             // quad-uniform
+    if (s < (uint32_t)lb) {
+      v = G1Quad::add(v, D[((u >> s) << (s + 1)) | (1u << s) | (u & ((1u << s) - 1))]);
+    } else if (s < (uint32_t)(lb + hb)) {
+      const uint32_t k = s - lb;
+      v = G1Quad::add(v, C[((u >> k) << (k + 1)) | (1u << k) | (u & ((1u << k) - 1))]);
+    } else {
+      v = G1Quad::add(v, C[u]);
+    }
+  }
+  v = fx_tree_q(v, red);
+  if (t == 0) {
+    const uint32_t e = s < (uint32_t)(lb + hb) ? s : 0;
+    for (uint32_t i = 0; i < e; ++i) v = G1Quad::dbl(v);
+    if (threadIdx.x == 0) sub[s] = v;
+  }
+}
+// the nsub <= 32 scaled subset sums -> *out (32 quads)
+__global__ void __launch_bounds__(128) msm_fxg_total_q(const Xyzz* sub, int nsub, Xyzz* out) {
+  __shared__ Xyzz red[32];
+  const uint32_t q = threadIdx.x >> 2;
+  const Xyzz v = fx_tree_q(q < (uint32_t)nsub ? sub[q] : G1::identity(), red);
+  if (threadIdx.x == 0) *out = v;
+}
 
 // Exact-content cache validation (snapshot_check below): diff[0] = 1 when a and b differ in
 // any of their `words` u64 (benign same-value race; vector stores only).
@@ -740,24 +1048,36 @@ static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* va
 static bool msm_fused_sort() {
   return env_default_on("PBF_MSM_FUSED_SORT");  // read per call: an A/B knob (=0: pair sort)
 }
+// digit width of pass p of a `bits`-bit sort: as equal as possible (msm_sort.hpp rs_width);
+// PBF_MSM_SORT_W8=1 keeps every pass but the last at 8 bits (A/B)
+static int msm_sort_width(int bits, int p) {
+  if (getenv("PBF_MSM_SORT_W8")) {  // read per call: an A/B knob
+    const int rest = bits - 8 * p;
+    return rest < 8 ? rest : 8;
+  }
+  return rs_width(bits, p);
+}
 // bits: key bits to sort (2 or 3 passes; the last lands in keys2 / vals2, the middle one in
-// the caller's keys / vals buffers, free once the codes are read)
-static int msm_sort_digits(pbf_ctx* ctx, const RsDigits& dg, uint32_t* keys2, uint32_t* vals2, uint32_t* mid_k,
+// the caller's mid_k / mid_v buffers, free once the codes are read)
+template <typename C>
+static int msm_sort_digits(pbf_ctx* ctx, const RsDigitsT<C>& dg, uint32_t* keys2, uint32_t* vals2, uint32_t* mid_k,
                            uint32_t* mid_v, uint64_t m, int bits, hipStream_t s) {
   if (m > 0xFFFFFFFFull - RS_TILE_MAX) return fail(PBF_EINVAL, "too many MSM entries");
-  if ((bits != 16 && bits != 20) || dg.kw % 256 || !rs_dig_ok(dg.n))
-    return fail(PBF_EINVAL, "digit sort: 16 or 20 key bits, whole key bytes per window, n >= 256");
+  const int passes = rs_passes(bits), w0 = msm_sort_width(bits, 0);
+  if (bits < 9 || bits > 24 || dg.kw % (1u << w0) || !rs_dig_ok(dg.n) || (passes == 3 && (!mid_k || !mid_v)))
+    return fail(PBF_EINVAL, "digit sort: 9..24 key bits, whole first-pass digits per window, n >= 256");
   DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
   const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
   int rc;
   if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
   uint32_t *k1 = (uint32_t*)tk.p, *v1 = (uint32_t*)tv.p, *hist = (uint32_t*)hb.p;
-  rs_pass<RS_ITEMS, true>(nullptr, nullptr, k1, v1, (uint32_t)m, 0, hist, s, dg);
-  if (bits == 16) {
-    rs_pass<RS_ITEMS>(k1, v1, keys2, vals2, (uint32_t)m, 8, hist, s);
+  rs_pass<RS_ITEMS, true, C>(nullptr, nullptr, k1, v1, (uint32_t)m, 0, hist, s, dg, w0);
+  const int w1 = msm_sort_width(bits, 1);
+  if (passes == 2) {
+    rs_pass<RS_ITEMS>(k1, v1, keys2, vals2, (uint32_t)m, w0, hist, s, RsDigits{}, w1);
   } else {
-    rs_pass<RS_ITEMS>(k1, v1, mid_k, mid_v, (uint32_t)m, 8, hist, s);
-    rs_pass<RS_ITEMS>(mid_k, mid_v, keys2, vals2, (uint32_t)m, 16, hist, s);
+    rs_pass<RS_ITEMS>(k1, v1, mid_k, mid_v, (uint32_t)m, w0, hist, s, RsDigits{}, w1);
+    rs_pass<RS_ITEMS>(mid_k, mid_v, keys2, vals2, (uint32_t)m, w0 + w1, hist, s, RsDigits{}, msm_sort_width(bits, 2));
   }
   PBF_HIP(hipGetLastError());
   return 0;
@@ -806,20 +1126,36 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   // length is known only on the device, so chunks past it return at once. No bucket memset:
   // the reduction reads only the buckets the accumulation wrote (fx_bucket).
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
-  PBF_HIP(hipMemsetAsync(w.span.p, 0, 4, s));
-  hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
-                     (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
-                     (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p,
-                     (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr);
   // the same tail as the fixed-base form, over 16 windows of 2^15 buckets (bucket id = key)
   constexpr uint32_t NBT = MSM_NW * MSM_NB;
+  DevBuf &hk = ctx->buf("msm.hkey"), &tk = ctx->buf("msm.tkey"), &braw = ctx->buf("msm.braw");
+  if ((rc = hk.ensure((uint64_t)nchunks * 4 + 4)) || (rc = tk.ensure((uint64_t)nchunks * 4 + 4))) return rc;
+  PBF_HIP(hipMemsetAsync(w.span.p, 0, 4, s));
+  if (msm_l29() && msm_rawflush()) {
+    if ((rc = braw.ensure((uint64_t)NBT * 144))) return rc;
+    hipLaunchKernelGGL(msm_chunk_acc_l29r, dim3((nchunks + 255) / 256), dim3(256), 0, s, (const Affine*)w.pts.p,
+                       (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p, (const uint32_t*)w.start.p,
+                       (const uint32_t*)w.end.p, (uint32_t)m, (uint32_t*)braw.p, (ChunkPart*)w.head.p,
+                       (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr, (uint32_t*)hk.p, (uint32_t*)tk.p);
+    hipLaunchKernelGGL(msm_l29_finish, dim3(grid1((uint64_t)NBT + 2ull * nchunks)), dim3(256), 0, s,
+                       (const uint32_t*)braw.p, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p, (ChunkPart*)w.tail.p,
+                       (const uint32_t*)hk.p, (const uint32_t*)tk.p, (const uint32_t*)w.start.p,
+                       (const uint32_t*)w.end.p, NBT, nchunks, MSM_SENTINEL);
+  } else {
+    hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s,
+                       (const Affine*)w.pts.p, (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p,
+                       (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, (uint32_t)m, (Xyzz*)w.buckets.p,
+                       (ChunkPart*)w.head.p, (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr,
+                       (uint32_t*)hk.p, (uint32_t*)tk.p);
+  }
   hipLaunchKernelGGL(msm_max_span, dim3(NBT / 256), dim3(256), 0, s, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, NBT, (uint32_t*)w.span.p);
   const uint64_t mean_span = m / ((uint64_t)NBT * MSM_CH) + 2;
   for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
     const uint64_t items = (uint64_t)NBT * ((mean_span + 2 * step - 1) / (2 * step));
     hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, s, (ChunkPart*)w.head.p,
-                       (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, step, (const uint32_t*)w.span.p);
+                       (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, step, (const uint32_t*)w.span.p,
+                       ~0u);
   }
   hipLaunchKernelGGL(msm_join_rest, dim3(NBT / 256), dim3(256), 0, s, (ChunkPart*)w.head.p,
                      (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, (const uint32_t*)w.span.p);
@@ -923,25 +1259,27 @@ int snapshot_check(pbf_ctx* ctx, const char* consumer, const SnapItem* items, in
 // differ from the ones it was built from, wherever they live); the table's identity flags are
 // kept with it (fixed_base.inf)
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
-  if (n == 0 || n > 0x7FFFFFFFull / FX_NW) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
+  const FxGeom g = fx_geom_of(fx_default_c(n));
+  if (n == 0 || n > 0x7FFFFFFFull / g.nw) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
   const SnapItem it{"g1pts", d_pts, 8 * n};
   bool same = false;
   int rc = snapshot_check(ctx, "fx", &it, 1, s, &same);
   if (rc) return rc;
   auto& fb = ctx->fixed_base;
-  if (same && fb.valid && fb.n == n && fb.table.p) {
+  if (same && fb.valid && fb.n == n && fb.c == g.c && fb.table.p) {
     *out = (const Affine*)fb.table.p;
     return 0;
   }
   fb.valid = false;
-  if ((rc = fb.table.ensure((uint64_t)FX_NW * n * sizeof(Affine))) || (rc = fb.inf.ensure(n))) return rc;
+  if ((rc = fb.table.ensure((uint64_t)g.nw * n * sizeof(Affine))) || (rc = fb.inf.ensure(n))) return rc;
   Affine* tbl = (Affine*)fb.table.p;
   hipLaunchKernelGGL(msm_points_to_mont, dim3(grid1(n)), dim3(256), 0, s, d_pts, tbl, (uint8_t*)fb.inf.p, n);
-  for (int w = 1; w < FX_NW; ++w)
+  for (int w = 1; w < g.nw; ++w)
     hipLaunchKernelGGL(msm_table_window, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                       (const Affine*)(tbl + (uint64_t)(w - 1) * n), tbl + (uint64_t)w * n, n);
+                       (const Affine*)(tbl + (uint64_t)(w - 1) * n), tbl + (uint64_t)w * n, n, g.c);
   PBF_HIP(hipGetLastError());
   fb.n = n;
+  fb.c = g.c;
   fb.valid = true;
   *out = tbl;
   return 0;
@@ -1011,7 +1349,9 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   auto& fb = ctx->fixed_base;
   if ((const void*)table != fb.table.p || n_table != fb.n || !fb.inf.p)
     return fail(PBF_EINVAL, "fixed-base MSM: not the context's table");
-  const uint64_t m = n * FX_NW;  // entries at most (zero digits are skipped)
+  const FxGeom g = fx_geom_of(fb.c);
+  const uint32_t NB = g.nb;
+  const uint64_t m = n * g.nw;  // entries at most (zero digits are skipped)
   MsmTail& tl = ctx->msm_tail;
   int rc;
   if ((rc = tl.ensure())) return rc;
@@ -1021,45 +1361,78 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
          &vals2 = ctx->buf("msm.vals2");
   DevBuf &start = ctx->buf(pre + "start"), &end = ctx->buf(pre + "end"), &buckets = ctx->buf(pre + "buckets"),
          &shares = ctx->buf(pre + "shares"), &parts = ctx->buf(pre + "parts"), &head = ctx->buf(pre + "head"),
-         &tail = ctx->buf(pre + "tail"), &spb = ctx->buf(pre + "span");
+         &tail = ctx->buf(pre + "tail"), &spb = ctx->buf(pre + "span"), &hk = ctx->buf(pre + "hkey"),
+         &tk = ctx->buf(pre + "tkey");
+  DevBuf& braw = ctx->buf("msm.braw");  // read only on s (msm_l29_finish), before the tail forks
   // a slot's buffers may still be read by its previous tail: reallocation waits for it
   if (tl.used[slot]) PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
   const uint64_t hbytes = (m / MSM_CH + 1) * sizeof(ChunkPart);
-  if ((head.bytes < hbytes || tail.bytes < hbytes) && tl.used[slot]) PBF_HIP(hipEventSynchronize(tl.done[slot]));
+  const uint64_t nshare = (1ull << g.hb) + (1ull << g.lb);
+  if ((head.bytes < hbytes || tail.bytes < hbytes || start.bytes < (uint64_t)NB * 4 || hk.bytes < m / MSM_CH * 4 + 8 ||
+       buckets.bytes < (uint64_t)NB * sizeof(Xyzz) || shares.bytes < nshare * sizeof(Xyzz)) &&
+      tl.used[slot])
+    PBF_HIP(hipEventSynchronize(tl.done[slot]));
   if ((rc = keys.ensure(m * 4)) || (rc = vals.ensure(m * 4)) || (rc = keys2.ensure(m * 4)) ||
-      (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)FX_NB * 4)) || (rc = end.ensure((uint64_t)FX_NB * 4)) ||
-      (rc = buckets.ensure((uint64_t)FX_NB * sizeof(Xyzz))) || (rc = shares.ensure((uint64_t)(FX_NH + 256) * sizeof(Xyzz))) ||
-      (rc = parts.ensure(16 * sizeof(Xyzz))) || (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) ||
-      (rc = spb.ensure(4)))
+      (rc = vals2.ensure(m * 4)) || (rc = start.ensure((uint64_t)NB * 4)) || (rc = end.ensure((uint64_t)NB * 4)) ||
+      (rc = buckets.ensure((uint64_t)NB * sizeof(Xyzz))) || (rc = shares.ensure(nshare * sizeof(Xyzz))) ||
+      (rc = parts.ensure(32 * sizeof(Xyzz))) || (rc = head.ensure(hbytes)) || (rc = tail.ensure(hbytes)) ||
+      (rc = spb.ensure(4)) || (rc = hk.ensure(m / MSM_CH * 4 + 8)) || (rc = tk.ensure(m / MSM_CH * 4 + 8)))
     return rc;
   const uint8_t* inf = (const uint8_t*)fb.inf.p;
   // ---- digits, sort by bucket, bucket bounds
+  if ((uint64_t)g.nw * n_table >= MSM_NEG) return fail(PBF_EINVAL, "fixed-base MSM: table too large");
   if (msm_fused_sort() && rs_dig_ok(n)) {
-    // keys holds the 2-byte digit codes; vals is not used
-    if ((uint64_t)FX_NW * n_table >= MSM_NEG) return fail(PBF_EINVAL, "fixed-base MSM: table too large");
-    hipLaunchKernelGGL(msm_fx_digits16, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n, (uint16_t*)keys.p);
-    const RsDigits dg{(const uint16_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, FX_NB, MSM_NEG};
-    if ((rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, nullptr, nullptr, m, FX_C, s)))
-      return rc;
+    // keys holds the digit codes (2 B per entry at c = 16, else 4 B); for a 3-pass sort keys
+    // and vals then take the middle pass (the codes are read by then)
+    if (g.c == 16) {
+      hipLaunchKernelGGL((msm_fx_digits_code<uint16_t, 16>), dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n,
+                         (uint16_t*)keys.p, g.c, g.nw);
+      const RsDigits dg{(const uint16_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, NB, MSM_NEG};
+      rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, (uint32_t*)keys.p, (uint32_t*)vals.p, m,
+                           g.c, s);
+    } else {
+      auto* dk = g.c == 18 ? msm_fx_digits_code<uint32_t, 18>
+                 : g.c == 20 ? msm_fx_digits_code<uint32_t, 20>
+                             : msm_fx_digits_code<uint32_t, 22>;
+      hipLaunchKernelGGL(dk, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n, (uint32_t*)keys.p, g.c, g.nw);
+      const RsDigitsT<uint32_t> dg{(const uint32_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, NB,
+                                   MSM_NEG};
+      rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, (uint32_t*)keys.p, (uint32_t*)vals.p, m,
+                           g.c, s);
+    }
+    if (rc) return rc;
   } else {
     hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
-                       (uint32_t*)keys.p, (uint32_t*)vals.p);
+                       (uint32_t*)keys.p, (uint32_t*)vals.p, g.c, g.nw);
     if ((rc = msm_sort_pairs(ctx, (const uint32_t*)keys.p, (const uint32_t*)vals.p, (uint32_t*)keys2.p,
-                             (uint32_t*)vals2.p, m, FX_C, s)))
+                             (uint32_t*)vals2.p, m, g.c, s)))
       return rc;
   }
-  hipLaunchKernelGGL(msm_fx_clear, dim3(FX_NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
+  hipLaunchKernelGGL(msm_fx_clear, dim3(NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
                      (uint32_t*)spb.p);
   hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
-                     (uint32_t*)start.p, (uint32_t*)end.p, FX_NB);
+                     (uint32_t*)start.p, (uint32_t*)end.p, NB);
   // ---- accumulation
   // no bucket memset: msm_fx_cd reads only the buckets the accumulation wrote (fx_bucket)
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
-  hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s, table, (const uint32_t*)keys2.p,
-                     (const uint32_t*)vals2.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)m,
-                     (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p, FX_NB, (const uint32_t*)nullptr);
-  hipLaunchKernelGGL(msm_max_span, dim3(FX_NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
-                     (const uint32_t*)end.p, FX_NB, (uint32_t*)spb.p);
+  if (msm_l29() && msm_rawflush(g.c > 16)) {
+    if ((rc = braw.ensure((uint64_t)NB * 144))) return rc;
+    hipLaunchKernelGGL(msm_chunk_acc_l29r, dim3((nchunks + 255) / 256), dim3(256), 0, s, table,
+                       (const uint32_t*)keys2.p, (const uint32_t*)vals2.p, (const uint32_t*)start.p,
+                       (const uint32_t*)end.p, (uint32_t)m, (uint32_t*)braw.p, (ChunkPart*)head.p, (ChunkPart*)tail.p,
+                       NB, (const uint32_t*)nullptr, (uint32_t*)hk.p, (uint32_t*)tk.p);
+    hipLaunchKernelGGL(msm_l29_finish, dim3(grid1((uint64_t)NB + 2ull * nchunks)), dim3(256), 0, s,
+                       (const uint32_t*)braw.p, (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p,
+                       (const uint32_t*)hk.p, (const uint32_t*)tk.p, (const uint32_t*)start.p, (const uint32_t*)end.p,
+                       NB, nchunks, NB);
+  } else {
+    hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s,
+                       table, (const uint32_t*)keys2.p, (const uint32_t*)vals2.p, (const uint32_t*)start.p,
+                       (const uint32_t*)end.p, (uint32_t)m, (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p,
+                       NB, (const uint32_t*)nullptr, (uint32_t*)hk.p, (uint32_t*)tk.p);
+  }
+  hipLaunchKernelGGL(msm_max_span, dim3(NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
+                     (const uint32_t*)end.p, NB, (uint32_t*)spb.p);
   PBF_HIP(hipGetLastError());
   // ---- the tail, on the side stream
   hipStream_t a = tl.aux;
@@ -1068,25 +1441,67 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   // join steps 1 .. FX_JOIN_GROUP / 2 (steps past the largest span exit at once); wider spans
   // are finished by msm_join_rest. The grid covers the mean span's pair slots (the kernel
   // strides over the rest).
-  const uint64_t mean_span = m / ((uint64_t)FX_NB * MSM_CH) + 2;
-  for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
-    const uint64_t items = (uint64_t)FX_NB * ((mean_span + 2 * step - 1) / (2 * step));
-    hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
-                       (const uint32_t*)start.p, (const uint32_t*)end.p, FX_NB, step, (const uint32_t*)spb.p);
-  }
-  hipLaunchKernelGGL(msm_join_rest, dim3(FX_NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
-                     (const uint32_t*)end.p, FX_NB, (const uint32_t*)spb.p);
-  if (msm_quad_tail()) {
-    hipLaunchKernelGGL(msm_fx_cd_q, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p,
-                       (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
-                       (const uint32_t*)end.p, (Xyzz*)shares.p);
-    hipLaunchKernelGGL(msm_fx_subsets_q, dim3(16), dim3(512), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
-    hipLaunchKernelGGL(msm_fx_total_q, dim3(1), dim3(64), 0, a, (const Xyzz*)parts.p, d_result);
+  if (fx_chunk_join()) {
+    // buckets spanning up to `cap` chunks (twice the mean span, a power of two): the per-bucket
+    // steps; heavier ones: the per-chunk steps up to FX_JOIN_GROUP_C / 2 (both exit at once past
+    // the largest span), then msm_join_rest_g
+    // wide windows (single-lane C / D sums): buckets spanning up to FX_SEQ_CAP chunks are not
+    // joined at all, fx_bucket_into adds their continuations in sequence
+    const bool wide = !(g.c == 16 || getenv("PBF_MSM_CD_QUAD"));
+    const uint64_t mean_span = m / ((uint64_t)NB * MSM_CH) + 2;
+    uint32_t cap = 2;
+    while (cap < 2 * mean_span && cap < FX_JOIN_GROUP_C) cap <<= 1;
+    if (wide) cap = FX_SEQ_CAP;
+    for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP_C; step <<= 1) {
+      if (step < cap && !wide) {
+        const uint64_t items = (uint64_t)NB * ((mean_span + 2 * step - 1) / (2 * step));
+        hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
+                           (const uint32_t*)start.p, (const uint32_t*)end.p, NB, step, (const uint32_t*)spb.p, cap);
+      }
+      hipLaunchKernelGGL(msm_join_chunks, dim3((uint32_t)grid1(nchunks)), dim3(256), 0, a, (ChunkPart*)head.p,
+                         (const uint32_t*)hk.p, (const uint32_t*)start.p, (const uint32_t*)end.p, nchunks, step,
+                         (const uint32_t*)spb.p, NB, cap);
+    }
+    hipLaunchKernelGGL(msm_join_rest_g, dim3(NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
+                       (const uint32_t*)end.p, NB, (const uint32_t*)spb.p, FX_JOIN_GROUP_C);
   } else {
+    const uint64_t mean_span = m / ((uint64_t)NB * MSM_CH) + 2;
+    for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
+      const uint64_t items = (uint64_t)NB * ((mean_span + 2 * step - 1) / (2 * step));
+      hipLaunchKernelGGL(msm_join_step, dim3((uint32_t)((items + 255) / 256)), dim3(256), 0, a, (ChunkPart*)head.p,
+                         (const uint32_t*)start.p, (const uint32_t*)end.p, NB, step, (const uint32_t*)spb.p, ~0u);
+    }
+    hipLaunchKernelGGL(msm_join_rest, dim3(NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
+                       (const uint32_t*)end.p, NB, (const uint32_t*)spb.p);
+  }
+  if (g.c == 16 && !msm_quad_tail()) {
     hipLaunchKernelGGL(msm_fx_cd, dim3(FX_NH + 256), dim3(256), 0, a, (const Xyzz*)buckets.p, (const ChunkPart*)head.p,
                        (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p);
     hipLaunchKernelGGL(msm_fx_subsets, dim3(16), dim3(128), 0, a, (const Xyzz*)shares.p, (Xyzz*)parts.p);
     hipLaunchKernelGGL(msm_fx_total, dim3(1), dim3(16), 0, a, (const Xyzz*)parts.p, d_result);
+  } else {
+    // C / D sums: quads at c = 16 (latency: 384 short trees), single lanes above (throughput:
+    // 2^18 .. 2^21 buckets); then the subset trees on quads
+    if (g.c == 16 || getenv("PBF_MSM_CD_QUAD")) {  // read per call: an A/B knob
+      auto* cd = g.c == 16 ? msm_fxg_cd_q<64> : msm_fxg_cd_q<128>;
+      const uint32_t qw = g.c == 16 ? 64 : 128;
+      hipLaunchKernelGGL(cd, dim3((uint32_t)nshare), dim3(4 * qw), 0, a, (const Xyzz*)buckets.p,
+                         (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
+                         (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb);
+    } else {
+      const uint32_t cap_seq = fx_chunk_join() ? FX_SEQ_CAP : 1;
+      if (getenv("PBF_MSM_CD_SEQ32"))  // read per call: an A/B knob
+        hipLaunchKernelGGL(msm_fxg_cd_seq<32>, dim3(fxg_cd_seq_groups(g, 32)), dim3(256), 0, a,
+                           (const Xyzz*)buckets.p, (const ChunkPart*)head.p, (const ChunkPart*)tail.p,
+                           (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
+      else
+        hipLaunchKernelGGL(msm_fxg_cd_seq<8>, dim3(fxg_cd_seq_groups(g, 8)), dim3(256), 0, a, (const Xyzz*)buckets.p,
+                           (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
+                           (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
+    }
+    hipLaunchKernelGGL(msm_fxg_subsets_q<128>, dim3(g.lb + g.hb + 1), dim3(512), 0, a, (const Xyzz*)shares.p,
+                       (Xyzz*)parts.p, g.lb, g.hb);
+    hipLaunchKernelGGL(msm_fxg_total_q, dim3(1), dim3(128), 0, a, (const Xyzz*)parts.p, g.lb + g.hb + 1, d_result);
   }
   PBF_HIP(hipGetLastError());
   PBF_HIP(hipEventRecord(tl.done[slot], a));

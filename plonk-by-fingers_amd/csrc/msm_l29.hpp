@@ -85,6 +85,35 @@ __device__ __forceinline__ L29 mul(const L29& a, const L29& b) {
   r.l[8] = (uint32_t)acc;
   return r;
 }
+// mul(a, a) with the square's symmetric column terms taken once, doubled (a_i (2 a_j), i < j:
+// 45 instead of 81 products for a a; 2 a_j < 2^30, so a column of <= 4 doubled terms, a square,
+// 9 m p terms and the carry stays below 18 x 2^58, the bound of mul's columns). The column sums
+// are the same integers as mul's, so the Montgomery digits and the result are identical.
+__device__ __forceinline__ L29 sqr(const L29& a) {
+  uint32_t m[9], a2[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a2[i] = a.l[i] << 1;
+  L29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; ++k) {
+    const int lo = k < 9 ? 0 : k - 8;
+#pragma unroll
+    for (int i = lo; i < k - i; ++i) acc += (uint64_t)a.l[i] * a2[k - i];
+    if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+    for (int i = lo; i < (k < 9 ? k : 9); ++i) acc += (uint64_t)m[i] * P29[k - i];
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * NP29) & MASK;
+      acc += (uint64_t)m[k] * P29[0];
+    } else {
+      r.l[k - 9] = (uint32_t)acc & MASK;
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
 // carry-normalise limbs < 2^32 (value < 2^261)
 __device__ __forceinline__ L29 norm(L29 a) {
 #pragma unroll
@@ -166,6 +195,78 @@ __device__ __forceinline__ Xyzz to_xyzz(const Acc& a) {
   return r;
 }
 
+// x 2^5 (mod p) of a normalised x < p, below 1.0001 p: the shift, then q = floor(y_8 / (P29[8] + 1))
+// (<= floor(32 x / p), so 32 x - q p >= 0, and 32 x - q p < (P29[8] + q + 1) 2^232) subtracted
+// with signed carries. ~50 VALU instead of a product by 2^266 (the domain change of a run's
+// first point: x 2^256 -> x 2^261).
+__device__ __forceinline__ L29 times32(const L29& x) {
+  uint32_t y[9];
+  y[0] = (x.l[0] << 5) & MASK;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) y[i] = ((x.l[i] << 5) | (x.l[i - 1] >> 24)) & MASK;
+  const uint32_t q = y[8] / (P29[8] + 1);
+  L29 r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int64_t v = (int64_t)y[i] - (int64_t)q * P29[i] + c;
+    r.l[i] = (uint32_t)v & MASK;
+    c = v >> 29;  // arithmetic: the borrow (0 after the top limb: the result is positive)
+  }
+  return r;
+}
+
+// a run's first point: X, Y = x 2^261, y 2^261 (the points' x 2^256 times 2^5, below 1.0001 p:
+// within the bounds of a product's output), ZZ = ZZZ = 1 in the x 2^266 domain
+__device__ __forceinline__ void start_run(Acc& a, const L29& x, const L29& y) {
+  a.X = times32(x);
+  a.Y = times32(y);
+  a.ZZ = konst(C266);
+  a.ZZZ = konst(C266);
+  a.id = false;
+}
+// The raw accumulator (36 u32: X, Y, ZZ, ZZZ limbs; ZZ all zero for the identity), stored at a
+// flush instead of the converted point: the conversion (4 products) then runs once per stored
+// sum in a separate, divergence-free kernel (msm.hip msm_l29_finish) rather than inside the
+// accumulation loop, where a wave pays it whenever any of its lanes flushes.
+__device__ __forceinline__ void store_raw(const Acc& a, uint32_t* dst) {
+  uint32_t w[36];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    w[i] = a.X.l[i];
+    w[9 + i] = a.Y.l[i];
+    w[18 + i] = a.id ? 0u : a.ZZ.l[i];
+    w[27 + i] = a.ZZZ.l[i];
+  }
+  uint4* d = (uint4*)dst;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+__device__ __forceinline__ Xyzz raw_to_xyzz(const uint32_t* src) {
+  const uint4* s4 = (const uint4*)src;
+  uint32_t w[36];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint4 v = s4[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+  Acc a;
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    a.X.l[i] = w[i];
+    a.Y.l[i] = w[9 + i];
+    a.ZZ.l[i] = w[18 + i];
+    a.ZZZ.l[i] = w[27 + i];
+    z |= w[18 + i];
+  }
+  a.id = z == 0;
+  return to_xyzz(a);
+}
+
 // acc += (x, y) (affine point, 29-bit limbs of its 32-bit Montgomery coordinates):
 // madd-2008-s. Returns true in the exceptional case P + P (the caller replaces acc by the
 // doubled point): P == 0 is detected through ZZ3 = ZZ PP == 0 (PP == 0 iff P == 0, ZZ != 0),
@@ -173,17 +274,12 @@ __device__ __forceinline__ Xyzz to_xyzz(const Acc& a) {
 // input dies as early as it can (the accumulation kernel is register-bound).
 __device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
   if (a.id) {
-    const L29 one = konst(C266);
-    a.X = mul(x, one);
-    a.Y = mul(y, one);
-    a.ZZ = one;
-    a.ZZZ = one;
-    a.id = false;
+    start_run(a, x, y);
     return false;
   }
   const L29 P = sub(mul(x, a.ZZ), a.X, M16P);
   const L29 R = sub(mul(y, a.ZZZ), a.Y, M16P);
-  const L29 PP = mul(P, P);
+  const L29 PP = sqr(P);
   const L29 ZZ3 = mul(a.ZZ, PP);
   if (zero_mod_p(ZZ3)) {  // P == 0: doubling (R == 0) or the identity
     L29 one{};
@@ -196,7 +292,7 @@ __device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
   const L29 YP = mul(a.Y, PPP);
   a.ZZZ = mul(a.ZZZ, PPP);
   const L29 Q = mul(a.X, PP);
-  const L29 RR = mul(R, R);
+  const L29 RR = sqr(R);
   L29 X3;
 #pragma unroll
   for (int i = 0; i < 9; ++i) X3.l[i] = RR.l[i] + M8P[i] - PPP.l[i] - 2 * Q.l[i];

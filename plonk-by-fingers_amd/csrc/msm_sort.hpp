@@ -1,6 +1,7 @@
 // Hand-written stable LSD radix sort of (key, value) u32 pairs for the MSM's bucket sort
-// (gfx950; round 3, replacing hipcub::DeviceRadixSort). Keys are bucket ids of at most 20
-// bits (the fixed-base form: 16 bits, the windowed form: 20), so 2-3 passes of 8-bit digits.
+// (gfx950; round 3, replacing hipcub::DeviceRadixSort). Keys are bucket ids of at most 24
+// bits (the fixed-base form: 16, 20 or 22 bits, the windowed form: 20), so 2-3 passes of
+// digits of at most 8 bits.
 // Each pass is three kernels and touches no global atomics:
 //   rs_hist     per tile of RS_TILE entries: its digit histogram (LDS atomics) -> hist[d][tile]
 //   rs_scan     per digit: exclusive prefix over the tiles, in place, and the digit's total
@@ -9,10 +10,11 @@
 //               rounds; the per-wave counts, scanned, order the waves), a locally sorted copy
 //               of the tile in LDS, then every digit's run written to its global position
 //               (consecutive lanes write consecutive addresses of a run)
-// A pass may read its input from RsDigits instead of (keys, vals): the fixed-base MSM's first
-// pass takes planar 16-bit signed digits and derives each entry's key and value from the digit
-// and the entry index, so the digit kernel writes 2 B per entry instead of 8 and the first
-// pass reads 2 B instead of 4 (histogram) and 8 (scatter).
+// A pass may read its input from RsDigitsT instead of (keys, vals): the fixed-base MSM's first
+// pass takes planar 16-bit (32-bit for windows wider than 16 bits) signed digits and derives
+// each entry's key and value from the digit and the entry index, so the digit kernel writes
+// 2 (4) B per entry instead of 8 and the first pass reads 2 (4) B instead of 4 (histogram)
+// and 8 (scatter).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -29,25 +31,33 @@ namespace pbf {
 // the largest (it bounds m).
 constexpr int RS_T = 256, RS_ITEMS = PBF_RS_ITEMS, RS_TILE = RS_T * 16, RS_TILE_MAX = RS_T * 64;
 
-// 16-bit signed digit code: |d| - 1 for d > 0, 0x8000 | (|d| - 1) for d < 0, RS_DIG_NONE for
+// Signed digit code of C = uint16_t (windows of up to 16 bits) or uint32_t (wider fixed-base
+// windows): |d| - 1 for d > 0, the top bit | (|d| - 1) for d < 0, all ones (rs_none<C>) for
 // no entry (a zero digit or an identity point)
 constexpr uint16_t RS_DIG_NONE = 0xFFFF;
-struct RsDigits {
-  const uint16_t* dig;  // dig[w * n + i]: window w's digit code of scalar i
-  uint32_t n;           // scalars
-  uint32_t n_table;     // value of entry (w, i) = w * n_table + first + i, | neg if d < 0
+template <typename C>
+__host__ __device__ constexpr uint32_t rs_none() { return (uint32_t)(C)~(C)0; }
+template <typename C>
+__host__ __device__ constexpr uint32_t rs_sign() { return (uint32_t)1 << (8 * sizeof(C) - 1); }
+template <typename C>
+struct RsDigitsT {
+  const C* dig;       // dig[w * n + i]: window w's digit code of scalar i
+  uint32_t n;         // scalars
+  uint32_t n_table;   // value of entry (w, i) = w * n_table + first + i, | neg if d < 0
   uint32_t first;
   uint32_t kw;    // key of entry (w, i) = w * kw + (|d| - 1) (fixed base: 0; windowed: 2^15)
-  uint32_t zkey;  // key of RS_DIG_NONE (sorts last)
+  uint32_t zkey;  // key of a no-entry code (sorts last)
   uint32_t neg;   // sign flag of the value
 };
-__device__ __forceinline__ uint32_t rs_dig_key(uint16_t c, uint32_t w, const RsDigits& dg) {
-  return c == RS_DIG_NONE ? dg.zkey : w * dg.kw + (c & 0x7FFFu);
+using RsDigits = RsDigitsT<uint16_t>;
+template <typename C>
+__device__ __forceinline__ uint32_t rs_dig_key(uint32_t c, uint32_t w, const RsDigitsT<C>& dg) {
+  return c == rs_none<C>() ? dg.zkey : w * dg.kw + (c & (rs_sign<C>() - 1));
 }
 
-template <int ITEMS, bool DIG = false>
-__global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m, uint32_t shift, uint32_t ntiles,
-                                                uint32_t* hist, RsDigits dg) {
+template <int ITEMS, bool DIG = false, typename C = uint16_t>
+__global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m, uint32_t shift, uint32_t mask,
+                                                uint32_t ntiles, uint32_t* hist, RsDigitsT<C> dg) {
   __shared__ uint32_t h[RS_T / 64][256];  // one histogram per wave (less atomic contention)
   const int wave = threadIdx.x >> 6;
 #pragma unroll
@@ -60,8 +70,8 @@ __global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m
 #pragma unroll
     for (int u = 0; u < ITEMS; ++u) {
       const uint32_t e = base + u * RS_T + threadIdx.x;
-      const uint16_t c = e < m ? dg.dig[e] : RS_DIG_NONE;
-      k[u] = e < m ? (c == RS_DIG_NONE ? dg.zkey : c & 0x7FFFu) : 0xFFFFFFFFu;
+      const uint32_t c = e < m ? (uint32_t)dg.dig[e] : rs_none<C>();
+      k[u] = e < m ? (c == rs_none<C>() ? dg.zkey : c & (rs_sign<C>() - 1)) : 0xFFFFFFFFu;
     }
   } else {
 #pragma unroll
@@ -72,7 +82,7 @@ __global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m
   }
 #pragma unroll
   for (int u = 0; u < ITEMS; ++u)
-    if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[wave][(k[u] >> shift) & 255], 1u);
+    if (k[u] != 0xFFFFFFFFu) atomicAdd(&h[wave][(k[u] >> shift) & mask], 1u);
   __syncthreads();
   uint32_t c = 0;
 #pragma unroll
@@ -127,10 +137,11 @@ __global__ void __launch_bounds__(RS_T) rs_scan(uint32_t* hist, uint32_t ntiles,
 // locally sorted copy of the tile in LDS, and each digit's run is written to its global
 // position.
 constexpr int RS_WAVES = RS_T / 64;
-template <int ITEMS, bool DIG = false>
+template <int ITEMS, bool DIG = false, typename C = uint16_t>
 __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) rs_scatter(const uint32_t* keys, const uint32_t* vals, uint32_t* okeys,
-                                                   uint32_t* ovals, uint32_t m, uint32_t shift, uint32_t ntiles,
-                                                   const uint32_t* hist, const uint32_t* total, RsDigits dg) {
+                                                   uint32_t* ovals, uint32_t m, uint32_t shift, uint32_t mask,
+                                                   uint32_t ntiles, const uint32_t* hist, const uint32_t* total,
+                                                   RsDigitsT<C> dg) {
   __shared__ uint32_t s[RS_T];
   __shared__ uint32_t gbase[256], lstart[256];
   __shared__ uint32_t wc[RS_WAVES][256];
@@ -148,7 +159,7 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const uint32_t e = e0 + r * 64;
-      key[r] = e < m ? dg.dig[e] : RS_DIG_NONE;
+      key[r] = e < m ? (uint32_t)dg.dig[e] : rs_none<C>();
     }
   } else {
 #pragma unroll
@@ -177,7 +188,8 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const bool valid = base + wave * RS_WQ + r * 64 + lane < m;
-    const uint32_t d = DIG ? (key[r] == RS_DIG_NONE ? dg.zkey : key[r] & 0x7FFFu) & 255 : (key[r] >> shift) & 255;
+    const uint32_t d =
+        DIG ? (key[r] == rs_none<C>() ? dg.zkey : key[r] & (rs_sign<C>() - 1)) & mask : (key[r] >> shift) & mask;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -209,11 +221,11 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       if (e0 + r * 64 < m) {
-        const uint32_t c = key[r], k = rs_dig_key((uint16_t)c, w, dg);
-        const uint32_t d = k & 255;
+        const uint32_t c = key[r], k = rs_dig_key(c, w, dg);
+        const uint32_t d = k & mask;
         const uint32_t pos = lstart[d] + wc[wave][d] + rank[r];
         lk[pos] = k;
-        lv[pos] = (w * dg.n_table + dg.first + i) | (c != RS_DIG_NONE && (c & 0x8000u) ? dg.neg : 0u);
+        lv[pos] = (w * dg.n_table + dg.first + i) | (c != rs_none<C>() && (c & rs_sign<C>()) ? dg.neg : 0u);
       }
       i += 64;
       const bool wrap = i >= dg.n;
@@ -224,7 +236,7 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       if (e0 + r * 64 < m) {
-        const uint32_t d = (key[r] >> shift) & 255;
+        const uint32_t d = (key[r] >> shift) & mask;
         const uint32_t pos = lstart[d] + wc[wave][d] + rank[r];
         lk[pos] = key[r];
         lv[pos] = val[r];
@@ -238,7 +250,7 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
     const uint32_t i = r * RS_T + t;
     if (i < count) {
       const uint32_t k = lk[i];
-      const uint32_t d = (k >> shift) & 255;
+      const uint32_t d = (k >> shift) & mask;
       const uint32_t o = gbase[d] + (i - lstart[d]);
       okeys[o] = k;
       ovals[o] = lv[i];
@@ -246,21 +258,30 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
   }
 }
 
-// One pass: (kin, vin) (or dg) -> (kout, vout) stably sorted by key bits [shift, shift + 8).
+// One pass: (kin, vin) (or dg) -> (kout, vout) stably sorted by key bits [shift, shift + dbits),
+// dbits <= 8 (narrower digits: longer runs per digit and tile on the store side).
 // hist: 256 * ntiles + 256 u32 of scratch.
-// DIG (pass 1 only, shift 0) requires dg.n >= RS_T (rs_dig_ok) and dg.kw % 256 == 0.
+// DIG (pass 1 only, shift 0) requires dg.n >= RS_T (rs_dig_ok) and dg.kw % 2^dbits == 0.
 inline bool rs_dig_ok(uint64_t n) { return n >= (uint64_t)RS_T; }
-template <int ITEMS = RS_ITEMS, bool DIG = false>
+template <int ITEMS = RS_ITEMS, bool DIG = false, typename C = uint16_t>
 inline void rs_pass(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout, uint32_t m,
-                    uint32_t shift, uint32_t* hist, hipStream_t s, RsDigits dg = {}) {
+                    uint32_t shift, uint32_t* hist, hipStream_t s, RsDigitsT<C> dg = {}, int dbits = 8) {
   constexpr uint32_t TILE = RS_T * ITEMS;
   static_assert(ITEMS >= 16 && TILE <= RS_TILE_MAX, "the scratch is sized for RS_TILE .. RS_TILE_MAX");
-  const uint32_t ntiles = (m + TILE - 1) / TILE;
+  const uint32_t ntiles = (m + TILE - 1) / TILE, mask = (1u << dbits) - 1;
   uint32_t* total = hist + 256ull * ntiles;
-  hipLaunchKernelGGL((rs_hist<ITEMS, DIG>), dim3(ntiles), dim3(RS_T), 0, s, kin, m, shift, ntiles, hist, dg);
+  hipLaunchKernelGGL((rs_hist<ITEMS, DIG, C>), dim3(ntiles), dim3(RS_T), 0, s, kin, m, shift, mask, ntiles, hist, dg);
   hipLaunchKernelGGL(rs_scan, dim3(256), dim3(RS_T), 0, s, hist, ntiles, total);
-  hipLaunchKernelGGL((rs_scatter<ITEMS, DIG>), dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, m, shift, ntiles,
-                     (const uint32_t*)hist, (const uint32_t*)total, dg);
+  hipLaunchKernelGGL((rs_scatter<ITEMS, DIG, C>), dim3(ntiles), dim3(RS_T), 0, s, kin, vin, kout, vout, m, shift, mask,
+                     ntiles, (const uint32_t*)hist, (const uint32_t*)total, dg);
+}
+
+// digit widths of a `bits`-bit sort: ceil(bits / 8) passes, widths as equal as possible (the
+// wider ones first): 16 -> 8, 8; 20 -> 7, 7, 6; 22 -> 8, 7, 7
+inline int rs_passes(int bits) { return (bits + 7) / 8; }
+inline int rs_width(int bits, int p) {
+  const int np = rs_passes(bits), base = bits / np;
+  return base + (p < bits % np ? 1 : 0);
 }
 
 // Sort m pairs by key bits [0, bits): keys/vals -> keys2/vals2 (inputs unchanged; tmpk / tmpv:
@@ -269,15 +290,17 @@ template <int ITEMS = RS_ITEMS>
 inline int rs_sort(const uint32_t* keys, const uint32_t* vals, uint32_t* keys2, uint32_t* vals2, uint32_t* tmpk,
                    uint32_t* tmpv, uint32_t m, int bits, uint32_t* hist, hipStream_t s) {
   if (m == 0) return 0;
-  const int passes = (bits + 7) / 8;
+  const int passes = rs_passes(bits);
   // pass p reads (k_in, v_in) and writes (k_out, v_out); the last pass writes keys2 / vals2
   const uint32_t* kin = keys;
   const uint32_t* vin = vals;
+  int shift = 0;
   for (int p = 0; p < passes; ++p) {
     // an even number of passes left after this one writes tmp, else keys2 (so the last lands there)
     uint32_t* kout = ((passes - 1 - p) % 2 == 0) ? keys2 : tmpk;
     uint32_t* vout = ((passes - 1 - p) % 2 == 0) ? vals2 : tmpv;
-    rs_pass<ITEMS>(kin, vin, kout, vout, m, (uint32_t)(8 * p), hist, s);
+    rs_pass<ITEMS>(kin, vin, kout, vout, m, (uint32_t)shift, hist, s, RsDigits{}, rs_width(bits, p));
+    shift += rs_width(bits, p);
     kin = kout;
     vin = vout;
   }

@@ -72,6 +72,45 @@ def test_product_matches_montgomery():
         assert value(r) < x * y // (1 << 261) + P + 1
 
 
+def sqr29(a):
+    """csrc/msm_l29.hpp l29::sqr, step for step: the doubled symmetric terms taken once."""
+    p29, np29 = C["P29"], C["NP29"][0]
+    a2 = [2 * v for v in a]
+    m = [0] * 9
+    r = [0] * 9
+    acc = 0
+    for k in range(17):
+        lo = 0 if k < 9 else k - 8
+        i = lo
+        while i < k - i:
+            acc += a[i] * a2[k - i]
+            i += 1
+        if k % 2 == 0:
+            acc += a[k // 2] * a[k // 2]
+        for i in range(lo, k if k < 9 else 9):
+            acc += m[i] * p29[k - i]
+        assert acc < 1 << 64, "column overflow"
+        if k < 9:
+            m[k] = ((acc & 0xFFFFFFFF) * np29) & MASK
+            acc += m[k] * p29[0]
+            assert acc & MASK == 0
+        else:
+            r[k - 9] = acc & MASK
+        acc >>= 29
+    r[8] = acc
+    return r
+
+
+def test_square_matches_product():
+    """l29::sqr (PP = P^2, RR = R^2 of madd-2008-s) is bit-identical to l29::mul(a, a) up to the
+    largest value a square takes (17.02 p) and at the 2^261 limit of the product's inputs."""
+    rng = random.Random(261)
+    cases = [0, 1, P - 1, int(17.02 * P), (1 << 261) - 1] + [rng.randrange(18 * P) for _ in range(500)]
+    for x in cases:
+        a = norm(limbs(x)) if x < 1 << 261 else limbs(x)
+        assert sqr29(a) == mul29(a, a)
+
+
 def norm(l):
     l = list(l)
     for i in range(8):
@@ -86,6 +125,32 @@ def sub(a, b, M):
     return norm(r)
 
 
+def times32(x):
+    """csrc/msm_l29.hpp l29::times32, step for step (a run's first point: x 2^5 mod p)."""
+    p29 = C["P29"]
+    y = [(x[0] << 5) & MASK] + [((x[i] << 5) | (x[i - 1] >> 24)) & MASK for i in range(1, 9)]
+    q = y[8] // (p29[8] + 1)
+    r, c = [0] * 9, 0
+    for i in range(9):
+        v = y[i] - q * p29[i] + c
+        r[i] = v & MASK
+        c = v >> 29
+    assert c == 0
+    return r
+
+
+def test_times32_start_of_run():
+    """The run start's x 2^5 by shift and one estimated subtraction: the residue of the product
+    by 2^266 it replaces, normalised, below 1.0001 p (inside the product's output bound)."""
+    rng = random.Random(32)
+    for x in [0, 1, P - 1, P // 2, (P * 31) // 32] + [rng.randrange(P) for _ in range(2000)]:
+        r = times32(limbs(x))
+        assert value(r) % P == x * 32 % P
+        assert all(v <= MASK for v in r)
+        assert value(r) < 1.0001 * P
+        assert value(r) % P == value(mul29(limbs(x), limbs(pow(2, 266, P)))) % P
+
+
 def test_lazy_madd_chain_bounds():
     """Random madd-2008-s chains in the kernel's domains and order: every intermediate stays
     within the derived bounds, and the chain's (X, Y, ZZ, ZZZ) agree with plain arithmetic."""
@@ -97,18 +162,18 @@ def test_lazy_madd_chain_bounds():
             x, y = rng.randrange(P), rng.randrange(P)
             x256, y256 = limbs(x * 2 ** 256 % P), limbs(y * 2 ** 256 % P)
             if X is None:
-                X, Y = mul29(x256, one), mul29(y256, one)
+                X, Y = times32(x256), times32(y256)
                 ZZ = ZZZ = one
                 continue
             Pv = sub(mul29(x256, ZZ), X, C["M16P"])
             R = sub(mul29(y256, ZZZ), Y, C["M16P"])
-            PP = mul29(Pv, Pv)
+            PP = sqr29(Pv)
             ZZ3 = mul29(ZZ, PP)
             PPP = mul29(Pv, PP)
             YP = mul29(Y, PPP)
             ZZZ = mul29(ZZZ, PPP)
             Q = mul29(X, PP)
-            RR = mul29(R, R)
+            RR = sqr29(R)
             X3 = [RR[i] + C["M8P"][i] - PPP[i] - 2 * Q[i] for i in range(9)]
             assert all(0 <= v < 1 << 32 for v in X3)
             X3 = norm(X3)

@@ -271,3 +271,77 @@ def test_fixed_base_msm_2p20_discrete_log(ctx):
     k = sum(a * b for a, b in zip(tv, sv)) % R
     assert got == enc(bn254.g1_mul(bn254.G1_GEN, k))
     del rng
+
+
+@pytest.mark.parametrize("c", [16, 18, 20, 22])
+def test_fixed_base_window_widths(ctx, monkeypatch, c):
+    """The fixed-base table's window width (PBF_MSM_FX_C, round 4: ceil(255 / c) windows of
+    2^(c-1) signed-digit buckets, 32-bit digit codes above c = 16, sorts of c key bits in passes
+    of balanced digit widths, the generalised quad reduction tail) gives the windowed MSM's
+    result: random scalars, digits at the c-bit recoding boundaries with carry chains, zero
+    scalars, tiles straddling windows, both sorts' first passes, and a point range."""
+    rnd = random.Random(c)
+    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    h = 1 << (c - 1)
+    edges = [h - 1, h, h + 1, (1 << c) - 1, 1, 0]
+    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(41)]
+    for n_points, n, kind in [(300, 300, "random"), (3000, 3000, "edges"), (70001, 70001, "random"),
+                              (5000, 5000, "equal")]:
+        pts = (base * (n_points // len(base) + 1))[:n_points]
+        if kind == "random":
+            sc = [rnd.randrange(R) for _ in range(n)]
+            sc[::97] = [0] * len(sc[::97])
+        elif kind == "edges":
+            sc = [sum(rnd.choice(edges) << (c * w) for w in range(256 // c + 1)) % R for _ in range(n)]
+        else:
+            sc = [rnd.randrange(R)] * n
+        dp, ds = _dev_points(pts), _dev_scalars(sc)
+        want = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n)
+        for fused in ("1", "0"):
+            monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
+            assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n) == want, (c, kind, fused)
+        if n == 300:
+            assert want == enc(bn254.msm_naive(pts, sc))
+    monkeypatch.setenv("PBF_MSM_FUSED_SORT", "1")
+    first, n = 8193, 40000
+    pts = (base * (70001 // len(base) + 1))[:70001]
+    sc = [rnd.randrange(R) for _ in range(n)]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    got = ctx.msm_g1_fixed_range_dev(dp.data_ptr(), len(pts), first, ds.data_ptr(), n)
+    assert got == ctx.msm_g1_dev(_dev_points(pts[first:first + n]).data_ptr(), ds.data_ptr(), n)
+    ctx.release_caches()
+
+
+@pytest.mark.parametrize("c", [20, 22])
+def test_fixed_base_wide_windows_2p20_discrete_log(ctx, monkeypatch, c):
+    """Config 4's size with the wide-window table: P_i = t_i G, result (sum s_i t_i) G."""
+    import torch
+
+    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    m = 1 << 20
+    t = bn254.random_limbs(m, 45 + c)
+    s = bn254.random_limbs(m, 46 + c)
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    dsc = torch.from_numpy(s.view(np.int64)).cuda()
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(dt.data_ptr(), pts.data_ptr(), m)
+    got = ctx.msm_g1_fixed_dev(pts.data_ptr(), m, dsc.data_ptr(), m)
+    tv, sv = bn254.limbs_to_ints(t), bn254.limbs_to_ints(s)
+    k = sum(a * b for a, b in zip(tv, sv)) % R
+    assert got == enc(bn254.g1_mul(bn254.G1_GEN, k))
+    ctx.release_caches()
+
+
+def test_sort_digit_widths_knob(ctx, monkeypatch):
+    """The windowed MSM's 20-bit sort in balanced 7/7/6-bit passes (default) and in 8/8/4
+    (PBF_MSM_SORT_W8=1) give the same result."""
+    rnd = random.Random(77)
+    n = 70001
+    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(29)]
+    pts = (base * (n // len(base) + 1))[:n]
+    sc = [rnd.randrange(R) for _ in range(n)]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    a = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n)
+    monkeypatch.setenv("PBF_MSM_SORT_W8", "1")
+    assert ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n) == a
+    assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n, ds.data_ptr(), n) == a
