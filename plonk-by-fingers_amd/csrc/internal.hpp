@@ -26,6 +26,12 @@ inline bool env_default_on(const char* name) {
   const char* e = getenv(name);
   return !(e && *e && atoi(e) == 0);
 }
+// A/B switch that is off by default: on only when the variable parses as a nonzero integer
+// ("1"); unset, empty or "0" keeps it off. Read per call.
+inline bool env_default_off(const char* name) {
+  const char* e = getenv(name);
+  return e && *e && atoi(e) != 0;
+}
 int fail(int code, const std::string& s);
 
 #define PBF_HIP(expr)                                                                        \

@@ -360,7 +360,7 @@ static bool msm_l29() {
 // (2^24 points: 32.5 against 32.0 ms). PBF_MSM_RAWFLUSH=0/1 forces either (A/B).
 static bool msm_rawflush(bool short_runs = true) {
   const char* e = getenv("PBF_MSM_RAWFLUSH");  // read per call: an A/B knob
-  if (e) return atoi(e) != 0;
+  if (e && *e) return atoi(e) != 0;
   return short_runs;
 }
 
@@ -805,7 +805,10 @@ __global__ void __launch_bounds__(64) msm_fx_total_q(const Xyzz* sub, Xyzz* out)
 static bool msm_quad_tail() {
   return env_default_on("PBF_MSM_QUAD");  // read per call: an A/B knob
 }
-// the fixed-base join indexed by chunk (msm_join_chunks, default) or by bucket (=0: A/B)
+// the wide-window join: light buckets summed in sequence by the C / D sums, heavy ones by
+// msm_join_chunks (default), or every bucket by the per-bucket steps (=0: A/B). The c = 16 form
+// always takes the per-bucket steps: its spans are even (random scalars: a 14-bit top window),
+// and the per-chunk steps would be a dozen idle launches per MSM on the tail stream.
 static bool fx_chunk_join() {
   return env_default_on("PBF_MSM_CHUNK_JOIN");  // read per call: an A/B knob
 }
@@ -1051,7 +1054,7 @@ static bool msm_fused_sort() {
 // digit width of pass p of a `bits`-bit sort: as equal as possible (msm_sort.hpp rs_width);
 // PBF_MSM_SORT_W8=1 keeps every pass but the last at 8 bits (A/B)
 static int msm_sort_width(int bits, int p) {
-  if (getenv("PBF_MSM_SORT_W8")) {  // read per call: an A/B knob
+  if (env_default_off("PBF_MSM_SORT_W8")) {  // read per call: an A/B knob
     const int rest = bits - 8 * p;
     return rest < 8 ? rest : 8;
   }
@@ -1441,13 +1444,13 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   // join steps 1 .. FX_JOIN_GROUP / 2 (steps past the largest span exit at once); wider spans
   // are finished by msm_join_rest. The grid covers the mean span's pair slots (the kernel
   // strides over the rest).
-  if (fx_chunk_join()) {
+  if (g.c > 16 && fx_chunk_join()) {
     // buckets spanning up to `cap` chunks (twice the mean span, a power of two): the per-bucket
     // steps; heavier ones: the per-chunk steps up to FX_JOIN_GROUP_C / 2 (both exit at once past
     // the largest span), then msm_join_rest_g
     // wide windows (single-lane C / D sums): buckets spanning up to FX_SEQ_CAP chunks are not
     // joined at all, fx_bucket_into adds their continuations in sequence
-    const bool wide = !(g.c == 16 || getenv("PBF_MSM_CD_QUAD"));
+    const bool wide = !(g.c == 16 || env_default_off("PBF_MSM_CD_QUAD"));
     const uint64_t mean_span = m / ((uint64_t)NB * MSM_CH) + 2;
     uint32_t cap = 2;
     while (cap < 2 * mean_span && cap < FX_JOIN_GROUP_C) cap <<= 1;
@@ -1482,15 +1485,15 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   } else {
     // C / D sums: quads at c = 16 (latency: 384 short trees), single lanes above (throughput:
     // 2^18 .. 2^21 buckets); then the subset trees on quads
-    if (g.c == 16 || getenv("PBF_MSM_CD_QUAD")) {  // read per call: an A/B knob
+    if (g.c == 16 || env_default_off("PBF_MSM_CD_QUAD")) {  // read per call: an A/B knob
       auto* cd = g.c == 16 ? msm_fxg_cd_q<64> : msm_fxg_cd_q<128>;
       const uint32_t qw = g.c == 16 ? 64 : 128;
       hipLaunchKernelGGL(cd, dim3((uint32_t)nshare), dim3(4 * qw), 0, a, (const Xyzz*)buckets.p,
                          (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
                          (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb);
     } else {
-      const uint32_t cap_seq = fx_chunk_join() ? FX_SEQ_CAP : 1;
-      if (getenv("PBF_MSM_CD_SEQ32"))  // read per call: an A/B knob
+      const uint32_t cap_seq = g.c > 16 && fx_chunk_join() ? FX_SEQ_CAP : 1;
+      if (env_default_off("PBF_MSM_CD_SEQ32"))  // read per call: an A/B knob
         hipLaunchKernelGGL(msm_fxg_cd_seq<32>, dim3(fxg_cd_seq_groups(g, 32)), dim3(256), 0, a,
                            (const Xyzz*)buckets.p, (const ChunkPart*)head.p, (const ChunkPart*)tail.p,
                            (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
