@@ -102,6 +102,7 @@ int pbf_ctx_release_caches(pbf_ctx* ctx) {
   PBF_HIP(hipSetDevice(ctx->device));
   PBF_HIP(hipStreamSynchronize(ctx->stream));
   if (ctx->msm_tail.aux) PBF_HIP(hipStreamSynchronize(ctx->msm_tail.aux));
+  if (ctx->msm_tail.prep) PBF_HIP(hipStreamSynchronize(ctx->msm_tail.prep));
   PBF_HIP(hipDeviceSynchronize());  // _dev callers' streams may still read the caches
   ctx->pk_key.clear();
   ctx->vk_key.clear();

@@ -122,14 +122,26 @@ struct ForkSet {
 // stream while the caller's stream goes on; MSM_TAIL_SLOTS workspaces rotate between the
 // MSMs in flight. msm_fixed_wait orders a stream after every tail enqueued so far.
 constexpr int MSM_TAIL_SLOTS = 3;
+// The prep stream (round 4, opt-in PBF_MSM_PREP=1: measured no faster, msm.hip
+// msm_scalars_ready): a caller that commits several polynomials that are all ready
+// (msm_scalars_ready, then msm_fixed_device with that event) gets each MSM's digits, sort and
+// bucket bounds enqueued on `prep`, so they run while the caller's stream accumulates the
+// previous MSM (the sort is memory-bound, the accumulation VALU-bound). MSM_PREP_SLOTS sets of
+// sort buffers rotate; prep_free[p] (recorded after the accumulation that read slot p) orders
+// their reuse.
+constexpr int MSM_PREP_SLOTS = 2;
 struct MsmTail {
   int device = 0;
   hipStream_t aux = nullptr;
   hipEvent_t ready[MSM_TAIL_SLOTS] = {}, done[MSM_TAIL_SLOTS] = {};
   bool used[MSM_TAIL_SLOTS] = {};
   int next = 0, last = -1;
+  hipStream_t prep = nullptr;
+  hipEvent_t prep_done[MSM_PREP_SLOTS] = {}, prep_free[MSM_PREP_SLOTS] = {}, sc_ready = nullptr;
+  bool prep_used[MSM_PREP_SLOTS] = {};
+  int prep_next = 0;
   int ensure();
-  ~MsmTail();  // waits for the side stream (declared after the buffers it uses)
+  ~MsmTail();  // waits for the side streams (declared after the buffers they use)
 };
 
 // Round-3 schedule of a plan with p.ip (ntt_ip.hip): the whole batch, scratch s0

@@ -271,7 +271,10 @@ msm_chunk_acc_l29(const Affine* pts, const uint32_t* keys, const uint32_t* vals,
 // executed it at every entry where any lane flushed: with ~100 entries per bucket (wide
 // fixed-base windows, the windowed form) that is most entries. hkey[t] / tkey[t]: the key of
 // chunk t's head / tail partial (the sentinel: none), compact for the join and the finish.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE)))
+#ifndef PBF_MSM_ACC_WPE_R
+#define PBF_MSM_ACC_WPE_R 3
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_MSM_ACC_WPE_R)))
 msm_chunk_acc_l29r(const Affine* pts, const uint32_t* keys, const uint32_t* vals, const uint32_t* start,
                    const uint32_t* end, uint32_t m, uint32_t* braw, ChunkPart* head, ChunkPart* tail, uint32_t sent,
                    const uint32_t* m_dev, uint32_t* hkey, uint32_t* tkey) {
@@ -1034,9 +1037,9 @@ static MsmWork msm_work(pbf_ctx* ctx) {
 // (key, value) pairs sorted by key bits [0, bits) into keys2 / vals2 (msm_sort.hpp), with the
 // context's scratch
 static int msm_sort_pairs(pbf_ctx* ctx, const uint32_t* keys, const uint32_t* vals, uint32_t* keys2, uint32_t* vals2,
-                          uint64_t m, int bits, hipStream_t s) {
+                          uint64_t m, int bits, hipStream_t s, const std::string& pre = "msm.") {
   if (m > 0xFFFFFFFFull - RS_TILE_MAX) return fail(PBF_EINVAL, "too many MSM entries");
-  DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
+  DevBuf &tk = ctx->buf(pre + "sort.k"), &tv = ctx->buf(pre + "sort.v"), &hb = ctx->buf(pre + "sort.hist");
   const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
   int rc;
   if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
@@ -1064,12 +1067,12 @@ static int msm_sort_width(int bits, int p) {
 // the caller's mid_k / mid_v buffers, free once the codes are read)
 template <typename C>
 static int msm_sort_digits(pbf_ctx* ctx, const RsDigitsT<C>& dg, uint32_t* keys2, uint32_t* vals2, uint32_t* mid_k,
-                           uint32_t* mid_v, uint64_t m, int bits, hipStream_t s) {
+                           uint32_t* mid_v, uint64_t m, int bits, hipStream_t s, const std::string& pre = "msm.") {
   if (m > 0xFFFFFFFFull - RS_TILE_MAX) return fail(PBF_EINVAL, "too many MSM entries");
   const int passes = rs_passes(bits), w0 = msm_sort_width(bits, 0);
   if (bits < 9 || bits > 24 || dg.kw % (1u << w0) || !rs_dig_ok(dg.n) || (passes == 3 && (!mid_k || !mid_v)))
     return fail(PBF_EINVAL, "digit sort: 9..24 key bits, whole first-pass digits per window, n >= 256");
-  DevBuf &tk = ctx->buf("msm.sort.k"), &tv = ctx->buf("msm.sort.v"), &hb = ctx->buf("msm.sort.hist");
+  DevBuf &tk = ctx->buf(pre + "sort.k"), &tv = ctx->buf(pre + "sort.v"), &hb = ctx->buf(pre + "sort.hist");
   const uint64_t ntiles = (m + RS_TILE - 1) / RS_TILE;
   int rc;
   if ((rc = tk.ensure(m * 4)) || (rc = tv.ensure(m * 4)) || (rc = hb.ensure((256 * ntiles + 256) * 4))) return rc;
@@ -1316,21 +1319,45 @@ int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_
 int MsmTail::ensure() {
   if (aux) return 0;
   PBF_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+  PBF_HIP(hipStreamCreateWithFlags(&prep, hipStreamNonBlocking));
   for (int i = 0; i < MSM_TAIL_SLOTS; ++i) {
     PBF_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
     PBF_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
   }
+  for (int i = 0; i < MSM_PREP_SLOTS; ++i) {
+    PBF_HIP(hipEventCreateWithFlags(&prep_done[i], hipEventDisableTiming));
+    PBF_HIP(hipEventCreateWithFlags(&prep_free[i], hipEventDisableTiming));
+  }
+  PBF_HIP(hipEventCreateWithFlags(&sc_ready, hipEventDisableTiming));
   return 0;
 }
 MsmTail::~MsmTail() {
   if (!aux) return;
   (void)hipSetDevice(device);
+  if (prep) (void)hipStreamSynchronize(prep);
   (void)hipStreamSynchronize(aux);
+  if (prep) (void)hipStreamDestroy(prep);
   (void)hipStreamDestroy(aux);
   for (int i = 0; i < MSM_TAIL_SLOTS; ++i) {
     if (ready[i]) (void)hipEventDestroy(ready[i]);
     if (done[i]) (void)hipEventDestroy(done[i]);
   }
+  for (int i = 0; i < MSM_PREP_SLOTS; ++i) {
+    if (prep_done[i]) (void)hipEventDestroy(prep_done[i]);
+    if (prep_free[i]) (void)hipEventDestroy(prep_free[i]);
+  }
+  if (sc_ready) (void)hipEventDestroy(sc_ready);
+}
+
+// Opt-in (PBF_MSM_PREP=1): measured in the prover (profiles/r04/prep_ab.log) at 2^20 gates 25.3-26.0
+// ms against 24.8 ms without it, at 2^24 gates 324.8-325.9 against 328.9 ms -- the sort kernels
+// take CU slots from the VALU-bound accumulation they run beside, which slows it by about as
+// much as their own time.
+hipEvent_t msm_scalars_ready(pbf_ctx* ctx, hipStream_t s) {
+  if (!env_default_off("PBF_MSM_PREP")) return nullptr;  // read per call: an A/B knob
+  MsmTail& t = ctx->msm_tail;
+  if (t.ensure() || hipEventRecord(t.sc_ready, s) != hipSuccess) return nullptr;  // one stream then
+  return t.sc_ready;
 }
 
 int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s) {
@@ -1347,7 +1374,7 @@ int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s) {
 // the bucket reduction (latency-bound chains of a few hundred waves), overlapping whatever
 // the caller enqueues next on `s`.
 int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64_t first, const uint64_t* d_sc,
-                     uint64_t n, hipStream_t s, Xyzz* d_result) {
+                     uint64_t n, hipStream_t s, Xyzz* d_result, hipEvent_t sc_ready) {
   if (first + n > n_table) return fail(PBF_EINVAL, "fixed-base MSM: range beyond the table");
   auto& fb = ctx->fixed_base;
   if ((const void*)table != fb.table.p || n_table != fb.n || !fb.inf.p)
@@ -1360,15 +1387,33 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   if ((rc = tl.ensure())) return rc;
   const int slot = tl.next;
   const std::string pre = "msm.f" + std::to_string(slot) + ".";
-  DevBuf &keys = ctx->buf("msm.keys"), &vals = ctx->buf("msm.vals"), &keys2 = ctx->buf("msm.keys2"),
-         &vals2 = ctx->buf("msm.vals2");
+  // digits, sort and bucket bounds: on the prep stream q (after the scalars' event; the sort
+  // buffers of prep slot ps) or on s
+  const bool use_prep = sc_ready != nullptr;
+  const int ps = tl.prep_next;
+  const hipStream_t q = use_prep ? tl.prep : s;
+  const std::string sp = use_prep ? "msm.p" + std::to_string(ps) + "." : std::string("msm.");
+  DevBuf &keys = ctx->buf(sp + "keys"), &vals = ctx->buf(sp + "vals"), &keys2 = ctx->buf(sp + "keys2"),
+         &vals2 = ctx->buf(sp + "vals2");
   DevBuf &start = ctx->buf(pre + "start"), &end = ctx->buf(pre + "end"), &buckets = ctx->buf(pre + "buckets"),
          &shares = ctx->buf(pre + "shares"), &parts = ctx->buf(pre + "parts"), &head = ctx->buf(pre + "head"),
          &tail = ctx->buf(pre + "tail"), &spb = ctx->buf(pre + "span"), &hk = ctx->buf(pre + "hkey"),
          &tk = ctx->buf(pre + "tkey");
   DevBuf& braw = ctx->buf("msm.braw");  // read only on s (msm_l29_finish), before the tail forks
-  // a slot's buffers may still be read by its previous tail: reallocation waits for it
-  if (tl.used[slot]) PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
+  if (use_prep) {
+    PBF_HIP(hipStreamWaitEvent(q, sc_ready, 0));
+    if (tl.prep_used[ps]) {
+      PBF_HIP(hipStreamWaitEvent(q, tl.prep_free[ps], 0));  // its last accumulation has read it
+      if (keys2.bytes < m * 4 || ctx->buf(sp + "sort.k").bytes < m * 4)
+        PBF_HIP(hipEventSynchronize(tl.prep_free[ps]));  // reallocation
+    }
+  }
+  // a slot's buffers may still be read by its previous tail: reuse waits for it, reallocation
+  // synchronises
+  if (tl.used[slot]) {
+    PBF_HIP(hipStreamWaitEvent(s, tl.done[slot], 0));
+    if (use_prep) PBF_HIP(hipStreamWaitEvent(q, tl.done[slot], 0));
+  }
   const uint64_t hbytes = (m / MSM_CH + 1) * sizeof(ChunkPart);
   const uint64_t nshare = (1ull << g.hb) + (1ull << g.lb);
   if ((head.bytes < hbytes || tail.bytes < hbytes || start.bytes < (uint64_t)NB * 4 || hk.bytes < m / MSM_CH * 4 + 8 ||
@@ -1382,39 +1427,44 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
       (rc = spb.ensure(4)) || (rc = hk.ensure(m / MSM_CH * 4 + 8)) || (rc = tk.ensure(m / MSM_CH * 4 + 8)))
     return rc;
   const uint8_t* inf = (const uint8_t*)fb.inf.p;
-  // ---- digits, sort by bucket, bucket bounds
+  // ---- digits, sort by bucket, bucket bounds (on q)
   if ((uint64_t)g.nw * n_table >= MSM_NEG) return fail(PBF_EINVAL, "fixed-base MSM: table too large");
   if (msm_fused_sort() && rs_dig_ok(n)) {
     // keys holds the digit codes (2 B per entry at c = 16, else 4 B); for a 3-pass sort keys
     // and vals then take the middle pass (the codes are read by then)
     if (g.c == 16) {
-      hipLaunchKernelGGL((msm_fx_digits_code<uint16_t, 16>), dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n,
+      hipLaunchKernelGGL((msm_fx_digits_code<uint16_t, 16>), dim3(grid1(n)), dim3(256), 0, q, d_sc, inf, first, n,
                          (uint16_t*)keys.p, g.c, g.nw);
       const RsDigits dg{(const uint16_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, NB, MSM_NEG};
       rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, (uint32_t*)keys.p, (uint32_t*)vals.p, m,
-                           g.c, s);
+                           g.c, q, sp);
     } else {
       auto* dk = g.c == 18 ? msm_fx_digits_code<uint32_t, 18>
                  : g.c == 20 ? msm_fx_digits_code<uint32_t, 20>
                              : msm_fx_digits_code<uint32_t, 22>;
-      hipLaunchKernelGGL(dk, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, first, n, (uint32_t*)keys.p, g.c, g.nw);
+      hipLaunchKernelGGL(dk, dim3(grid1(n)), dim3(256), 0, q, d_sc, inf, first, n, (uint32_t*)keys.p, g.c, g.nw);
       const RsDigitsT<uint32_t> dg{(const uint32_t*)keys.p, (uint32_t)n, (uint32_t)n_table, (uint32_t)first, 0, NB,
                                    MSM_NEG};
       rc = msm_sort_digits(ctx, dg, (uint32_t*)keys2.p, (uint32_t*)vals2.p, (uint32_t*)keys.p, (uint32_t*)vals.p, m,
-                           g.c, s);
+                           g.c, q, sp);
     }
     if (rc) return rc;
   } else {
-    hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, s, d_sc, inf, n_table, first, n,
+    hipLaunchKernelGGL(msm_fx_digits, dim3(grid1(n)), dim3(256), 0, q, d_sc, inf, n_table, first, n,
                        (uint32_t*)keys.p, (uint32_t*)vals.p, g.c, g.nw);
     if ((rc = msm_sort_pairs(ctx, (const uint32_t*)keys.p, (const uint32_t*)vals.p, (uint32_t*)keys2.p,
-                             (uint32_t*)vals2.p, m, g.c, s)))
+                             (uint32_t*)vals2.p, m, g.c, q, sp)))
       return rc;
   }
-  hipLaunchKernelGGL(msm_fx_clear, dim3(NB / 256), dim3(256), 0, s, (uint32_t*)start.p, (uint32_t*)end.p,
+  hipLaunchKernelGGL(msm_fx_clear, dim3(NB / 256), dim3(256), 0, q, (uint32_t*)start.p, (uint32_t*)end.p,
                      (uint32_t*)spb.p);
-  hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)keys2.p, m,
+  hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, q, (const uint32_t*)keys2.p, m,
                      (uint32_t*)start.p, (uint32_t*)end.p, NB);
+  if (use_prep) {
+    PBF_HIP(hipGetLastError());
+    PBF_HIP(hipEventRecord(tl.prep_done[ps], q));
+    PBF_HIP(hipStreamWaitEvent(s, tl.prep_done[ps], 0));
+  }
   // ---- accumulation
   // no bucket memset: msm_fx_cd reads only the buckets the accumulation wrote (fx_bucket)
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
@@ -1437,6 +1487,11 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   hipLaunchKernelGGL(msm_max_span, dim3(NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
                      (const uint32_t*)end.p, NB, (uint32_t*)spb.p);
   PBF_HIP(hipGetLastError());
+  if (use_prep) {  // prep slot ps is free once the accumulation has read keys2 / vals2
+    PBF_HIP(hipEventRecord(tl.prep_free[ps], s));
+    tl.prep_used[ps] = true;
+    tl.prep_next = (ps + 1) % MSM_PREP_SLOTS;
+  }
   // ---- the tail, on the side stream
   hipStream_t a = tl.aux;
   PBF_HIP(hipEventRecord(tl.ready[slot], s));

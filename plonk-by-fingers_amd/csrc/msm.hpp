@@ -14,8 +14,15 @@ int msm_fixed_lookup(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_
 // sum_{i<n} scalars[i] * P_(first+i) against a table of n_table points; the XYZZ result
 // (Montgomery) is written to *d_result by the context's side stream (see msm_fixed_wait);
 // nothing on the host waits for it.
+// sc_ready (msm_scalars_ready): the scalars were complete when it was recorded on s, so the
+// digits, the sort and the bucket bounds may run on the context's prep stream, overlapping the
+// accumulation of an MSM enqueued before this one (null: everything on s).
 int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64_t first, const uint64_t* d_sc,
-                     uint64_t n, hipStream_t s, Xyzz* d_result);
+                     uint64_t n, hipStream_t s, Xyzz* d_result, hipEvent_t sc_ready = nullptr);
+// Records on s the point at which the scalars of the next MSMs are complete; returns the event
+// for msm_fixed_device, or null when the prep stream is off (the default; PBF_MSM_PREP=1 turns
+// it on: measured no faster, msm.hip).
+hipEvent_t msm_scalars_ready(pbf_ctx* ctx, hipStream_t s);
 // Orders stream s after every fixed-base MSM tail enqueued on this context so far (call
 // before reading a d_result of msm_fixed_device on s).
 int msm_fixed_wait(pbf_ctx* ctx, hipStream_t s);

@@ -849,8 +849,10 @@ struct Prover {
   const Affine* srs_tbl = nullptr;
   uint64_t srs_n = 0;
   Xyzz* slots = nullptr;  // 9 (this rank's partial sums when sharded)
-  int commit(const uint64_t* coeff, uint64_t len, int slot) {
-    return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot);
+  // ready: msm_scalars_ready recorded after every polynomial of this round's commitments was
+  // complete, so each MSM's digits and sort overlap the previous MSM's accumulation (msm.hpp)
+  int commit(const uint64_t* coeff, uint64_t len, int slot, hipEvent_t ready = nullptr) {
+    return msm_fixed_device(ctx, srs_tbl, srs_n, 0, coeff, len, s, slots + slot, ready);
   }
   // Horner from the top coefficient over p of L >= 2 coefficients (k_hs1..3): q = the quotient
   // of (p - y) / (x - z) (L - 1 coefficients), *rem = p(z) - y
@@ -1627,8 +1629,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   }
   PBF_HIP(hipGetLastError());
   uint64_t pts[9][8];
-  for (int k = 0; k < 3; ++k)
-    if ((rc = P.commit(C(k), n + 2, k))) return rc;
+  {
+    hipEvent_t ready = msm_scalars_ready(ctx, s);
+    for (int k = 0; k < 3; ++k)
+      if ((rc = P.commit(C(k), n + 2, k, ready))) return rc;
+  }
   P.mark("round 1 commits (3 MSM)");
 
   // ---- round 2: accumulator (plonk.rs:278-313)
@@ -1748,10 +1753,13 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)")))
     return rc;
-  if ((rc = P.commit(tq, m, 4))) return rc;            // t_lo
-  P.mark("round 3 quotient + INTT");
-  if ((rc = P.commit(tq + 4 * m, m, 5))) return rc;    // t_mid
-  if ((rc = P.commit(tq + 8 * m, m, 6))) return rc;    // t_hi
+  {
+    hipEvent_t ready = msm_scalars_ready(ctx, s);
+    if ((rc = P.commit(tq, m, 4, ready))) return rc;            // t_lo
+    P.mark("round 3 quotient + INTT");
+    if ((rc = P.commit(tq + 4 * m, m, 5, ready))) return rc;    // t_mid
+    if ((rc = P.commit(tq + 8 * m, m, 6, ready))) return rc;    // t_hi
+  }
   P.mark("round 3 commits (3 MSM)");
 
   // ---- round 4: evaluations at z (plonk.rs:393-399), linearisation r(x) (:401-422)
@@ -1873,10 +1881,13 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   const uint64_t lnum = rlen > m ? rlen : m;  // numerator coefficients (t parts m, r rlen, a/b/c n+2)
   const uint64_t wlen = lnum - 1;             // = max(rlen - 1, m)
   if ((rc = P.synth_div(W2, lnum, zc, u256_zero(), W1, "W_z division left a remainder (plonk.rs:438)"))) return rc;
-  if ((rc = P.commit(W1, wlen, 7))) return rc;
   uint64_t* W3 = W0;  // W1 still feeds the W_z commitment's MSM
   if ((rc = P.synth_div(zx, n + 3, zw, zw_z, W3, "W_zw division left a remainder (plonk.rs:442)"))) return rc;
-  if ((rc = P.commit(W3, n + 2, 8))) return rc;
+  {
+    hipEvent_t ready = msm_scalars_ready(ctx, s);
+    if ((rc = P.commit(W1, wlen, 7, ready))) return rc;
+    if ((rc = P.commit(W3, n + 2, 8, ready))) return rc;
+  }
   if ((rc = P.finish_commits(9, pts))) return rc;
   P.mark("round 5 openings + 2 MSM");
 

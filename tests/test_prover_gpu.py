@@ -221,3 +221,22 @@ def test_shared_snapshots_across_caches(ctx):
     assert ctx.plonk_prove_bn254(*A, chal, rnd, srs1, mode=1) == pa1
     msm()
     assert ctx.plonk_prove_bn254(*Bc, chal, rnd, srs2, mode=1) == pb2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_msm_prep_stream_same_proof(ctx, monkeypatch, mode):
+    """The opt-in MSM prep stream (PBF_MSM_PREP=1: each round's commitments sort on a second
+    stream while the previous one accumulates, csrc/msm.hip msm_scalars_ready) gives the same
+    proof as the one-stream schedule, over two proofs (the prep buffers and their events are
+    reused by the second)."""
+    n = 1 << 12
+    rng = random.Random(4242 + mode)
+    q, cp, abc = P.mul_gates_circuit(n, 0x5EED0042)
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    srs = ctx.srs_create(rng.randrange(1, P.R), 2 * n + 2)
+    monkeypatch.setenv("PBF_MSM_PREP", "0")
+    ref = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=mode)
+    monkeypatch.setenv("PBF_MSM_PREP", "1")
+    for _ in range(2):
+        assert ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=mode) == ref
