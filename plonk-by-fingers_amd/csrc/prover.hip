@@ -85,8 +85,19 @@ __device__ __forceinline__ U256 pow64(U256 b) {
 // a Montgomery-form power is the canonical product (a * xR * R^-1): no conversions.
 // c0 (Montgomery form, used when has_c0): an extra constant factor of every output -- the
 // quotient's circuit slots come out at a chosen R-degree this way, for free (see QuotArgs)
+// Round 4: a thread's first power c0 base^(e_off + e_mult i0), i0 = 64 PV_CHUNK v + l (wave v,
+// lane l), comes from host-computed tables instead of two square-and-multiply chains per thread
+// (~80 dependent products, which were most of the kernel's time at 2^20 gates): x0 = c0
+// base^e_off, tl[l] = base^(e_mult l), tv[k] = base^(e_mult 64 PV_CHUNK 2^k) for the set bits k
+// of v, step = base^(64 e_mult).
+constexpr int SP_WBITS = 27;  // waves < 2^27
+struct ScalePow {
+  U256 x0, step;
+  U256 tl[64];
+  U256 tv[SP_WBITS];
+};
 __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out,
-                            uint64_t count, U256 base, uint64_t e_off, uint64_t e_mult, U256 c0, uint32_t has_c0) {
+                            uint64_t count, ScalePow sp) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
@@ -95,9 +106,10 @@ __global__ void k_scale_pow(const uint64_t* in, uint64_t in_off, uint64_t in_str
       for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
     return;
   }
-  U256 x = fr_pow(base, e_off + e_mult * i0);
-  if (has_c0) x = Fr::mul_tp(x, c0);
-  const U256 step = fr_pow(base, 64 * e_mult);
+  U256 x = Fr::mul_tp(sp.x0, sp.tl[t % 64]);
+  for (uint64_t v = t / 64, k = 0; v; v >>= 1, ++k)
+    if (v & 1) x = Fr::mul_tp(x, sp.tv[k]);
+  const U256 step = sp.step;
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     const uint64_t j = in_off + in_stride * i;
     if (j < len) u256_to_u64(Fr::mul_tp(u256_from_u64(in + 4 * j), x), out + 4 * i);
@@ -806,8 +818,23 @@ struct Prover {
     // outputs at R-degree deg: the constant R^deg in Montgomery form is R^(deg + 1)
     U256 c0 = Fr::one_plain();
     for (int d = 0; d <= deg; ++d) c0 = Fr::to_mont(c0);
+    // the start-power tables (k_scale_pow), Montgomery products on the host
+    auto hpow = [](U256 a, uint64_t e) {
+      U256 r = fr_one_m();
+      for (; e; e >>= 1, a = Fr::mul(a, a))
+        if (e & 1) r = Fr::mul(r, a);
+      return r;
+    };
+    ScalePow sp;
+    sp.x0 = Fr::mul(deg != 0 ? c0 : fr_one_m(), hpow(base, e_off));
+    sp.step = hpow(base, 64 * e_mult);
+    const U256 bm = hpow(base, e_mult);
+    sp.tl[0] = fr_one_m();
+    for (int l = 1; l < 64; ++l) sp.tl[l] = Fr::mul(sp.tl[l - 1], bm);
+    sp.tv[0] = hpow(sp.step, PV_CHUNK);
+    for (int k = 1; k < SP_WBITS; ++k) sp.tv[k] = Fr::mul(sp.tv[k - 1], sp.tv[k - 1]);
     hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
-                       in_stride, len, out, cnt, base, e_off, e_mult, c0, (uint32_t)(deg != 0));
+                       in_stride, len, out, cnt, sp);
   }
   // k coset NTTs of size N: slot i = evaluations of sum_j srcs[i][j] (bases[i] x)^j at g w_N^e
   // (this rank's blocks when sharded), slots count() apart in `out`, at R-degree degs[i]
