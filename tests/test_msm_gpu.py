@@ -345,3 +345,28 @@ def test_sort_digit_widths_knob(ctx, monkeypatch):
     monkeypatch.setenv("PBF_MSM_SORT_W8", "1")
     assert ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n) == a
     assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n, ds.data_ptr(), n) == a
+
+
+@pytest.mark.parametrize("c", [16, 22])
+def test_fixed_base_heavy_buckets(ctx, monkeypatch, c):
+    """Skewed digit distributions through the fixed-base joins: 2^18 equal scalars (every
+    window's n entries in ONE bucket: spans of ~6100 chunks, past the per-chunk steps' 4096, so
+    msm_join_rest_g finishes them) and 2^18 small scalars (< 2^40: two or three nonzero windows,
+    a few thousand heavy buckets). Compared with the windowed MSM; P_i = t_i G random."""
+    import torch
+
+    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    m = 1 << 18
+    t = bn254.random_limbs(m, 700 + c)
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(dt.data_ptr(), pts.data_ptr(), m)
+    rng = np.random.default_rng(c)
+    eq = np.tile(bn254.random_limbs(1, 800 + c).reshape(1, 4), (m, 1))
+    small = np.zeros((m, 4), dtype=np.uint64)
+    small[:, 0] = rng.integers(0, 1 << 40, size=m, dtype=np.uint64)
+    for sc in (eq, small):
+        ds = torch.from_numpy(np.ascontiguousarray(sc).reshape(-1).view(np.int64)).cuda()
+        want = ctx.msm_g1_dev(pts.data_ptr(), ds.data_ptr(), m)
+        assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want, c
+    ctx.release_caches()
