@@ -770,6 +770,11 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
     if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
     if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
+    // the regrouped 2^24 plan takes the XCD-blocked order in every pass (round 4: 2 x 2^24
+    // 0.433-0.437 ms against 0.447-0.453 k-major, 0.462-0.466 linear, five alternations on one
+    // box, profiles/r04/ntt_order24_ab.log); the 2-pass plans keep k-major (2^20 x 32: 0.352-0.355
+    // k-major against 0.362-0.364, profiles/r04/ntt_order_ab.log)
+    if (rg && tiles % 8 == 0) a.xcd_kmajor = 2;
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
