@@ -767,6 +767,10 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
       if (i == 0) a.post_tw = (const uint64_t*)p.twpass[1]->p;
       else a.skip_pass_tw = 1;
     }
+    // the first pass of a 2-pass plan reads the second pass's twiddle table by column too
+    // (post_tw): k-major keeps its rows in the XCD's L2 across the polynomials of a block
+    // (round 4: 2^20 x 32 0.354-0.357 ms against 0.368-0.371 linear, profiles/r04/ntt_orders_sweep.log)
+    if (a.post_tw && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) a.xcd_kmajor = 1;
     if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
     if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
     if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
@@ -778,6 +782,12 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
+    }
+    if (const char* o = getenv("PBF_NTT_ORDERS")) {  // A/B: one digit per pass, e.g. "021"
+      if (strlen(o) > i && o[i] >= '0' && o[i] <= '2') {
+        const uint32_t ord = (uint32_t)(o[i] - '0');
+        a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
+      }
     }
     const uint32_t grid = persist ? persistent_grid((const void*)fn, tile / 16, tiles) : (uint32_t)tiles;
     // A/B diagnostic: extra dynamic LDS per workgroup (PBF_NTT_LDSPAD bytes) lowers the
