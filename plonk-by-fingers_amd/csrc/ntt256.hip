@@ -240,6 +240,19 @@ __global__ void __launch_bounds__(256) ntt256_small_kernel(const U256* in, U256*
   }
 }
 
+// Plan-time fill of a per-pass twiddle table T[r][k] = w^(r k n / (Ns R)), r < R, k < Ns, from
+// the two-level tables: the values the pass kernel's two-level branch computes per element
+// (one Fr product each) computed once instead.
+__global__ void tw256_fill_kernel(U256* t, const U256* tw0, const U256* tw1, uint32_t log_n, uint32_t log_ns,
+                                  uint32_t logr, uint32_t tw_bits) {
+  const uint64_t count = 1ull << (log_ns + logr), n = 1ull << log_n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = i >> log_ns, k = i & ((1ull << log_ns) - 1);
+    const uint64_t x = ((r * k) << (log_n - log_ns - logr)) & (n - 1);
+    t[i] = Fr::mul(tw0[x & ((1ull << tw_bits) - 1)], tw1[x >> tw_bits]);
+  }
+}
+
 __global__ void pointwise_mul256_kernel(const U256* a, const U256* b, U256* c, uint64_t count) {
   // inputs canonical; mont(a)*b = a*b*R*R^-1 = a*b canonical in one product
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
@@ -282,7 +295,8 @@ struct Plan256 {
   std::vector<int> logr;
   uint32_t tw_bits = 0;
   U256 n_inv{};
-  DevBuf small_tw, tw0, tw1;
+  bool fold_scale = false;  // inverse: n^-1 folded into the last pass's twiddles (tw1s / its table)
+  DevBuf small_tw, tw0, tw1, tw1s;
   std::vector<std::shared_ptr<DevBuf>> rtab, twpass;
 };
 
@@ -328,30 +342,53 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
   p->tw_bits = (log_n + 1) / 2;
   int rc = up256(p->tw0, h_powers(wm, 1ull << p->tw_bits));
   if (rc) return rc;
+  // The inverse's n^-1 rides in its last pass's twiddles (every element of a pass with Ns > 1
+  // takes one twiddle product, and the pass is linear): tw1s = tw1 n^-1 for the two-level form,
+  // the per-pass table scaled likewise; PBF_NTT256_SCALE_PASS=1 keeps the separate product (A/B).
+  p->fold_scale = inverse && !getenv("PBF_NTT256_SCALE_PASS");
   {
     const U256 step = h_pow(wm, 1ull << p->tw_bits);
-    rc = up256(p->tw1, h_powers(step, n >> p->tw_bits));
+    std::vector<U256> t1 = h_powers(step, n >> p->tw_bits);
+    rc = up256(p->tw1, t1);
     if (rc) return rc;
+    if (p->fold_scale) {
+      for (auto& x : t1) x = Fr::mul(x, p->n_inv);
+      if ((rc = up256(p->tw1s, t1))) return rc;
+    }
   }
+  // per-pass tables up to 2^tw_log entries (32 B each); larger passes fall back to the two-level
+  // tables (one extra Fr product per element). Tables past 2^20 entries are filled on the device.
+  int tw_log = 26;
+  if (const char* e = getenv("PBF_NTT256_TWLOG")) tw_log = atoi(e);
   uint64_t ns = 1;
-  for (int lr : p->logr) {
+  uint32_t log_ns = 0;
+  for (size_t pi = 0; pi < p->logr.size(); ++pi) {
+    const int lr = p->logr[pi];
     const uint64_t R = 1ull << lr;
+    const bool fold = p->fold_scale && pi + 1 == p->logr.size();
     auto rb = std::make_shared<DevBuf>();
     if ((rc = up256(*rb, h_powers(h_pow(wm, n / R), R)))) return rc;
     p->rtab.push_back(rb);
     auto tb = std::make_shared<DevBuf>();
-    if (ns > 1 && R * ns <= (1ull << 20)) {
+    if (ns > 1 && R * ns > (1ull << 20) && tw_log > 20 && R * ns <= (1ull << tw_log)) {
+      if ((rc = tb->ensure(R * ns * sizeof(U256)))) return rc;
+      hipLaunchKernelGGL(tw256_fill_kernel, dim3(2048), dim3(256), 0, 0, (U256*)tb->p, (const U256*)p->tw0.p,
+                         (const U256*)(fold ? p->tw1s.p : p->tw1.p), log_n, log_ns, (uint32_t)lr, p->tw_bits);
+      PBF_HIP(hipGetLastError());
+      PBF_HIP(hipStreamSynchronize(0));
+    } else if (ns > 1 && R * ns <= (1ull << 20)) {
       const uint64_t step = n / (ns * R);
       std::vector<U256> t(R * ns);
       for (uint64_t r = 0; r < R; ++r) {
         const U256 wr = h_pow(wm, step * r);
         U256 z = one_m;
-        for (uint64_t k = 0; k < ns; ++k) { t[r * ns + k] = z; z = Fr::mul(z, wr); }
+        for (uint64_t k = 0; k < ns; ++k) { t[r * ns + k] = fold ? Fr::mul(z, p->n_inv) : z; z = Fr::mul(z, wr); }
       }
       if ((rc = up256(*tb, t))) return rc;
     }
     p->twpass.push_back(tb);
     ns *= R;
+    log_ns += lr;
   }
   return 0;
 }
@@ -414,7 +451,8 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
     const bool conv = getenv("PBF_NTT256_CONV") != nullptr;
     a.conv_in = conv && i == 0;
     a.conv_out = conv && i == P - 1;
-    a.scale = (p.inverse && i == P - 1);
+    a.scale = (p.inverse && i == P - 1 && !p.fold_scale);
+    if (p.fold_scale && i == P - 1) a.tw1 = (const U256*)p.tw1s.p;
     Pass256Fn fn = pass256_fn(lr);
     if (!fn) return fail(PBF_EINVAL, "no 256-bit kernel for this radix");
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
