@@ -253,6 +253,13 @@ __global__ void tw256_fill_kernel(U256* t, const U256* tw0, const U256* tw1, uin
   }
 }
 
+// c = a b / R for canonical a, b (one Montgomery product); the inverse transform that follows
+// (a get_plan256(..., extra_r) plan) puts the R back
+__global__ void pointwise_mont256_kernel(const U256* a, const U256* b, U256* c, uint64_t count) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+    c[i] = Fr::mul_tp(a[i], b[i]);
+}
+
 __global__ void pointwise_mul256_kernel(const U256* a, const U256* b, U256* c, uint64_t count) {
   // inputs canonical; mont(a)*b = a*b*R*R^-1 = a*b canonical in one product
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
@@ -333,6 +340,7 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
     nm = Fr::to_mont(nn);
   }
   p->n_inv = h_inv(nm);
+  if (inverse == 2) p->n_inv = Fr::mul(p->n_inv, Fr::to_mont(Fr::to_mont(Fr::one_plain())));  // n^-1 R
   if (inverse) wm = h_inv(wm);
   if (n <= 2048) return up256(p->small_tw, h_powers(wm, n));
   // passes of radix <= 2^9 (LDS tile 2048 x 32 B)
@@ -590,14 +598,17 @@ std::mutex& plans256_mu() {
   static std::mutex m;
   return m;
 }
-int get_plan256(pbf_ctx* ctx, const uint64_t* omega, uint64_t n, int inverse, Plan256** out) {
-  Key256 k{ctx, {omega[0], omega[1], omega[2], omega[3]}, n, inverse ? 1 : 0};
+// extra_r (inverse only): the plan's scale is n^-1 R, for inputs that came out of one Montgomery
+// product too few (pointwise_mont256_kernel): the R rides in the last pass's twiddles for free
+int get_plan256(pbf_ctx* ctx, const uint64_t* omega, uint64_t n, int inverse, Plan256** out, bool extra_r = false) {
+  const int kind = inverse ? (extra_r ? 2 : 1) : 0;
+  Key256 k{ctx, {omega[0], omega[1], omega[2], omega[3]}, n, kind};
   std::lock_guard<std::mutex> g(plans256_mu());
   auto it = plans256().find(k);
   if (it != plans256().end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<Plan256> p(new Plan256());
   PBF_HIP(hipSetDevice(ctx->device));
-  int rc = make_plan256(omega, n, inverse ? 1 : 0, p.get());
+  int rc = make_plan256(omega, n, kind, p.get());
   if (rc) return rc;
   *out = p.get();
   plans256()[k] = std::move(p);
@@ -644,8 +655,9 @@ int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, si
   if (!ctx || !omega || !out || (!a && la) || (!b && lb)) return fail(PBF_EINVAL, "null argument");
   const size_t n = la + lb;
   Plan256 *fw, *iv;
+  const bool mont = !getenv("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
   int rc = get_plan256(ctx, omega, n, 0, &fw);
-  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv);
+  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv, mont);
   if (rc) return rc;
   if (!canonical_vec(a, la) || !canonical_vec(b, lb)) return fail(PBF_EINVAL, "input not canonical");
   hipStream_t s = ctx->host_stream();
@@ -657,7 +669,8 @@ int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, si
   if ((rc = run256(*fw, d, d, 2, ctx->scratch0, ctx->scratch1, s))) return rc;
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s, d, d + n, d, (uint64_t)n);
+  hipLaunchKernelGGL(mont ? pointwise_mont256_kernel : pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s, d, d + n,
+                     d, (uint64_t)n);
   PBF_HIP(hipGetLastError());
   if ((rc = run256(*iv, d, d, 1, ctx->scratch0, ctx->scratch1, s))) return rc;
   PBF_HIP(hipMemcpyAsync(out, d, n * 32, hipMemcpyDeviceToHost, s));
@@ -671,8 +684,9 @@ int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d
                           uint64_t* d_out, size_t n, size_t batch, void* stream) {
   if (!ctx || !omega || !d_a || !d_b || !d_out) return fail(PBF_EINVAL, "null argument");
   Plan256 *fw, *iv;
+  const bool mont = !getenv("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
   int rc = get_plan256(ctx, omega, n, 0, &fw);
-  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv);
+  if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv, mont);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   if ((rc = ctx->io2.ensure(batch * n * 32))) return rc;
@@ -681,8 +695,8 @@ int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d
   if ((rc = run256(*fw, (const U256*)d_b, fb, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
   uint64_t blocks = (batch * n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s, (const U256*)d_out, fb, (U256*)d_out,
-                     (uint64_t)(batch * n));
+  hipLaunchKernelGGL(mont ? pointwise_mont256_kernel : pointwise_mul256_kernel, dim3(blocks), dim3(256), 0, s,
+                     (const U256*)d_out, fb, (U256*)d_out, (uint64_t)(batch * n));
   PBF_HIP(hipGetLastError());
   return run256(*iv, (const U256*)d_out, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s);
 }
