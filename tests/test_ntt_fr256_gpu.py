@@ -106,6 +106,49 @@ def test_mul_ntt_config3_size_evaluation_identity(ctx):
     assert torch.equal(dd, dc)
 
 
+@pytest.mark.parametrize("logn", [21, 22])
+def test_twiddle_table_forms_agree(monkeypatch, logn):
+    """The last pass's twiddles three ways: a per-pass table filled on the device (default, past
+    2^20 entries), the two-level tables (PBF_NTT256_TWLOG=20), and with the inverse's n^-1 as a
+    separate product (PBF_NTT256_SCALE_PASS=1) instead of folded into those twiddles: identical
+    forward and inverse outputs, and the round trip restores the input. mul_ntt likewise with its
+    one-product pointwise against the two-product form (PBF_MUL_NTT_TWO_PRODUCTS)."""
+    import torch
+
+    n = 1 << logn
+    w = bn254.root_of_unity(n)
+    x = torch.from_numpy(bn254.random_limbs(n, 40 + logn).view(np.int64)).cuda()
+    y = torch.from_numpy(bn254.random_limbs(n, 50 + logn).view(np.int64)).cuda()
+    half = torch.zeros_like(x)
+    half[: n * 2] = x[: n * 2]  # n/2 coefficients, zero-padded: a mul_ntt operand
+    outs = []
+    for env in ({}, {"PBF_NTT256_TWLOG": "20"}, {"PBF_NTT256_SCALE_PASS": "1"},
+                {"PBF_MUL_NTT_TWO_PRODUCTS": "1"}):
+        for k in ("PBF_NTT256_TWLOG", "PBF_NTT256_SCALE_PASS", "PBF_MUL_NTT_TWO_PRODUCTS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = pbf.Context(0)  # plans are cached per context: a fresh one per setting
+        try:
+            f = torch.empty_like(x)
+            c.ntt_fr_batch_dev(w, x.data_ptr(), f.data_ptr(), n, 1)
+            i = torch.empty_like(x)
+            c.ntt_fr_batch_dev(w, f.data_ptr(), i.data_ptr(), n, 1, inverse=True)
+            hy = torch.zeros_like(y)
+            hy[: n * 2] = y[: n * 2]
+            m = torch.empty_like(x)
+            c.mul_ntt_fr_dev(w, half.data_ptr(), hy.data_ptr(), m.data_ptr(), n, 1,
+                             stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(i, x)
+            outs.append((f, m))
+        finally:
+            c.close()
+    for f, m in outs[1:]:
+        assert torch.equal(f, outs[0][0])
+        assert torch.equal(m, outs[0][1])
+
+
 def test_fr_errors(ctx):
     with pytest.raises(pbf.PbfError):
         ctx.ntt_fr(bn254.root_of_unity(16), [1] * 8)  # omega order 16 != 8
