@@ -28,6 +28,7 @@ struct Pass256 {
   const U256* twpass;  // [r][k] pass twiddles (Montgomery) or null
   const U256* tw0;     // two-level table (Montgomery)
   const U256* tw1;
+  const U256* mul_by;  // last pass (Ns > 1) only, or null: outputs become mont(mul_by[i], y) (mul_ntt)
   U256 n_inv;          // Montgomery form
   uint64_t n;
   uint32_t log_n, log_ns, tw_bits, blocks_per_poly, batch;
@@ -167,7 +168,9 @@ __device__ __forceinline__ void stage256(U256* v, U256* lds, const U256* wq, con
         } else {
           const uint64_t j = j0 + w;
           const uint64_t msk = (1ull << a.log_ns) - 1;
-          out[((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & msk) + ((uint64_t)r << a.log_ns)] = y;
+          const uint64_t o = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & msk) + ((uint64_t)r << a.log_ns);
+          if (a.mul_by) y = PBF_FRMUL(a.mul_by[(out - a.out) + o], y);  // same element: read, then written
+          out[o] = y;
         }
       }
     }
@@ -416,14 +419,18 @@ static Pass256Fn pass256_fn(int logr) {
 }
 static int threads256(int logr) { return ((cols256(logr) << logr) / 4); }
 
+// mul_by (not for n <= 2048): the last pass multiplies its outputs by mul_by's elements (one
+// Montgomery product: mont(m, y) = m y / R) -- mul_ntt's pointwise product fused into the second
+// operand's forward transform
 static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
-                  hipStream_t st) {
+                  hipStream_t st, const U256* mul_by = nullptr) {
   if (batch == 0) return 0;
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * sizeof(U256), hipMemcpyDeviceToDevice, st));
     return 0;
   }
   if (p.logr.empty()) {
+    if (mul_by) return fail(PBF_EINVAL, "fused product needs a multi-pass transform");
     hipLaunchKernelGGL(ntt256_small_kernel, dim3(batch), dim3(256), 0, st, d_in, d_out,
                        (const U256*)p.small_tw.p, p.log_n, p.n_inv, (uint32_t)p.inverse);
     PBF_HIP(hipGetLastError());
@@ -445,6 +452,7 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
     a.twpass = (const U256*)p.twpass[i]->p;
     a.tw0 = (const U256*)p.tw0.p;
     a.tw1 = (const U256*)p.tw1.p;
+    a.mul_by = (i == P - 1) ? mul_by : nullptr;
     a.n_inv = p.n_inv;
     a.n = p.n;
     a.log_n = p.log_n;
@@ -689,6 +697,14 @@ int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d
   if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv, mont);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  // fused (default past 2048 points): b's forward transform multiplies its last pass's outputs by
+  // a's (already in d_out) and stores the product there; PBF_MUL_NTT_NO_FUSE=1: pointwise kernel
+  if (mont && n > 2048 && !getenv("PBF_MUL_NTT_NO_FUSE")) {
+    if ((rc = run256(*fw, (const U256*)d_a, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
+    if ((rc = run256(*fw, (const U256*)d_b, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s, (const U256*)d_out)))
+      return rc;
+    return run256(*iv, (const U256*)d_out, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s);
+  }
   if ((rc = ctx->io2.ensure(batch * n * 32))) return rc;
   U256* fb = (U256*)ctx->io2.p;
   if ((rc = run256(*fw, (const U256*)d_a, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s))) return rc;

@@ -111,8 +111,9 @@ def test_twiddle_table_forms_agree(monkeypatch, logn):
     """The last pass's twiddles three ways: a per-pass table filled on the device (default, past
     2^20 entries), the two-level tables (PBF_NTT256_TWLOG=20), and with the inverse's n^-1 as a
     separate product (PBF_NTT256_SCALE_PASS=1) instead of folded into those twiddles: identical
-    forward and inverse outputs, and the round trip restores the input. mul_ntt likewise with its
-    one-product pointwise against the two-product form (PBF_MUL_NTT_TWO_PRODUCTS)."""
+    forward and inverse outputs, and the round trip restores the input. mul_ntt likewise: its
+    product fused into the second operand's last pass (default), the one-product pointwise kernel
+    (PBF_MUL_NTT_NO_FUSE) and the two-product form (PBF_MUL_NTT_TWO_PRODUCTS)."""
     import torch
 
     n = 1 << logn
@@ -123,8 +124,8 @@ def test_twiddle_table_forms_agree(monkeypatch, logn):
     half[: n * 2] = x[: n * 2]  # n/2 coefficients, zero-padded: a mul_ntt operand
     outs = []
     for env in ({}, {"PBF_NTT256_TWLOG": "20"}, {"PBF_NTT256_SCALE_PASS": "1"},
-                {"PBF_MUL_NTT_TWO_PRODUCTS": "1"}):
-        for k in ("PBF_NTT256_TWLOG", "PBF_NTT256_SCALE_PASS", "PBF_MUL_NTT_TWO_PRODUCTS"):
+                {"PBF_MUL_NTT_TWO_PRODUCTS": "1"}, {"PBF_MUL_NTT_NO_FUSE": "1"}):
+        for k in ("PBF_NTT256_TWLOG", "PBF_NTT256_SCALE_PASS", "PBF_MUL_NTT_TWO_PRODUCTS", "PBF_MUL_NTT_NO_FUSE"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
