@@ -405,11 +405,72 @@ def main() -> int:
                     out["extra"]["cpu_baselines_configs_3_5"] = cpu_baselines_bn254()
                 except Exception as e:  # reported, never fatal to the headline line
                     out["extra"]["cpu_baselines_configs_3_5"] = {"error": repr(e)}
-        print(json.dumps(out), flush=True)
+        if world > 1 and dist is not None:
+            out["config"]["world"] = dist.get_world_size()
+            out["config"]["backend"] = dist.get_backend()
+        # cpu_baseline before extra: the driver reads the line's tail
+        line = {k: v for k, v in out.items() if k != "extra"}
+        if "extra" in out:
+            line["extra"] = out["extra"]
+        print(json.dumps(compact_line(line), separators=(",", ":")), flush=True)
     if dist:
         dist.destroy_process_group()
     ctx.close()
     return 0
+
+
+# keys whose string values are descriptions, moved into extra["notes"] by compact_line
+_NOTE_KEYS = ("sample", "note", "peak_source", "proving_key", "rounds_note", "source", "calibration", "kernel", "unit")
+# the order of `extra` in the printed line: the driver keeps only the tail of stdout, so the
+# north-star and per-config headline entries come last
+_EXTRA_ORDER = ("notes", "cpu_baselines_configs_3_5", "config1_plonk_by_hand", "config5_prove_2p20_mode0",
+                "config5_prove_2p20_4_streams", "config5_prove_2p20", "config4_bn254_msm_2p20", "config4_pairing_check",
+                "config4_pairings_batch", "config4_kzg_commit_2p20", "config3_bn254_polymul_2p22", "ntt_2p24",
+                "config5_prove_2p24", "config5_prove_sharded")
+
+
+def _round_sig(x, sig: int = 4):
+    if isinstance(x, float) and x == x and x not in (float("inf"), float("-inf")) and x != 0.0:
+        from math import floor, log10
+
+        return round(x, sig - 1 - int(floor(log10(abs(x)))))
+    return x
+
+
+def compact_line(out: dict) -> dict:
+    """The printed form of the bench line: floats to 4 significant digits, long descriptive
+    strings of `extra` moved into one `extra.notes` map (keyed entry.path), and `extra`'s
+    entries ordered so the north-star 2^24 NTT, config 3 and the 2^24-gate proof end the line
+    (the driver's record keeps the last few KB of stdout)."""
+    notes = {}
+
+    def walk(v, path, move=True):
+        if isinstance(v, dict):
+            r = {}
+            for k, x in v.items():
+                if move and k in _NOTE_KEYS and isinstance(x, str) and len(x) > 24:
+                    notes[f"{path}.{k}"] = x
+                else:
+                    r[k] = walk(x, f"{path}.{k}", move)
+            return r
+        if isinstance(v, list):
+            return [walk(x, path, move) for x in v]
+        return _round_sig(v)
+
+    top = {k: walk(v, k, move=False) for k, v in out.items() if k != "extra"}
+    if "extra" in out:
+        ex = {k: walk(v, k) for k, v in out["extra"].items()}
+        ordered = {"notes": notes}
+        for k in _EXTRA_ORDER:
+            if k in ex:
+                ordered[k] = ex[k]
+        for k in ex:  # anything not listed goes before the headline entries
+            if k not in ordered:
+                ordered = {**{kk: vv for kk, vv in ordered.items() if kk in ("notes", "cpu_baselines_configs_3_5")},
+                           k: ex[k], **{kk: vv for kk, vv in ordered.items()
+                                        if kk not in ("notes", "cpu_baselines_configs_3_5")}}
+        top["extra"] = ordered
+    return top
 
 
 def _median_ms(fn, reps: int = 20, warmup: int = 2) -> dict:

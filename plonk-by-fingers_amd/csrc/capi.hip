@@ -23,6 +23,7 @@ using namespace pbf;
 void pbf_internal_drop_plans256(const void* ctx);  // ntt256.hip
 void pbf_internal_drop_tl256(const void* ctx);     // ntt256.hip
 void pbf_internal_forget_ctx(const pbf_ctx* ctx);  // group.hip
+void pbf_internal_release_group_bufs(const pbf_ctx* ctx);  // group.hip
 
 int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan** out) {
   auto key = std::make_tuple(m, omega, n, inverse ? 1 : 0);
@@ -104,6 +105,7 @@ int pbf_ctx_release_caches(pbf_ctx* ctx) {
   if (ctx->msm_tail.aux) PBF_HIP(hipStreamSynchronize(ctx->msm_tail.aux));
   if (ctx->msm_tail.prep) PBF_HIP(hipStreamSynchronize(ctx->msm_tail.prep));
   PBF_HIP(hipDeviceSynchronize());  // _dev callers' streams may still read the caches
+  pbf_internal_release_group_bufs(ctx);  // the multi-GPU groups' exchange buffers
   ctx->pk_key.clear();
   ctx->vk_key.clear();
   ctx->vk_pts.clear();

@@ -32,11 +32,13 @@ using namespace pbf;
 // ---- RCCL, resolved at run time (the subset the group uses; types from rccl.h)
 typedef void* nccl_comm_t;
 typedef int nccl_result_t;
-constexpr int NCCL_UINT8 = 1;
+constexpr int NCCL_UINT8 = 1;  // ncclDataType_t: ncclInt8 = 0, ncclUint8 = 1 (stable in the RCCL / NCCL ABI)
 struct Rccl {
+  std::string path;  // "" = the process's / ROCm's librccl; else PBF_RCCL_LIB
   void* h = nullptr;
   nccl_result_t (*comm_init_all)(nccl_comm_t*, int, const int*) = nullptr;
   nccl_result_t (*comm_destroy)(nccl_comm_t) = nullptr;
+  nccl_result_t (*comm_abort)(nccl_comm_t) = nullptr;
   nccl_result_t (*send)(const void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
   nccl_result_t (*recv)(void*, size_t, int, int, nccl_comm_t, hipStream_t) = nullptr;
   nccl_result_t (*all_gather)(const void*, void*, size_t, int, nccl_comm_t, hipStream_t) = nullptr;
@@ -45,26 +47,42 @@ struct Rccl {
   const char* (*err)(nccl_result_t) = nullptr;
   bool load() {
     if (h) return true;
-    // reuse a copy already in the process (torch's), else the ROCm one
-    for (const char* name : {"librccl.so.1", "librccl.so"})
-      if ((h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!path.empty()) {
+      h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    } else {
+      // reuse a copy already in the process (torch's), else the ROCm one
+      for (const char* name : {"librccl.so.1", "librccl.so"})
+        if ((h = dlopen(name, RTLD_NOW | RTLD_NOLOAD))) break;
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!h) return false;
     comm_init_all = (decltype(comm_init_all))dlsym(h, "ncclCommInitAll");
     comm_destroy = (decltype(comm_destroy))dlsym(h, "ncclCommDestroy");
+    comm_abort = (decltype(comm_abort))dlsym(h, "ncclCommAbort");
     send = (decltype(send))dlsym(h, "ncclSend");
     recv = (decltype(recv))dlsym(h, "ncclRecv");
     all_gather = (decltype(all_gather))dlsym(h, "ncclAllGather");
     group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
     group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
     err = (decltype(err))dlsym(h, "ncclGetErrorString");
-    return comm_init_all && comm_destroy && send && recv && all_gather && group_start && group_end && err;
+    return comm_init_all && comm_destroy && comm_abort && send && recv && all_gather && group_start && group_end && err;
   }
 };
-Rccl& rccl() {
-  static Rccl r;
-  return r;
+// one loaded library per path: PBF_RCCL_LIB (read when a group is built) selects a stand-in
+// implementation of the same entry points (tests/native/fake_rccl.cpp: exercises this branch
+// on one device, where RCCL itself refuses two ranks)
+std::mutex g_rccl_mu;
+Rccl* rccl_lib() {
+  static std::vector<std::unique_ptr<Rccl>> libs;
+  const char* e = getenv("PBF_RCCL_LIB");
+  const std::string path = e ? e : "";
+  std::lock_guard<std::mutex> l(g_rccl_mu);
+  for (auto& r : libs)
+    if (r->path == path) return r->load() ? r.get() : nullptr;
+  libs.emplace_back(new Rccl());
+  libs.back()->path = path;
+  return libs.back()->load() ? libs.back().get() : nullptr;
 }
 
 // reusable barrier for the rank threads of one call; abort() releases every waiter with false
@@ -110,6 +128,9 @@ struct Group {
   std::vector<uint64_t> serial;  // the contexts' creation serials (a destroyed context never matches)
   uint32_t G = 0;
   bool same_device = true;
+  bool use_rccl = false;             // distinct devices, or PBF_GROUP_FORCE_RCCL=1 (stand-in tests)
+  std::atomic<bool> broken{false};   // communicators aborted after a failure: dropped by group_for
+  Rccl* R = nullptr;
   std::vector<nccl_comm_t> nccl;
   std::vector<DevBuf> send, recv;   // per rank, on its device
   std::vector<hipEvent_t> ev_ready, ev_done;
@@ -126,8 +147,19 @@ struct Group {
       if (g < send.size()) send[g].release();
       if (g < recv.size()) recv[g].release();
     }
+    if (!broken)  // aborted communicators are already freed
+      for (nccl_comm_t c : nccl)
+        if (c) (void)R->comm_destroy(c);
+  }
+  // a rank failed: release every rank waiting on a host barrier and every collective in flight
+  // (ncclCommAbort unblocks peers whose partner never posts its half); the group is then dropped
+  // by group_for. Ranks check `broken` before posting, so none posts on an aborted communicator
+  // once the flag is seen.
+  void abort_all() {
+    if (bar) bar->abort();
+    if (!use_rccl || broken.exchange(true)) return;
     for (nccl_comm_t c : nccl)
-      if (c) (void)rccl().comm_destroy(c);
+      if (c) (void)R->comm_abort(c);
   }
   std::vector<int> devs;
   int ctx_device(uint32_t g) const { return devs[g]; }
@@ -145,10 +177,17 @@ struct Group {
       std::sort(sorted.begin(), sorted.end());
       if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
         return fail(PBF_EINVAL, "multi-GPU group: contexts must share one device or all be on distinct devices");
-      if (!rccl().load()) return fail(PBF_ECOMM, std::string("multi-GPU group: cannot load librccl: ") + dlerror());
+    }
+    const char* force = getenv("PBF_GROUP_FORCE_RCCL");  // test only: the RCCL branch on one device
+    use_rccl = !same_device || (force && force[0] == '1');
+    if (use_rccl) {
+      if (!(R = rccl_lib())) {
+        const char* e = dlerror();
+        return fail(PBF_ECOMM, std::string("multi-GPU group: cannot load librccl: ") + (e ? e : "missing symbols"));
+      }
       nccl.assign(G, nullptr);
-      const nccl_result_t r = rccl().comm_init_all(nccl.data(), (int)G, devs.data());
-      if (r) return fail(PBF_ECOMM, std::string("ncclCommInitAll: ") + rccl().err(r));
+      const nccl_result_t r = R->comm_init_all(nccl.data(), (int)G, devs.data());
+      if (r) return fail(PBF_ECOMM, std::string("ncclCommInitAll: ") + R->err(r));
     }
     send.resize(G);
     recv.resize(G);
@@ -192,22 +231,30 @@ struct Group {
     for (uint32_t g = 0; g < G; ++g) PBF_HIP(hipStreamWaitEvent(s, ev_done[g], 0));
     return 0;
   }
+  // RCCL: every rank passes a host barrier before it posts, so a rank that failed earlier (an
+  // allocation, a launch, an input check) releases the others instead of leaving their halves
+  // of the exchange without a partner (their stream would never drain)
+  int rccl_ready() {
+    if (!bar->wait() || broken) return fail(PBF_ECOMM, "multi-GPU group: a rank failed");
+    return 0;
+  }
   int all_to_all(uint32_t r, size_t b) {
-    if (same_device) return copy_exchange(r, b, false);
-    Rccl& R = rccl();
-    nccl_result_t e = R.group_start();
+    if (!use_rccl) return copy_exchange(r, b, false);
+    if (int rc = rccl_ready()) return rc;
+    nccl_result_t e = R->group_start();
     for (uint32_t g = 0; g < G && !e; ++g) {
-      if ((e = R.send((const char*)send[r].p + (size_t)g * b, b, NCCL_UINT8, (int)g, nccl[r], stream[r]))) break;
-      e = R.recv((char*)recv[r].p + (size_t)g * b, b, NCCL_UINT8, (int)g, nccl[r], stream[r]);
+      if ((e = R->send((const char*)send[r].p + (size_t)g * b, b, NCCL_UINT8, (int)g, nccl[r], stream[r]))) break;
+      e = R->recv((char*)recv[r].p + (size_t)g * b, b, NCCL_UINT8, (int)g, nccl[r], stream[r]);
     }
-    const nccl_result_t e2 = R.group_end();
-    if (e || e2) return fail(PBF_ECOMM, std::string("RCCL all-to-all: ") + R.err(e ? e : e2));
+    const nccl_result_t e2 = R->group_end();
+    if (e || e2) return fail(PBF_ECOMM, std::string("RCCL all-to-all: ") + R->err(e ? e : e2));
     return 0;
   }
   int all_gather(uint32_t r, size_t b) {
-    if (same_device) return copy_exchange(r, b, true);
-    const nccl_result_t e = rccl().all_gather(send[r].p, recv[r].p, b, NCCL_UINT8, nccl[r], stream[r]);
-    if (e) return fail(PBF_ECOMM, std::string("ncclAllGather: ") + rccl().err(e));
+    if (!use_rccl) return copy_exchange(r, b, true);
+    if (int rc = rccl_ready()) return rc;
+    const nccl_result_t e = R->all_gather(send[r].p, recv[r].p, b, NCCL_UINT8, nccl[r], stream[r]);
+    if (e) return fail(PBF_ECOMM, std::string("ncclAllGather: ") + R->err(e));
     return 0;
   }
   pbf_comm comm(uint32_t r);
@@ -224,7 +271,7 @@ struct Group {
         else rcs[g] = fn(g);
         if (rcs[g]) {
           msgs[g] = pbf_last_error();
-          bar->abort();
+          abort_all();
         }
       });
     for (auto& t : ts) t.join();
@@ -275,6 +322,9 @@ int group_for(pbf_ctx* const* ctxs, uint32_t world, Group** out) {
     for (uint32_t h = g + 1; h < world; ++h)
       if (ctxs[g] == ctxs[h]) return fail(PBF_EINVAL, "a context appears twice (one context per rank)");
   std::lock_guard<std::mutex> l(g_groups_mu);
+  auto& v = groups();  // a group whose communicators were aborted is rebuilt
+  v.erase(std::remove_if(v.begin(), v.end(), [](const std::unique_ptr<Group>& g) { return g->broken.load(); }),
+          v.end());
   for (auto& gp : groups()) {
     if (gp->G != world) continue;
     bool same = true;
@@ -420,7 +470,41 @@ int host_mul_ntt_multi(Group* grp, const NttOps& ops,
   });
 }
 
+// BN254 r (little-endian u64 limbs): Fr inputs are canonical residues, as in the single-GPU calls
+bool fr_canonical(const uint64_t* v, size_t n) {
+  static const uint64_t R[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull,
+                                0x30644e72e131a029ull};
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t* x = v + 4 * i;
+    int k = 3;
+    while (k >= 0 && x[k] == R[k]) --k;
+    if (k < 0 || x[k] > R[k]) return false;
+  }
+  return true;
+}
+// the _dev forms: every rank holds nl elements per polynomial, a power of two >= G (the
+// stride-shard layout and the per-peer blocks of nl / G)
+int check_nl(size_t nl, uint32_t G) {
+  if (nl < G || (nl & (nl - 1)) || nl % G) return fail(PBF_EINVAL, "nl must be a power of two >= world");
+  return 0;
+}
+
 }  // namespace
+
+// pbf_ctx_release_caches: the exchange buffers of every group with this member are freed (the
+// communicators stay; the next call allocates again)
+void pbf_internal_release_group_bufs(const pbf_ctx* c) {
+  std::lock_guard<std::mutex> l(g_groups_mu);
+  for (auto& g : groups()) {
+    if (std::find(g->ctx.begin(), g->ctx.end(), c) == g->ctx.end()) continue;
+    for (uint32_t r = 0; r < g->G; ++r) {
+      (void)hipSetDevice(g->devs[r]);
+      g->send[r].release();
+      g->recv[r].release();
+    }
+    g->capacity = 0;
+  }
+}
 
 void pbf_internal_forget_ctx(const pbf_ctx* c) {
   std::lock_guard<std::mutex> l(g_groups_mu);
@@ -459,6 +543,7 @@ int pbf_ntt_u64_multi_dev(pbf_ctx* const* ctxs, uint32_t world, uint64_t modulus
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
+  if ((rc = check_nl(nl, world))) return rc;
   if ((rc = g->ensure(batch * nl * 8))) return rc;
   const NttOps ops = u64_ops(modulus, omega, world);
   return g->run([&](uint32_t r) {
@@ -473,6 +558,7 @@ int pbf_ntt_fr256_multi(pbf_ctx* const* ctxs, uint32_t world, const uint64_t* om
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
+  if (!fr_canonical(in, n)) return fail(PBF_EINVAL, "input not canonical");
   if (in == out) {
     std::vector<uint64_t> tmp(in, in + 4 * n);
     return host_ntt_multi(g, fr_ops(omega, world), tmp.data(), out, n, inverse);
@@ -486,6 +572,7 @@ int pbf_ntt_fr256_multi_dev(pbf_ctx* const* ctxs, uint32_t world, const uint64_t
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
+  if ((rc = check_nl(nl, world))) return rc;
   if ((rc = g->ensure(batch * nl * 32))) return rc;
   const NttOps ops = fr_ops(omega, world);
   return g->run([&](uint32_t r) {
@@ -500,6 +587,13 @@ int pbf_mul_ntt_u64_multi(pbf_ctx* const* ctxs, uint32_t world, uint64_t modulus
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
+  FieldKind k;
+  FieldArgs fa;
+  if (!field_for(modulus, &k, &fa)) return fail(PBF_EUNSUPPORTED, "unsupported modulus");
+  for (size_t i = 0; i < la; ++i)
+    if (a[i] >= modulus) return fail(PBF_EINVAL, "input not canonical");
+  for (size_t i = 0; i < lb; ++i)
+    if (b[i] >= modulus) return fail(PBF_EINVAL, "input not canonical");
   return host_mul_ntt_multi(
       g, u64_ops(modulus, omega, world),
       [=](pbf_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* z, size_t cnt, hipStream_t s) {
@@ -514,6 +608,7 @@ int pbf_mul_ntt_fr256_multi(pbf_ctx* const* ctxs, uint32_t world, const uint64_t
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
+  if (!fr_canonical(a, la) || !fr_canonical(b, lb)) return fail(PBF_EINVAL, "input not canonical");
   return host_mul_ntt_multi(
       g, fr_ops(omega, world),
       [](pbf_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* z, size_t cnt, hipStream_t s) {
@@ -587,7 +682,7 @@ int pbf_multi_backend(pbf_ctx* const* ctxs, uint32_t world, int* backend) {
   Group* g;
   int rc = group_for(ctxs, world, &g);
   if (rc) return rc;
-  *backend = g->same_device ? 0 : 1;
+  *backend = g->use_rccl ? 1 : 0;
   return 0;
 }
 

@@ -1088,7 +1088,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   pbf_ctx* ctx = P.ctx;
   const hipStream_t s = P.s;
   const uint64_t n = P.n, G = P.G, r = P.rank, Bn = P.B, Sn = Bn / G, NE = P.nl;
-  const uint64_t E = 32, CS = n + 8, CRS = P.CRS(), SSS = P.SSS();
+  const uint64_t E = 32, CRS = P.CRS(), SSS = P.SSS();
   const U256 one = fr_one_m();
   auto C = [&](int k) { return cslot[k]; };
   auto CE = [&](int k) { return ceslot[k]; };
@@ -1549,7 +1549,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     bool same = false;
     if ((rc = snapshot_check(ctx, "pk", items, 2, s, &same))) return rc;
     if (!same) ctx->pk_key.clear();
-    pk_key = {(uint64_t)n, (uint64_t)P.G, (uint64_t)P.rank};
+    // sharded: the key's CR ranges follow Ls (2n in mode 0, n in mode 1), so the layout is part of the key
+    pk_key = {(uint64_t)n, (uint64_t)P.G, (uint64_t)P.rank, P.G > 1 ? P.Ls : 0};
     for (int i = 0; i < 8; ++i) pk_key.push_back(k1k2[i]);
     DevBuf& kc = ctx->buf("pk.coef");
     DevBuf& ks = ctx->buf("pk.coset");

@@ -179,6 +179,27 @@ def test_prove_multi_matches_single(ranks, G, log_n, mode):
         assert np.array_equal(pts, ref[0]) and np.array_equal(fs, ref[1]), (G, log_n, mode)
 
 
+def test_prove_multi_modes_interleaved_on_one_key(ranks):
+    """One circuit proved in mode 1, then mode 0, then mode 1 on the same sharded contexts: the
+    ranks' proving keys are laid out on Ls = n (mode 1) or 2n (mode 0) ranges, so a key built in
+    one mode must not be taken by the other. Each proof equals the single-GPU one."""
+    import pbf
+
+    n, G = 1 << 10, 4
+    single = pbf.Context(0)
+    try:
+        dq, dc, dabc, dsrs, srs_m, chal, rnd = _device_inputs(single, n, 0x5EED7000, 0)  # SRS long enough for mode 0
+        ref = {m: single.plonk_prove_bn254_dev(n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd,
+                                               dsrs.data_ptr(), srs_m, mode=m) for m in (1, 0)}
+    finally:
+        single.close()
+    for m in (1, 0, 1, 0):
+        pts, fs = pbf.plonk_prove_bn254_multi_dev(ranks[:G], n, [dq.data_ptr()] * G, [dc.data_ptr()] * G,
+                                                  [dabc.data_ptr()] * G, chal, rnd, [dsrs.data_ptr()] * G, srs_m,
+                                                  mode=m)
+        assert np.array_equal(pts, ref[m][0]) and np.array_equal(fs, ref[m][1]), m
+
+
 def test_prove_multi_host_inputs_match_oracle(ranks):
     """pbf_plonk_prove_bn254_multi (host inputs) against the literal restatement's committed
     proofs (tests/golden/plonk_bn254.json, oracle/plonk_bn254.py) at their largest n."""
