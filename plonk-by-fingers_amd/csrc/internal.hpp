@@ -99,6 +99,11 @@ struct NttPlan {
   bool rg = false;
   mutable bool rg_built = false;
   mutable DevBuf rg_tc1, rg_t2, rg_t3;
+  // two-pass 4096 x 4096 plan for 2^24-point standard-root transforms (ntt_r4k.hpp; opt-in
+  // PBF_NTT_R4K=1): stage tables of both passes and the inter-pass [j][k] table, built lazily
+  bool r4k = false;
+  mutable bool r4k_built = false;
+  mutable DevBuf r4k_tst1, r4k_tst2, r4k_post;
   bool ip = false;
   std::vector<int> ip_r;
   std::vector<std::shared_ptr<DevBuf>> ip_tw, ip_tc;

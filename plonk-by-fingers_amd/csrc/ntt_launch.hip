@@ -4,6 +4,7 @@
 #include <mutex>
 #include "internal.hpp"
 #include "ntt_gl.hpp"
+#include "ntt_r4k.hpp"
 
 namespace pbf {
 
@@ -325,6 +326,8 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   // regrouped 2^24 plan (default for 8,8,8 standard-root plans; PBF_NTT_NO_RG=1 restores the
   // round-2 passes): three twiddle layers of order 4096, 2^18 and 2^24
   if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && !getenv("PBF_NTT_NO_RG")) p->rg = true;
+  // two-pass 4096 x 4096 plan (ntt_r4k.hpp)
+  if (p->gl && log_n == 24 && getenv("PBF_NTT_R4K")) p->r4k = true;
   // round-3 in-place schedule: opt-in (PBF_NTT_IP=1) while it measures slower than the
   // round-2 Stockham plan
   if (p->gl && getenv("PBF_NTT_IP") && !getenv("PBF_NTT_V2")) {
@@ -696,8 +699,67 @@ static int ensure_rg_tables(const NttPlan& p) {
   return 0;
 }
 
+// The two-pass plan's tables (ntt_r4k.hpp): tst[b][c] = w_4096^(b c) for pass 1, the same times
+// n^-1 for an inverse's pass 2, post[j][k] = w^(j k) (2^24 entries) for pass 1's stores
+static int ensure_r4k_tables(const NttPlan& p) {
+  if (p.r4k_built) return 0;
+  const uint64_t m = p.m;
+  uint64_t w = p.omega;
+  if (p.inverse && !hinv(p.omega, m, &w)) return fail(1, "omega not invertible");
+  const uint64_t w4096 = hpow(w, 4096, m);
+  std::vector<uint64_t> t1(4096), t2(4096);
+  for (uint64_t b = 0; b < 64; ++b)
+    for (uint64_t c = 0; c < 64; ++c) {
+      t1[b * 64 + c] = hpow(w4096, b * c, m);
+      t2[b * 64 + c] = p.inverse ? hmul(t1[b * 64 + c], p.n_inv, m) : t1[b * 64 + c];
+    }
+  std::vector<uint64_t> post(1ull << 24);
+  for (uint64_t j = 0; j < 4096; ++j) {
+    const uint64_t st = hpow(w, j, m);
+    uint64_t y = 1;
+    uint64_t* row = post.data() + (j << 12);
+    for (uint64_t k = 0; k < 4096; ++k) { row[k] = y; y = hmul(y, st, m); }
+  }
+  int rc;
+  if ((rc = upload(p.r4k_tst1, t1)) || (rc = upload(p.r4k_tst2, t2)) || (rc = upload(p.r4k_post, post))) return rc;
+  p.r4k_built = true;
+  return 0;
+}
+
+// ntt_r4k.hip
+int launch_r4k_pass(const R4kArgs& a, bool first, int e64, uint32_t tiles, bool persist, hipStream_t stream);
+
+static int run_r4k(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                   hipStream_t stream, size_t soff) {
+  int rc = ensure_r4k_tables(p);
+  if (rc) return rc;
+  if (batch * 512 > 0x7fffffffull) return fail(1, "batch too large");
+  R4kArgs a;
+  a.batch = (uint32_t)batch;
+  a.kmajor = batch > 1 && !getenv("PBF_NTT_NO_KMAJOR") ? 1 : 0;
+  const uint32_t grid = (uint32_t)(512 * batch);
+  // pass 1: in -> s0 (inter-pass twiddle applied at the stores)
+  a.in = d_in;
+  a.out = (uint64_t*)s0.p + soff;
+  a.tst = (const uint64_t*)p.r4k_tst1.p;
+  a.post = (const uint64_t*)p.r4k_post.p;
+  a.scaled = 0;
+  const char* mode = getenv("PBF_NTT_R4K");
+  const bool persist = mode && mode[0] == '2';
+  if ((rc = launch_r4k_pass(a, true, p.e64, grid, persist, stream))) return rc;
+  // pass 2: s0 -> out (n^-1 in the stage table of an inverse)
+  a.in = (const uint64_t*)s0.p + soff;
+  a.out = d_out;
+  a.tst = (const uint64_t*)p.r4k_tst2.p;
+  a.post = nullptr;
+  a.scaled = p.inverse ? 1 : 0;
+  if ((rc = launch_r4k_pass(a, false, p.e64, grid, persist, stream))) return rc;
+  return 0;
+}
+
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                         DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff) {
+  if (p.r4k && split_log == 0 && gl_pad(p) == 0) return run_r4k(p, d_in, d_out, batch, s0, stream, soff);
   const size_t P = p.logr.size();
   // two-pass plans with equal tile widths may keep the intermediate blocked (ntt_gl.hpp BLK)
   bool blk = false;
@@ -779,6 +841,11 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     // box, profiles/r04/ntt_order24_ab.log); the 2-pass plans keep k-major (2^20 x 32: 0.352-0.355
     // k-major against 0.362-0.364, profiles/r04/ntt_order_ab.log)
     if (rg && tiles % 8 == 0) a.xcd_kmajor = 2;
+    // round 5: the last pass takes XCD k-major instead (both polynomials of a column block on one
+    // XCD, so each slice of its 128 MiB T3 table is read into one L2 once, not once per XCD of
+    // each polynomial): calibrated traffic 1.886 -> 1.753 GB per 2 x 2^24 step, time level
+    // (0.4375-0.4433 against 0.4362-0.4379 ms, profiles/r05/order24.log)
+    if (rg && i == 2 && batch > 1 && tiles % 8 == 0) a.xcd_kmajor = 1;
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
@@ -821,7 +888,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   const size_t P = p.logr.size();
   const size_t bytes = batch * (p.gl ? gl_pitch(p) : p.n) * 8;
   int rc = s0.ensure(bytes);
-  if (!rc && P > 2) rc = s1.ensure(bytes);
+  if (!rc && P > 2 && !(p.r4k && split_log == 0 && gl_pad(p) == 0)) rc = s1.ensure(bytes);
   if (rc) return rc;
   uint32_t log_ns = 0;
   if (p.gl) return run_gl_passes(p, d_in, d_out, batch, s0, s1, stream, split_log, fork);

@@ -166,6 +166,41 @@ def test_regrouped_2p24_matches_stockham(monkeypatch, inverse):
     assert np.array_equal(outs[0][0], oracle.ntt_gl_par(w, host[0], inverse=inverse))
 
 
+@pytest.mark.parametrize("inverse", [False, True])
+@pytest.mark.parametrize("batch", [1, 2])
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_two_pass_r4k_2p24_matches_default(monkeypatch, vectors, inverse, batch, mode):
+    """The two-pass 4096 x 4096 plan (ntt_r4k.hpp, PBF_NTT_R4K=1: 64 x 64 register DFTs in
+    512-thread workgroups, LDS exchange in two rounds; =2: its persistent form with the next
+    tile's even rows LDS-DMA'd during stage II) against the default three-pass plan, forward and
+    inverse, batch 1 (linear tile order) and 2 (XCD k-major), bit-exact; forward against the
+    2^24 golden digest."""
+    import torch
+
+    n = 1 << 24
+    w = root(GOLD, n)
+    host = np.stack([oracle.splitmix_field(GOLD, 950 + i, n) for i in range(batch)])
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for env in ({}, {"PBF_NTT_R4K": mode}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = pbf.Context(0)
+        d_in = torch.from_numpy(host.view(np.int64)).cuda()
+        d_out = torch.empty_like(d_in)
+        c.ntt_batch_dev(GOLD, w, d_in.data_ptr(), d_out.data_ptr(), n, batch, inverse=inverse, stream=stream)
+        torch.cuda.synchronize()
+        outs.append(d_out.cpu().numpy().view(np.uint64).copy())
+        if env and not inverse and batch == 1:
+            cg = vectors["large"][2]
+            a = oracle.splitmix_field(cg["modulus"], cg["seed"], cg["n"])
+            assert sha(c.ntt(cg["modulus"], cg["omega"], a)) == cg["sha256_fwd"]
+        c.close()
+        for k in env:
+            monkeypatch.delenv(k)
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_batch_dev_matches_single(ctx):
     import torch
 
