@@ -552,6 +552,23 @@ ntt_gl_pass_kernel(GlPassArgs a) {
   gl_tile<LOGR, E64, FIRST, TILE, false, BLK, RG>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
 }
 
+// Two groups' passes in one launch (ntt_launch.hip run_gl_dual): `second` is pass 2 of one
+// polynomial group, `first` pass 1 of the next (independent data). Workgroups alternate roles
+// in runs of 8, so each role's tile ids keep their XCD (tile & 7 == blockIdx & 7, as the
+// XCD-aware tile orders assume) and both roles run together on every XCD.
+template <int LOGR, int E64, int TILE>
+__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_gl_dual_kernel(GlPassArgs second, GlPassArgs first) {
+  gl_shape_checks<LOGR, TILE>();
+  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
+  const uint32_t b = blockIdx.x, grp = b >> 3;
+  const uint32_t tile = ((grp >> 1) << 3) | (b & 7);
+  if (grp & 1)
+    gl_tile<LOGR, E64, true, TILE, false>(first, lds, tile, first.blocks_per_poly * first.batch, threadIdx.x, 0);
+  else
+    gl_tile<LOGR, E64, false, TILE, false>(second, lds, tile, second.blocks_per_poly * second.batch, threadIdx.x, 0);
+}
+
 // ---- regrouped 2^24 plan (DESIGN.md §3.1 "Regrouped twiddles") --------------------------
 // The three radix-2^8 passes of a 2^24 transform re-cut so that every general (table)
 // twiddle sits between DFT blocks of 64 points: with the index bits in four groups of six,

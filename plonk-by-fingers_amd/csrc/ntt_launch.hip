@@ -582,9 +582,18 @@ static GlPassFn gl_fn_rg(int pass) {
   return ntt_gl_pass_kernel<8, E, false, 4096, false, 3>;
 }
 
+// one pass launch of a group, recorded instead of launched (the dual-group schedule below)
+struct GlLaunch {
+  GlPassFn fn;
+  uint32_t grid, block;
+  size_t lds;
+  GlPassArgs a;
+};
+
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0,
+                        std::vector<GlLaunch>* rec = nullptr);
 
 // Padded intermediates (PBF_NTT_PAD = elements per row, A/B): the scratch between passes i and
 // i+1 keeps each of its rows (n / R_(i+1) elements: what pass i+1 reads as one row r) `pad`
@@ -626,6 +635,60 @@ ForkSet::~ForkSet() {
   if (fork) (void)hipEventDestroy(fork);
 }
 
+// Dual-group schedule of a two-pass plan (round 5, opt-in PBF_NTT_DUAL=1): ONE stream, launches
+// {pass 1 of group 0}, {pass 2 of group g-1 + pass 1 of group g} (one launch, the two roles
+// interleaved in runs of 8 workgroups so both run at once on every XCD: ntt_gl_dual_kernel),
+// ..., {pass 2 of the last group}. Two groups' passes overlap as with the two-stream schedule,
+// without its per-call fork and join (cross-queue event waits, ~20 us of idle GPU per call at
+// 2^20 x 32: profiles/r04/ntt_2p20_timeline.txt). Measured slower (2^20 x 32: 0.411 against
+// 0.357 ms, profiles/r05/dual_ab.log): each launch ends in a tail of its last workgroups that the
+// two-stream schedule fills with the other stream's kernel. Returns -1 when the plan has no
+// dual-group kernel (the caller falls back to the stream schedule).
+typedef void (*GlDualFn)(GlPassArgs, GlPassArgs);
+template <int E>
+static GlDualFn gl_fn_dual(int logr, int tile) {
+  if (logr == 10 && tile == 8192) return ntt_gl_dual_kernel<10, E, 8192>;
+  if (logr == 9 && tile == 4096) return ntt_gl_dual_kernel<9, E, 4096>;
+  if (logr == 8 && tile == 4096) return ntt_gl_dual_kernel<8, E, 4096>;
+  return nullptr;
+}
+
+static int run_gl_dual(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, size_t G, DevBuf& s0,
+                       DevBuf& s1, hipStream_t stream) {
+  if (p.logr.size() != 2 || p.logr[0] != p.logr[1] || batch <= G || p.r4k || gl_pad(p) || getenv("PBF_NTT_BLK") ||
+      getenv("PBF_NTT_PERSIST"))
+    return -1;
+  const int tile = gl_tile(p.logr[0]);
+  const GlDualFn dual = p.e64 == 39 ? gl_fn_dual<39>(p.logr[0], tile) : gl_fn_dual<153>(p.logr[0], tile);
+  if (!dual) return -1;
+  const size_t groups = (batch + G - 1) / G;  // the last one may be smaller
+  std::vector<std::vector<GlLaunch>> L(groups);
+  for (size_t g = 0; g < groups; ++g) {
+    const size_t b = std::min(G, batch - g * G);
+    const int rc = run_gl_group(p, d_in + g * G * p.n, d_out + g * G * p.n, b, s0, s1, stream, 0, g * G * gl_pitch(p),
+                                &L[g]);
+    if (rc) return rc;
+    if (L[g].size() != 2 || L[g][0].block != L[g][1].block) return -1;
+  }
+  auto launch = [&](const GlLaunch& l) -> int {
+    hipLaunchKernelGGL(l.fn, dim3(l.grid), dim3(l.block), l.lds, stream, l.a);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  };
+  int rc = launch(L[0][0]);
+  for (size_t g = 1; g < groups && !rc; ++g) {
+    const GlLaunch &sec = L[g - 1][1], &fst = L[g][0];
+    if (sec.grid == fst.grid && sec.grid % 8 == 0 && !sec.lds && !fst.lds) {
+      hipLaunchKernelGGL(dual, dim3(2 * fst.grid), dim3(fst.block), 0, stream, sec.a, fst.a);
+      PBF_HIP(hipGetLastError());
+    } else {  // unequal groups (the remainder): the two passes one after the other
+      if (!(rc = launch(sec))) rc = launch(fst);
+    }
+  }
+  if (!rc) rc = launch(L[groups - 1][1]);
+  return rc;
+}
+
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
   // default schedule (measured best at 2^20 x 32): groups of 4
@@ -633,6 +696,10 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   size_t G = batch >= 8 ? 4 : batch;
   if (const char* g = getenv("PBF_NTT_GROUP")) G = (size_t)atoll(g);
   if (split_log != 0 || G == 0 || G >= batch) return run_gl_group(p, d_in, d_out, batch, s0, s1, stream, split_log);
+  if (getenv("PBF_NTT_DUAL") && !getenv("PBF_NTT_STREAMS")) {
+    const int rc = run_gl_dual(p, d_in, d_out, batch, G, s0, s1, stream);
+    if (rc != -1) return rc;  // -1: this plan has no dual-group form
+  }
   // PBF_NTT_STREAMS=k: groups round-robin over the caller's stream and k-1 more (disjoint
   // scratch), so the passes of k groups run concurrently and their phases interleave
   // (the extra streams are the context's own ForkSet; without one everything stays on `stream`)
@@ -758,7 +825,7 @@ static int run_r4k(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size
 }
 
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff) {
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff, std::vector<GlLaunch>* rec) {
   if (p.r4k && split_log == 0 && gl_pad(p) == 0) return run_r4k(p, d_in, d_out, batch, s0, stream, soff);
   const size_t P = p.logr.size();
   // two-pass plans with equal tile widths may keep the intermediate blocked (ntt_gl.hpp BLK)
@@ -860,8 +927,12 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     // A/B diagnostic: extra dynamic LDS per workgroup (PBF_NTT_LDSPAD bytes) lowers the
     // workgroups resident per CU without changing the code
     const size_t ldspad = getenv("PBF_NTT_LDSPAD") ? (size_t)atoll(getenv("PBF_NTT_LDSPAD")) : 0;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), ldspad, stream, a);
-    PBF_HIP(hipGetLastError());
+    if (rec) {
+      rec->push_back(GlLaunch{fn, grid, (uint32_t)(tile / 16), ldspad, a});
+    } else {
+      hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), ldspad, stream, a);
+      PBF_HIP(hipGetLastError());
+    }
     log_ns += lr;
   }
   return 0;

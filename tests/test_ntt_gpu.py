@@ -251,6 +251,36 @@ def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     assert np.array_equal(d_out.cpu().numpy().view(np.uint64), host)
 
 
+@pytest.mark.parametrize("logn,batch", [(16, 12), (16, 9), (16, 5), (20, 8), (14, 32)])
+def test_dual_group_schedule(ctx, monkeypatch, logn, batch):
+    """The dual-group schedule of batched two-pass transforms (PBF_NTT_DUAL=1, ntt_launch.hip
+    run_gl_dual: one stream, pass 2 of group g-1 and pass 1 of group g in one launch, a smaller
+    last group launched on its own) against the default two-stream schedule and the oracle,
+    forward and inverse, in place."""
+    import torch
+
+    n = 1 << logn
+    w = root(GOLD, n)
+    host = np.stack([oracle.splitmix_field(GOLD, 4100 + i, n) for i in range(batch)])
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for env in ({"PBF_NTT_DUAL": "1"}, {}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        d = torch.from_numpy(host.view(np.int64)).cuda()
+        ctx.ntt_batch_dev(GOLD, w, d.data_ptr(), d.data_ptr(), n, batch, stream=stream)
+        torch.cuda.synchronize()
+        outs.append(d.cpu().numpy().view(np.uint64).copy())
+        ctx.ntt_batch_dev(GOLD, w, d.data_ptr(), d.data_ptr(), n, batch, inverse=True, stream=stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint64), host)
+        for k in env:
+            monkeypatch.delenv(k)
+    assert np.array_equal(outs[0], outs[1])
+    for i in (0, batch - 1):
+        assert np.array_equal(outs[0][i], oracle.ntt_iter(GOLD, w, host[i]))
+
+
 @pytest.mark.parametrize("env", [{"PBF_NTT_TWMAX_LOG": "18"}, {"PBF_NTT_TWSPLIT": "1"},
                                  {"PBF_NTT_TWMAX_LOG": "18", "PBF_NTT_NO_TWSPLIT": "1"}, {"PBF_NTT_PAD": "16"}])
 def test_twiddle_table_paths(monkeypatch, vectors, env):
