@@ -98,9 +98,10 @@ def cpu_baselines_bn254() -> dict:
       config 4 (pairing): the 2-pair KZG pairing check of plonk.rs:646-650 in the Python
                 restatement (oracle/bn254_pairing.py, optimal ate, one core);
       config 5: the generalised C++ prover (oracle/prover_cpu.cpp oracle_plonk_prove_cpu: the GPU
-                prover's O(n log n) algorithms, 4 x u64 Montgomery, every step per proof) at 2^14
-                gates on one core and on all cores, extrapolated n log n to 2^20 (x91.4) and 2^24
-                (x1755); and the literal Python Plonk::prove (O(n^3) interpolation) at n = 8."""
+                prover's O(n log n) algorithms, 4 x u64 Montgomery, every step per proof) measured at
+                2^16 gates on one core and at 2^20 gates on all cores, extrapolated n log n (1 core:
+                x20 to 2^20; all cores: x19.2 to 2^24); and the literal Python Plonk::prove (O(n^3)
+                interpolation) at n = 8."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import random as _r
 
@@ -167,23 +168,32 @@ def cpu_baselines_bn254() -> dict:
     out["config4_pairing_check"] = {"ms": t * 1e3, "unit": "ms (measured)", "cores": 1, "kind": "port", "ok": ok,
                                     "sample": "e(G, H) e(-G, H) == 1 by oracle/bn254_pairing.py pairing_check "
                                               "(Python big integers: optimal-ate Miller loops + one final exp)"}
-    # config 5: the generalised C++ prover at 2^14 gates, 1 core and all cores
-    n5 = 1 << 14
-    q5, c5, abc5 = oracle.synth_circuit(n5, 0x5EED0005, threads=threads)
-    srs5 = oracle.g1_progression(0x5EED0005C0FFEE, 0x1234567, n5 + 3)  # any points: timing only
-    chal5 = [0x1111 * (i + 3) for i in range(5)]
-    rnd5 = [0x2222 * (i + 5) for i in range(9)]
-    f20 = (20 * (1 << 20)) / (14 * n5)
-    f24 = (24 * (1 << 24)) / (14 * n5)
-    for label, th in (("1_core", 1), ("all_cores", threads)):
+    # config 5: the generalised C++ prover (no proving key, every step per proof), measured at
+    # 2^16 gates on one core and at 2^20 gates on all cores; the remaining
+    # extrapolations are n log n: 1 core x 20.0 to 2^20 (x 384 to 2^24), all cores x 19.2 to 2^24
+    f16_20 = (20 * (1 << 20)) / (16 * (1 << 16))
+    f16_24 = (24 * (1 << 24)) / (16 * (1 << 16))
+    f20_24 = (24 * (1 << 24)) / (20 * (1 << 20))
+    for label, th, ln in (("1_core", 1, 16), ("all_cores", threads, 20)):
+        n5 = 1 << ln
+        q5, c5, abc5 = oracle.synth_circuit(n5, 0x5EED0005, threads=threads)
+        srs5 = oracle.g1_progression(0x5EED0005C0FFEE, 0x1234567, n5 + 3)  # any points: timing only
+        chal5 = [0x1111 * (i + 3) for i in range(5)]
+        rnd5 = [0x2222 * (i + 5) for i in range(9)]
         t0 = time.perf_counter()
         oracle.plonk_prove_cpu(n5, q5, c5, abc5, chal5, rnd5, srs5, mode=1, threads=th)
         t = time.perf_counter() - t0
-        out[f"config5_prove_cpp_{label}"] = {
-            "ms_2p14": t * 1e3, "ms_2p20": t * f20 * 1e3, "ms_2p24": t * f24 * 1e3, "cores": th, "kind": "port",
-            "unit": "ms per proof (2^14 measured; 2^20 / 2^24 extrapolated n log n: x91.4 / x1755)",
-            "sample": "oracle/prover_cpu.cpp oracle_plonk_prove_cpu (NTT interpolation and quotient, prefix-product "
-                      "accumulator, synthetic-division openings, Pippenger commitments; no proving key), mode 1"}
+        if ln == 16:
+            ent = {"ms_2p16": t * 1e3, "ms_2p20": t * f16_20 * 1e3, "ms_2p24": t * f16_24 * 1e3,
+                   "unit": "ms per proof (2^16 measured; 2^20 / 2^24 extrapolated n log n: x20.0 / x384)"}
+        else:
+            ent = {"ms_2p20": t * 1e3, "ms_2p24": t * f20_24 * 1e3,
+                   "unit": "ms per proof (2^20 measured; 2^24 extrapolated n log n: x19.2)"}
+        out[f"config5_prove_cpp_{label}"] = dict(
+            ent, cores=th, kind="port",
+            sample="oracle/prover_cpu.cpp oracle_plonk_prove_cpu (NTT interpolation and quotient, prefix-product "
+                   "accumulator, synthetic-division openings, Pippenger commitments; no proving key), mode 1")
+        del q5, c5, abc5, srs5
     prov = {}
     r2 = _r.Random(0x5EED0003)
     for n in (8,):

@@ -620,6 +620,11 @@ int ForkSet::ensure(int streams) {
     if (!aux[i]) PBF_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     if (!join[i]) PBF_HIP(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
   }
+  if (!flags) {
+    PBF_HIP(hipMalloc((void**)&flags, GL_MAX_STREAMS * sizeof(uint64_t)));
+    PBF_HIP(hipMemset(flags, 0, GL_MAX_STREAMS * sizeof(uint64_t)));
+    PBF_HIP(hipDeviceSynchronize());
+  }
   return 0;
 }
 
@@ -633,6 +638,7 @@ ForkSet::~ForkSet() {
     if (join[i]) (void)hipEventDestroy(join[i]);
   }
   if (fork) (void)hipEventDestroy(fork);
+  if (flags) (void)hipFree(flags);
 }
 
 // Dual-group schedule of a two-pass plan (round 5, opt-in PBF_NTT_DUAL=1): ONE stream, launches
@@ -708,12 +714,20 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   if (!fork) ns = 1;
   hipStream_t sts[GL_MAX_STREAMS];
   sts[0] = stream;
+  const bool memop = getenv("PBF_NTT_MEMOP") != nullptr;
+  uint64_t seq = 0;
   if (ns > 1) {
     int rc = fork->ensure(ns);
     if (rc) return rc;
     for (int i = 1; i < ns; ++i) sts[i] = fork->aux[i];
-    PBF_HIP(hipEventRecord(fork->fork, stream));
-    for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], fork->fork, 0));
+    if (memop) {
+      seq = ++fork->seq;
+      PBF_HIP(hipStreamWriteValue64(stream, fork->flags, seq, 0));
+      for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitValue64(sts[i], fork->flags, seq, hipStreamWaitValueGte, ~0ull));
+    } else {
+      PBF_HIP(hipEventRecord(fork->fork, stream));
+      for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], fork->fork, 0));
+    }
   }
   int gi = 0;
   for (size_t g0 = 0; g0 < batch; g0 += G, ++gi) {
@@ -724,8 +738,13 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   }
   if (ns > 1) {
     for (int i = 1; i < ns; ++i) {
-      PBF_HIP(hipEventRecord(fork->join[i], sts[i]));
-      PBF_HIP(hipStreamWaitEvent(stream, fork->join[i], 0));
+      if (memop) {
+        PBF_HIP(hipStreamWriteValue64(sts[i], fork->flags + i, seq, 0));
+        PBF_HIP(hipStreamWaitValue64(stream, fork->flags + i, seq, hipStreamWaitValueGte, ~0ull));
+      } else {
+        PBF_HIP(hipEventRecord(fork->join[i], sts[i]));
+        PBF_HIP(hipStreamWaitEvent(stream, fork->join[i], 0));
+      }
     }
   }
   return 0;
