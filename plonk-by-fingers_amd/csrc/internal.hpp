@@ -118,8 +118,8 @@ struct ForkSet {
   int device = 0;
   hipStream_t aux[GL_MAX_STREAMS] = {};  // aux[0] unused: slot 0 is the caller's stream
   hipEvent_t fork = nullptr, join[GL_MAX_STREAMS] = {};
-  // stream memory operations instead of events (A/B, PBF_NTT_MEMOP=1): flags[0] fork,
-  // flags[i] join of stream i, each set to the call's sequence number
+  // stream memory operations instead of events (default; PBF_NTT_EVENTS=1 for events): flags[0]
+  // fork, flags[i] join of stream i, each set to the call's sequence number
   uint64_t* flags = nullptr;
   uint64_t seq = 0;
   int ensure(int streams);               // streams 1..streams-1 and the event pair exist

@@ -714,7 +714,11 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   if (!fork) ns = 1;
   hipStream_t sts[GL_MAX_STREAMS];
   sts[0] = stream;
-  const bool memop = getenv("PBF_NTT_MEMOP") != nullptr;
+  // fork / join by stream memory operations (round 5 default; PBF_NTT_EVENTS=1 restores hipEvent
+  // waits): a flag written by one stream and waited on by the other resolves faster than an
+  // event wait across hardware queues: 2^20 x 32 0.349-0.352 against 0.357-0.360 ms, three
+  // alternations on one box (profiles/r05/memop_ab.log)
+  const bool memop = getenv("PBF_NTT_EVENTS") == nullptr;
   uint64_t seq = 0;
   if (ns > 1) {
     int rc = fork->ensure(ns);

@@ -225,7 +225,7 @@ def test_batch_dev_matches_single(ctx):
                                  {"PBF_NTT_GROUP": "1", "PBF_NTT_STREAMS": "3"}, {"PBF_NTT_STREAMS": "1"},
                                  {"PBF_NTT_GROUP": "0"}, {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"},
                                  {"PBF_NTT_NO_KMAJOR": "1"}, {"PBF_NTT_PAD": "16"}, {"PBF_NTT_PAD": "8", "PBF_NTT_STREAMS": "1"},
-                                 {"PBF_NTT_NO_PRETW": "1"}])
+                                 {"PBF_NTT_NO_PRETW": "1"}, {"PBF_NTT_EVENTS": "1"}])
 @pytest.mark.parametrize("logn", [16, 20])
 def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     """Every opt-in schedule of the Goldilocks pass kernel (blocked intermediate, persistent
