@@ -783,6 +783,196 @@ __global__ void __launch_bounds__(PT) pairing_product_kernel(const uint64_t* g1,
   }
 }
 
+// ---------------------------------------------------------------- lane engine (throughput)
+// Batched independent pairings (pbf_pairing_bn254_dev at n >= PAIR_LANE_MIN):
+// ONE LANE PER PAIRING. The Miller loop's step schedule and the final exponentiation are the
+// same for every pairing (fixed 6u+2 and exponent), so the 64 lanes of a wave run one
+// instruction stream in lock-step on 64 different pairs -- no cross-lane traffic, no barriers,
+// every lane busy -- where the workgroup engine above spends its lanes on one pairing's
+// latency. The state (f in Fq12, T, Q, P) is per lane; what does not fit the registers the
+// compiler keeps in scratch. Fq12 in the tower Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - xi)
+// (flat w^k: c0 = (w^0, w^2, w^4), c1 = (w^1, w^3, w^5), the ABI's tower order); Karatsuba
+// products (54 Fq products), complex squaring in the Miller loop (36), the line as a sparse
+// operand (a yP at w^0, b xP at w^1, c at w^3: 39), Granger-Scott cyclotomic squaring in the
+// hard part (21). Line formulas, step schedule and final-exponentiation chain are the
+// workgroup engine's (prep_lines_kernel, make_fe_prog), so every value is the exact reduced
+// pairing, bit-identical to oracle/bn254_pairing.py.
+struct Fq6 {
+  Fq2 c0, c1, c2;
+};
+struct Fq12 {
+  Fq6 c0, c1;
+};
+__device__ __forceinline__ Fq6 f6_add(const Fq6& a, const Fq6& b) {
+  return {f2_add(a.c0, b.c0), f2_add(a.c1, b.c1), f2_add(a.c2, b.c2)};
+}
+__device__ __forceinline__ Fq6 f6_sub(const Fq6& a, const Fq6& b) {
+  return {f2_sub(a.c0, b.c0), f2_sub(a.c1, b.c1), f2_sub(a.c2, b.c2)};
+}
+__device__ __forceinline__ Fq6 f6_neg(const Fq6& a) { return {f2_neg(a.c0), f2_neg(a.c1), f2_neg(a.c2)}; }
+__device__ __forceinline__ Fq6 f6_mul_v(const Fq6& a) { return {f2_mul_xi(a.c2), a.c0, a.c1}; }
+// the Fq6 products are real calls (one copy each): inlined, the engine's code grows past what
+// the compiler schedules in reasonable time
+__device__ __noinline__ Fq6 f6_mul(const Fq6& a, const Fq6& b) {
+  const Fq2 t0 = f2_mul(a.c0, b.c0), t1 = f2_mul(a.c1, b.c1), t2 = f2_mul(a.c2, b.c2);
+  const Fq2 u0 = f2_sub(f2_sub(f2_mul(f2_add(a.c1, a.c2), f2_add(b.c1, b.c2)), t1), t2);
+  const Fq2 u1 = f2_sub(f2_sub(f2_mul(f2_add(a.c0, a.c1), f2_add(b.c0, b.c1)), t0), t1);
+  const Fq2 u2 = f2_sub(f2_sub(f2_mul(f2_add(a.c0, a.c2), f2_add(b.c0, b.c2)), t0), t2);
+  return {f2_add(t0, f2_mul_xi(u0)), f2_add(u1, f2_mul_xi(t2)), f2_add(u2, t1)};
+}
+// a (b0 + b1 v): c0 = a0 b0 + xi a2 b1, c1 = a0 b1 + a1 b0, c2 = a1 b1 + a2 b0
+__device__ __noinline__ Fq6 f6_mul_01(const Fq6& a, const Fq2& b0, const Fq2& b1) {
+  return {f2_add(f2_mul(a.c0, b0), f2_mul_xi(f2_mul(a.c2, b1))), f2_add(f2_mul(a.c0, b1), f2_mul(a.c1, b0)),
+          f2_add(f2_mul(a.c1, b1), f2_mul(a.c2, b0))};
+}
+__device__ __forceinline__ Fq12 f12_mul(const Fq12& a, const Fq12& b) {
+  const Fq6 t0 = f6_mul(a.c0, b.c0), t1 = f6_mul(a.c1, b.c1);
+  const Fq6 s = f6_mul(f6_add(a.c0, a.c1), f6_add(b.c0, b.c1));
+  return {f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(s, t0), t1)};
+}
+// (a0 + a1 w)^2 = (a0 + a1)(a0 + v a1) - t - v t + 2 t w, t = a0 a1
+__device__ __forceinline__ Fq12 f12_sqr(const Fq12& a) {
+  const Fq6 t = f6_mul(a.c0, a.c1);
+  const Fq6 s = f6_mul(f6_add(a.c0, a.c1), f6_add(a.c0, f6_mul_v(a.c1)));
+  return {f6_sub(f6_sub(s, t), f6_mul_v(t)), f6_add(t, t)};
+}
+// f * l, l = A0 + (B0 + B1 v) w (the line: A0 = a yP at w^0, B0 = b xP at w^1, B1 = c at w^3)
+__device__ __forceinline__ Fq12 f12_mul_line(const Fq12& f, const Fq2& A0, const Fq2& B0, const Fq2& B1) {
+  const Fq6 t0 = {f2_mul(f.c0.c0, A0), f2_mul(f.c0.c1, A0), f2_mul(f.c0.c2, A0)};
+  const Fq6 t1 = f6_mul_01(f.c1, B0, B1);
+  const Fq6 s = f6_mul_01(f6_add(f.c0, f.c1), f2_add(A0, B0), B1);
+  return {f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(s, t0), t1)};
+}
+__device__ __forceinline__ Fq12 f12_conj(const Fq12& a) { return {a.c0, f6_neg(a.c1)}; }
+// x^q: flat g_k -> conj(g_k) FROB1[k]
+__device__ __forceinline__ Fq12 f12_frob1(const Fq12& a, const PairingConsts& k) {
+  auto fr = [&](const Fq2& g, int i) { return f2_mul(f2_conj(g), Fq2{k.frob1[i][0], k.frob1[i][1]}); };
+  return {{fr(a.c0.c0, 0), fr(a.c0.c1, 2), fr(a.c0.c2, 4)}, {fr(a.c1.c0, 1), fr(a.c1.c1, 3), fr(a.c1.c2, 5)}};
+}
+// x^(q^2): flat g_k -> g_k FROB2[k]
+__device__ __forceinline__ Fq12 f12_frob2(const Fq12& a, const PairingConsts& k) {
+  return {{f2_muls(a.c0.c0, k.frob2[0]), f2_muls(a.c0.c1, k.frob2[2]), f2_muls(a.c0.c2, k.frob2[4])},
+          {f2_muls(a.c1.c0, k.frob2[1]), f2_muls(a.c1.c1, k.frob2[3]), f2_muls(a.c1.c2, k.frob2[5])}};
+}
+// Granger-Scott squaring in the cyclotomic subgroup (the workgroup engine's w_csqr, per lane):
+// A_m = g_m + g_(m+3) s (s = w^3, s^2 = xi), A_m^2 = (a^2 + xi b^2) + 2 a b s; flat outputs
+// 3 S -/+ 2 g_k
+__device__ __noinline__ Fq12 f12_csqr(const Fq12& x) {
+  const Fq2 g[6] = {x.c0.c0, x.c1.c0, x.c0.c1, x.c1.c1, x.c0.c2, x.c1.c2};  // flat w^0..w^5
+  Fq2 lo[3], hi[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const Fq2 a = g[m], b = g[m + 3];
+    lo[m] = f2_add(f2_sqr(a), f2_mul_xi(f2_sqr(b)));
+    hi[m] = f2_dbl(f2_mul(a, b));
+  }
+  const Fq2 S[6] = {lo[0], f2_mul_xi(hi[2]), lo[1], hi[0], lo[2], hi[1]};
+  Fq2 o[6];
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    const Fq2 s3 = f2_add(f2_dbl(S[kk]), S[kk]), g2 = f2_dbl(g[kk]);
+    o[kk] = (kk & 1) ? f2_add(s3, g2) : f2_sub(s3, g2);
+  }
+  return {{o[0], o[2], o[4]}, {o[1], o[3], o[5]}};
+}
+__device__ __forceinline__ Fq6 f6_inv(const Fq6& n, const PairingConsts& k) {
+  const Fq2 t0 = f2_sub(f2_sqr(n.c0), f2_mul_xi(f2_mul(n.c1, n.c2)));
+  const Fq2 t1 = f2_sub(f2_mul_xi(f2_sqr(n.c2)), f2_mul(n.c0, n.c1));
+  const Fq2 t2 = f2_sub(f2_sqr(n.c1), f2_mul(n.c0, n.c2));
+  const Fq2 den = f2_add(f2_mul(n.c0, t0), f2_mul_xi(f2_add(f2_mul(n.c2, t1), f2_mul(n.c1, t2))));
+  const Fq2 di = f2_inv(den, k);
+  return {f2_mul(t0, di), f2_mul(t1, di), f2_mul(t2, di)};
+}
+// f^((q^12-1)/r): make_fe_prog's chain run by an interpreter over per-lane Fq12 registers (a
+// local array: scratch), each primitive inlined once; the hard part's squarings are cyclotomic
+// (the value is in the cyclotomic subgroup there, so they are the same field elements)
+__device__ __noinline__ void f12_final_exp(Fq12* R, const PairingConsts& k) {
+  const Fq2 z{u256_zero(), u256_zero()};
+  for (int pc = 0; pc < c_fe_prog.n; ++pc) {
+    const FeOp o = c_fe_prog.ops[pc];
+    const Fq12 a = R[o.op == FE_INVN ? o.dst : o.a];
+    Fq12 d;
+    switch (o.op) {
+      case FE_MUL: d = f12_mul(a, R[o.b]); break;
+      case FE_CSQR: d = f12_csqr(a); break;
+      case FE_CONJ: d = f12_conj(a); break;
+      case FE_FROB1: d = f12_frob1(a, k); break;
+      case FE_FROB2: d = f12_frob2(a, k); break;
+      case FE_COPY: d = a; break;
+      default: d = Fq12{f6_inv(a.c0, k), {z, z, z}}; break;  // FE_INVN: an Fq6 value (c1 = 0)
+    }
+    R[o.dst] = d;
+  }
+}
+
+constexpr size_t PAIR_LANE_MIN = 64;  // batches from this size take the lane engine
+
+__global__ void __launch_bounds__(64) pairing_lane_kernel(const uint64_t* g1, const uint64_t* g2, size_t n,
+                                                          uint64_t* out, PairingConsts k) {
+  const size_t i0 = (size_t)blockIdx.x * 64 + threadIdx.x;
+  const size_t i = i0 < n ? i0 : n - 1;  // surplus lanes repeat the last pair and store nothing
+  const uint64_t* p = g1 + 8 * i;
+  const uint64_t* q = g2 + 16 * i;
+  const bool inf = all_zero(p, 8) || all_zero(q, 16);
+  const U256 xp = ld_mont(p), yp = ld_mont(p + 4);
+  const Fq2 xq{ld_mont(q), ld_mont(q + 4)}, yq{ld_mont(q + 8), ld_mont(q + 12)};
+  // Q, pi(Q), -pi^2(Q) (prep_lines_kernel)
+  const Fq2 gx{k.frob1[2][0], k.frob1[2][1]}, gy{k.frob1[3][0], k.frob1[3][1]};
+  const Fq2 x1 = f2_mul(f2_conj(xq), gx), y1 = f2_mul(f2_conj(yq), gy);
+  const Fq2 x2 = f2_mul(f2_conj(x1), gx), y2 = f2_neg(f2_mul(f2_conj(y1), gy));
+  Fq2 X = xq, Y = yq, Z{k.one, u256_zero()};
+  const Fq2 zero{u256_zero(), u256_zero()};
+  Fq12 f{{Fq2{k.one, u256_zero()}, zero, zero}, {zero, zero, zero}};
+  for (int st = 0; st < NSTEP; ++st) {
+    const int kind = c_steps.kind[st];
+    Fq2 la, lb, lc;  // line: la yP + (lb xP) w + lc w^3
+    if (kind == ST_DBL) {
+      if (st > 0) f = f12_sqr(f);
+      // w = 3X^2, s = 2YZ, R = Y s, B = (X+R)^2 - X^2 - R^2, h = w^2 - 2B,
+      // X3 = h s, Y3 = w (B - h) - 2 R^2, Z3 = s^3; line (sZ, -wZ, wX - R)
+      const Fq2 xx = f2_sqr(X), w = f2_add(f2_dbl(xx), xx), s = f2_dbl(f2_mul(Y, Z));
+      const Fq2 R = f2_mul(Y, s), RR = f2_sqr(R);
+      const Fq2 B = f2_sub(f2_sub(f2_sqr(f2_add(X, R)), xx), RR);
+      const Fq2 h = f2_sub(f2_sqr(w), f2_dbl(B));
+      la = f2_mul(s, Z);
+      lb = f2_neg(f2_mul(w, Z));
+      lc = f2_sub(f2_mul(w, X), R);
+      X = f2_mul(h, s);
+      Y = f2_sub(f2_mul(w, f2_sub(B, h)), f2_dbl(RR));
+      Z = f2_mul(f2_sqr(s), s);
+    } else {
+      const Fq2 xa = kind == ST_ADD_Q ? xq : (kind == ST_ADD_PI ? x1 : x2);
+      const Fq2 ya = kind == ST_ADD_Q ? yq : (kind == ST_ADD_PI ? y1 : y2);
+      // N = yq Z - Y, D = xq Z - X, A = N^2 Z - D^3 - 2 D^2 X, X3 = D A,
+      // Y3 = N (D^2 X - A) - D^3 Y, Z3 = D^3 Z; line (D, -N, N xq - D yq)
+      const Fq2 N = f2_sub(f2_mul(ya, Z), Y), D = f2_sub(f2_mul(xa, Z), X);
+      const Fq2 DD = f2_sqr(D), DDD = f2_mul(D, DD), DDX = f2_mul(DD, X);
+      const Fq2 A = f2_sub(f2_sub(f2_mul(f2_sqr(N), Z), DDD), f2_dbl(DDX));
+      la = D;
+      lb = f2_neg(N);
+      lc = f2_sub(f2_mul(N, xa), f2_mul(D, ya));
+      X = f2_mul(D, A);
+      Y = f2_sub(f2_mul(N, f2_sub(DDX, A)), f2_mul(DDD, Y));
+      Z = f2_mul(DDD, Z);
+    }
+    f = f12_mul_line(f, f2_muls(la, yp), f2_muls(lb, xp), lc);
+  }
+  Fq12 R[16];
+  R[0] = f;
+  f12_final_exp(R, k);
+  f = R[0];
+  if (inf) f = Fq12{{Fq2{k.one, u256_zero()}, zero, zero}, {zero, zero, zero}};
+  if (i0 < n) {
+    uint64_t* o = out + 48 * i;
+    const Fq2 c[6] = {f.c0.c0, f.c0.c1, f.c0.c2, f.c1.c0, f.c1.c1, f.c1.c2};
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      st_canon(o + 8 * j, c[j].c0);
+      st_canon(o + 8 * j + 4, c[j].c1);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- G2 scalar multiplication
 struct G2A {
   Fq2 x, y;
@@ -876,10 +1066,19 @@ static int prep_lines(pbf_ctx* ctx, const uint64_t* d_g2, size_t n, hipStream_t 
   return 0;
 }
 
-// e(P_i, Q_i) for every i: prepared lines, then one workgroup per pair
+// e(P_i, Q_i) for every i: from PAIR_LANE_MIN pairs one lane per pairing (pairing_lane_kernel;
+// PBF_PAIR_WG=1 keeps the workgroup engine), below that prepared lines, then one workgroup per
+// pair (the latency form)
 static int pairing_values(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_g2, size_t n, uint64_t* d_out,
                           hipStream_t s) {
   const PairingConsts k = make_consts();
+  const char* lane_env = getenv("PBF_PAIR_LANE");  // A/B: 1 forces the lane engine, 0 the workgroup one
+  const bool lane = lane_env ? lane_env[0] == '1' : (n >= PAIR_LANE_MIN && !getenv("PBF_PAIR_WG"));
+  if (lane) {
+    hipLaunchKernelGGL(pairing_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, d_g1, d_g2, n, d_out, k);
+    PBF_HIP(hipGetLastError());
+    return 0;
+  }
   PrepLine* lines;
   uint8_t* qinf;
   int rc = prep_lines(ctx, d_g2, n, s, k, &lines, &qinf);

@@ -52,6 +52,41 @@ def test_bilinearity_on_device(ctx):
     assert e1 == B.f12_flat(B.f12_pow(B.f12_from_flat(e2), a * b))
 
 
+def test_lane_engine_matches_oracle(ctx, monkeypatch):
+    """The lane-per-pairing engine (pairing_lane_kernel, PBF_PAIR_LANE=1 forces it below its
+    batch threshold) against the oracle: generators, random points, identities, bilinearity."""
+    monkeypatch.setenv("PBF_PAIR_LANE", "1")
+    rng = random.Random(41)
+    ps = [B.G1_GEN, None, B.G1_GEN] + [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(2)]
+    qs = [B.G2_GEN, B.G2_GEN, None] + [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(2)]
+    got = ctx.pairing_bn254(ps, qs)
+    one = B.f12_flat(B.F12_ONE)
+    assert got[1] == one and got[2] == one
+    for idx in (0, 3, 4):
+        assert got[idx] == B.f12_flat(B.pairing(ps[idx], qs[idx])), idx
+    a, b = 77, 1009
+    e1, e2 = ctx.pairing_bn254([B.g1_mul(B.G1_GEN, a), B.G1_GEN], [B.g2_mul(B.G2_GEN, b), B.G2_GEN])
+    assert e1 == B.f12_flat(B.f12_pow(B.f12_from_flat(e2), a * b))
+
+
+def test_lane_engine_matches_workgroup_engine(ctx, monkeypatch):
+    """A batch of 131 pairs (two full waves and a ragged one; identities mixed in) through both
+    engines, bit for bit (the default for this size is the lane engine)."""
+    rng = random.Random(43)
+    n = 131
+    ks = [rng.randrange(1, B.R) for _ in range(n)]
+    ls = [rng.randrange(1, B.R) for _ in range(n)]
+    ps = ctx.g1_bn254_mul([B.G1_GEN] * n, ks) if hasattr(ctx, "g1_bn254_mul") else [B.g1_mul(B.G1_GEN, k) for k in ks]
+    qs = ctx.g2_bn254_mul([B.G2_GEN] * n, ls)
+    ps[5] = None
+    qs[77] = None
+    monkeypatch.setenv("PBF_PAIR_LANE", "0")
+    wg = ctx.pairing_bn254(ps, qs)
+    monkeypatch.setenv("PBF_PAIR_LANE", "1")
+    lane = ctx.pairing_bn254(ps, qs)
+    assert lane == wg
+
+
 def test_g2_mul_matches_oracle(ctx):
     rng = random.Random(9)
     ks = [0, 1, 2, B.R - 1, rng.randrange(B.R), rng.randrange(B.R)]
