@@ -41,6 +41,29 @@ FQ_MUL_PEAK = MAD_RATE / 136
 BUFFER_SETS = 3  # input/output pairs the NTT steps rotate over
 
 
+def pairing_fq_products() -> int:
+    """Fq products of one pairing in the lane engine (csrc/pairing.hip pairing_lane_kernel):
+    Miller steps of 6u+2 (doubling: f^2 36 + T 34 + line evaluation 4 + sparse product 45; mixed
+    addition: T 37 + 4 + 45), then make_fe_prog's final exponentiation (Fq12 product 54,
+    cyclotomic square 21, Frobenius q 18 / q^2 12, the Fq6 inversion ~30 plus one Fq inversion)."""
+    ate_lo, u = 0x9d797039be763ba8, 0x44e992b44a6909f1
+    adds = bin(ate_lo).count("1") + 2
+    miller = 64 * (36 + 34 + 4 + 45) - 36 + adds * (37 + 4 + 45)
+    naf, e = [], u
+    while e:
+        z = 0
+        if e & 1:
+            z = 2 - (e & 3)
+            e = e - 1 if z > 0 else e + 1
+        naf.append(z)
+        e >>= 1
+    powu = 21 * (len(naf) - 1) + 54 * sum(1 for z in naf[:-1] if z)
+    # easy part 4 products + 1 frob2 + inverse; hard part 3 powu, 12 squares, 17 products,
+    # 2 frob1 + 3 frob2 (make_fe_prog)
+    fe = 4 * 54 + 12 + 30 + 3 * powu + 12 * 21 + 17 * 54 + 2 * 18 + 3 * 12
+    return miller + fe
+
+
 def root_of_unity(n: int) -> int:
     return pow(7, (GOLD - 1) // n, GOLD)
 
@@ -99,8 +122,8 @@ def cpu_baselines_bn254() -> dict:
                 restatement (oracle/bn254_pairing.py, optimal ate, one core);
       config 5: the generalised C++ prover (oracle/prover_cpu.cpp oracle_plonk_prove_cpu: the GPU
                 prover's O(n log n) algorithms, 4 x u64 Montgomery, every step per proof) measured at
-                2^16 gates on one core and at 2^20 gates on all cores, extrapolated n log n (1 core:
-                x20 to 2^20; all cores: x19.2 to 2^24); and the literal Python Plonk::prove (O(n^3)
+                2^17 gates on one core and at 2^20 gates on all cores, extrapolated n log n (1 core:
+                x9.4 to 2^20; all cores: x19.2 to 2^24); and the literal Python Plonk::prove (O(n^3)
                 interpolation) at n = 8."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import random as _r
@@ -169,12 +192,12 @@ def cpu_baselines_bn254() -> dict:
                                     "sample": "e(G, H) e(-G, H) == 1 by oracle/bn254_pairing.py pairing_check "
                                               "(Python big integers: optimal-ate Miller loops + one final exp)"}
     # config 5: the generalised C++ prover (no proving key, every step per proof), measured at
-    # 2^16 gates on one core and at 2^20 gates on all cores; the remaining
-    # extrapolations are n log n: 1 core x 20.0 to 2^20 (x 384 to 2^24), all cores x 19.2 to 2^24
-    f16_20 = (20 * (1 << 20)) / (16 * (1 << 16))
-    f16_24 = (24 * (1 << 24)) / (16 * (1 << 16))
+    # 2^17 gates on one core and at 2^20 gates on all cores; the remaining
+    # extrapolations are n log n: 1 core x 9.4 to 2^20 (x 180 to 2^24), all cores x 19.2 to 2^24
+    f17_20 = (20 * (1 << 20)) / (17 * (1 << 17))
+    f17_24 = (24 * (1 << 24)) / (17 * (1 << 17))
     f20_24 = (24 * (1 << 24)) / (20 * (1 << 20))
-    for label, th, ln in (("1_core", 1, 16), ("all_cores", threads, 20)):
+    for label, th, ln in (("1_core", 1, 17), ("all_cores", threads, 20)):
         n5 = 1 << ln
         q5, c5, abc5 = oracle.synth_circuit(n5, 0x5EED0005, threads=threads)
         srs5 = oracle.g1_progression(0x5EED0005C0FFEE, 0x1234567, n5 + 3)  # any points: timing only
@@ -183,9 +206,9 @@ def cpu_baselines_bn254() -> dict:
         t0 = time.perf_counter()
         oracle.plonk_prove_cpu(n5, q5, c5, abc5, chal5, rnd5, srs5, mode=1, threads=th)
         t = time.perf_counter() - t0
-        if ln == 16:
-            ent = {"ms_2p16": t * 1e3, "ms_2p20": t * f16_20 * 1e3, "ms_2p24": t * f16_24 * 1e3,
-                   "unit": "ms per proof (2^16 measured; 2^20 / 2^24 extrapolated n log n: x20.0 / x384)"}
+        if ln == 17:
+            ent = {"ms_2p17": t * 1e3, "ms_2p20": t * f17_20 * 1e3, "ms_2p24": t * f17_24 * 1e3,
+                   "unit": "ms per proof (2^17 measured; 2^20 / 2^24 extrapolated n log n: x9.4 / x180)"}
         else:
             ent = {"ms_2p20": t * 1e3, "ms_2p24": t * f20_24 * 1e3,
                    "unit": "ms per proof (2^20 measured; 2^24 extrapolated n log n: x19.2)"}
@@ -230,7 +253,9 @@ def live_traffic(log_n: int, batch: int, steps: int = 6, fetch_scale: float = 1.
     tmp = tempfile.mkdtemp(prefix="pbf_traffic_", dir="/tmp")
     child = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", "0", "--no-cpu",
              "--no-extra", "--no-traffic", "--log-n", str(log_n), "--batch", str(batch)]
-    env = dict(os.environ, TMPDIR="/tmp")
+    # events for the NTT's stream fork / join in the profiled child (the library also switches to
+    # them under counter collection: the profiler serialises the queues a flag wait spans)
+    env = dict(os.environ, TMPDIR="/tmp", PBF_NTT_EVENTS="1")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", tmp, "-o", counter.lower(), "--"] + child
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -435,7 +460,7 @@ _NOTE_KEYS = ("sample", "note", "peak_source", "proving_key", "rounds_note", "so
 # north-star and per-config headline entries come last
 _EXTRA_ORDER = ("notes", "cpu_baselines_configs_3_5", "config1_plonk_by_hand", "config5_prove_2p20_mode0",
                 "config5_prove_2p20_4_streams", "config5_prove_2p20", "config4_bn254_msm_2p20", "config4_pairing_check",
-                "config4_pairings_batch", "config4_kzg_commit_2p20", "config3_bn254_polymul_2p22", "ntt_2p24",
+                "config4_pairings_batch", "config4_pairings_batch_65536", "config4_kzg_commit_2p20", "config3_bn254_polymul_2p22", "ntt_2p24",
                 "config5_prove_2p24", "config5_prove_sharded")
 
 
@@ -655,18 +680,47 @@ def other_configs(ctx, sp) -> dict:
     first_ms = (time.perf_counter() - t0) * 1e3
     ctx2.close()
     t = _median_ms(lambda: oks.append(ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])))  # e(G,H) e(-G,H) = 1
-    res["config4_pairing_check"] = dict(t, ok=all(oks), first_call_ms=first_ms,
-                                        note="host round trip incl. copies; 2 pairs, one multi-Miller loop and "
-                                             "one final exponentiation; prepared G2 lines reused after the first "
-                                             "call (first_call_ms: fresh context, lines built)")
-    npair = 4096
-    g1 = pbf.ints_to_limbs([c for _ in range(npair) for c in G1G])
-    g2 = pbf.ints_to_limbs([c for _ in range(npair) for c in (G2G[0][0], G2G[0][1], G2G[1][0], G2G[1][1])])
-    d1, d2 = torch.from_numpy(g1.view(np.int64)).cuda(), torch.from_numpy(g2.view(np.int64)).cuda()
-    dout = torch.empty(npair * 48, dtype=torch.int64, device="cuda")
-    t = _median_ms(lambda: ctx.pairing_bn254_dev(d1.data_ptr(), d2.data_ptr(), npair, dout.data_ptr(), stream=sp),
-                   reps=5, warmup=1)
-    res["config4_pairings_batch"] = dict(t, pairings_per_s=npair / (t["ms"] / 1e3), batch=npair)
+    # device time of the same check: the context's host stream set to torch's stream, so HIP
+    # events on it bracket the copies and the kernel (the call still synchronises)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    dev = _median_ms(lambda: oks.append(ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G])))
+    ctx.set_stream(0)
+    wall = []
+    for _ in range(11):
+        t0 = time.perf_counter()
+        oks.append(ctx.pairing_check_bn254([G1G, negG1], [G2G, G2G]))
+        wall.append((time.perf_counter() - t0) * 1e3)
+    res["config4_pairing_check"] = dict(t, ok=all(oks), first_call_ms=first_ms, device_ms=dev["ms"],
+                                        host_wall_ms=sorted(wall)[len(wall) // 2],
+                                        note="ms: HIP events on torch's stream around the synchronous call "
+                                             "(host round trip incl. copies); device_ms: events on the context's "
+                                             "own stream (the copies and the kernel); 2 pairs, one multi-Miller "
+                                             "loop and one final exponentiation, prepared G2 lines reused after "
+                                             "the first call (first_call_ms: fresh context)")
+    # batched independent pairings (distinct random P_i = k_i G, Q_i = l_i H; Q_i repeat with
+    # period 4096): one lane per pairing (pairing_lane_kernel)
+    nq = 4096
+    rng2 = np.random.default_rng(11)
+    qs = ctx.g2_bn254_mul([G2G] * nq, [int(x) for x in rng2.integers(1, 1 << 62, size=nq)])
+    g2l = pbf.ints_to_limbs([c for q in qs for c in (q[0][0], q[0][1], q[1][0], q[1][1])])
+    fq_pp = pairing_fq_products()
+    for npair in (4096, 65536):
+        sc = rng2.integers(0, 1 << 62, size=(npair, 4), dtype=np.uint64)
+        sc[:, 3] = 0
+        dsc = torch.from_numpy(sc.reshape(-1).view(np.int64)).cuda()
+        d1 = torch.empty(npair * 8, dtype=torch.int64, device="cuda")
+        ctx.g1_mul_base_dev(dsc.data_ptr(), d1.data_ptr(), npair, stream=sp)
+        d2 = torch.from_numpy(np.tile(g2l, npair // nq).view(np.int64)).cuda()
+        dout = torch.empty(npair * 48, dtype=torch.int64, device="cuda")
+        t = _median_ms(lambda: ctx.pairing_bn254_dev(d1.data_ptr(), d2.data_ptr(), npair, dout.data_ptr(), stream=sp),
+                       reps=5, warmup=1)
+        ach = npair * fq_pp / (t["ms"] / 1e3)
+        res[f"config4_pairings_batch{'' if npair == 4096 else '_' + str(npair)}"] = dict(
+            t, pairings_per_s=npair / (t["ms"] / 1e3), batch=npair,
+            roofline={"bound": "valu (Fq products)", "achieved": ach, "peak": FQ_MUL_PEAK, "unit": "Fq products/s",
+                      "frac": ach / FQ_MUL_PEAK, "fq_products_per_pairing": fq_pp},
+            note="one lane per pairing (pairing_lane_kernel); a batch of 4096 fills 64 of 1024 SIMDs")
+        del d1, d2, dout, dsc
     # config 5: generalised PLONK prove (+ verify) of the synthetic mul circuit, 2^20 gates on
     # one GPU (scripts/bench_prover.py; 2^24 gates: profiles/r01/session2/prover_2p22_2p24.log)
     sys.path.insert(0, os.path.join(ROOT, "scripts"))

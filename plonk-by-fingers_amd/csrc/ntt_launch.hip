@@ -718,7 +718,10 @@ static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
   // waits): a flag written by one stream and waited on by the other resolves faster than an
   // event wait across hardware queues: 2^20 x 32 0.349-0.352 against 0.357-0.360 ms, three
   // alternations on one box (profiles/r05/memop_ab.log)
-  const bool memop = getenv("PBF_NTT_EVENTS") == nullptr;
+  // Under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION, which serialises dispatches
+  // across queues) a stream waiting on a flag that another queue writes never resumes: events
+  // there (profiles/r05/memop_prof.log).
+  const bool memop = getenv("PBF_NTT_EVENTS") == nullptr && getenv("ROCPROF_COUNTER_COLLECTION") == nullptr;
   uint64_t seq = 0;
   if (ns > 1) {
     int rc = fork->ensure(ns);
