@@ -29,6 +29,7 @@
 // limbs (GT: 12 Fq in tower order c0.a0, c0.a1, c0.a2, c1.a0, c1.a1, c1.a2 = w^0, w^2,
 // w^4, w^1, w^3, w^5).
 #include <cstring>
+#include <mutex>
 #include <vector>
 #include "../../include/pbf.h"
 #include "ec_bn254.hpp"
@@ -107,69 +108,110 @@ __device__ __forceinline__ Fq2 f2_mul_xi(const Fq2& a) {
 __device__ __forceinline__ bool f2_eq(const Fq2& a, const Fq2& b) { return Fq::eq(a.c0, b.c0) && Fq::eq(a.c1, b.c1); }
 __device__ __forceinline__ bool f2_is_zero(const Fq2& a) { return Fq::is_zero(a.c0) && Fq::is_zero(a.c1); }
 
-__device__ __forceinline__ bool u256_is_one(const U256& a) {
-  uint32_t o = a.w[0] ^ 1u;
+// a + b without the reduction (< 2q for canonical a, b): a Montgomery product accepts operands
+// below 2q (their product is below q R, so the result stays below 2q before its subtraction)
+__device__ __forceinline__ U256 u256_add_raw(const U256& a, const U256& b) {
+  U256 r;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 1; i < 8; ++i) o |= a.w[i];
+  for (int l = 0; l < 8; ++l) r.w[l] = __builtin_addc(a.w[l], b.w[l], c, &c);
+  return r;
+}
+// Montgomery inverse (aR)^-1 -> a^-1 R by Kaliski's almost-inverse (round 5; binary extended
+// Euclid with one halving mod q per bit before, ~400 k cycles on one lane, now ~1/4 of that):
+// u = q, v = aR, r = 0, s = 1 keep u s + v r = q; every step subtracts the smaller odd value
+// from the larger, adds r and s, and strips the difference's trailing zeros at once (the
+// other of r, s doubled as many times), counting them in k (254 <= k <= 508). It ends with
+// x = q - r = (aR)^-1 2^k mod q, and one Montgomery product with 2^-k R^3 (g_inv2k, filled by
+// the host from K_R3) gives a^-1 R. a != 0.
+__device__ U256 g_inv2k[512];  // 2^-k R^3 mod q (plain), k < 512
+
+__device__ __forceinline__ bool u256_zero_p(const U256& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= a.w[i];
   return o == 0;
 }
-__device__ __forceinline__ bool u256_geq(const U256& a, const U256& b) {
+__device__ __forceinline__ int u256_ctz(const U256& a) {  // a != 0
+  uint32_t w = a.w[7];
+  int base = 224;
 #pragma unroll
-  for (int i = 7; i >= 0; --i)
-    if (a.w[i] != b.w[i]) return a.w[i] > b.w[i];
-  return true;
-}
-__device__ __forceinline__ void u256_shr1(U256& a) {
-#pragma unroll
-  for (int i = 0; i < 7; ++i) a.w[i] = (a.w[i] >> 1) | (a.w[i + 1] << 31);
-  a.w[7] >>= 1;
-}
-__device__ __forceinline__ U256 u256_sub_raw(const U256& a, const U256& b) {
-  U256 d;
-  uint64_t borrow = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t t = (uint64_t)a.w[i] - b.w[i] - borrow;
-    d.w[i] = (uint32_t)t;
-    borrow = (t >> 63) & 1;
+  for (int l = 6; l >= 0; --l) {
+    if (a.w[l] != 0) { w = a.w[l]; base = 32 * l; }
   }
-  return d;
+  return base + __builtin_ctz(w);
 }
-// x / 2 mod q for canonical x (x odd: (x + q) / 2 < q, no overflow since q < 2^254)
-__device__ __forceinline__ void fq_half(U256& x) {
-  if (x.w[0] & 1) {
-    uint64_t c = 0;
+__device__ __forceinline__ void u256_shr(U256& a, int t) {  // 0 <= t < 256
+  while (t >= 32) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint64_t t = (uint64_t)x.w[i] + Bn254FqParams::P[i] + c;
-      x.w[i] = (uint32_t)t;
-      c = t >> 32;
-    }
+    for (int l = 0; l < 7; ++l) a.w[l] = a.w[l + 1];
+    a.w[7] = 0;
+    t -= 32;
   }
-  u256_shr1(x);
-}
-// Montgomery inverse (aR)^-1 -> a^-1 R: binary extended Euclid on the representative, then
-// one Montgomery product with R^3 ((aR)^-1 R^3 R^-1 = a^-1 R). a != 0.
-__device__ __noinline__ U256 fq_inv(const U256& am, const PairingConsts& k) {
-  U256 u = am, v, x1 = u256_zero(), x2 = u256_zero();
+  if (t) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v.w[i] = Bn254FqParams::P[i];
-  x1.w[0] = 1;
+    for (int l = 0; l < 7; ++l) a.w[l] = __builtin_amdgcn_alignbit(a.w[l + 1], a.w[l], (uint32_t)t);
+    a.w[7] >>= t;
+  }
+}
+__device__ __forceinline__ void u256_shl(U256& a, int t) {  // no bits lost (a 2^t < 2^256)
+  while (t >= 32) {
+#pragma unroll
+    for (int l = 7; l > 0; --l) a.w[l] = a.w[l - 1];
+    a.w[0] = 0;
+    t -= 32;
+  }
+  if (t) {
+#pragma unroll
+    for (int l = 7; l > 0; --l) a.w[l] = __builtin_amdgcn_alignbit(a.w[l], a.w[l - 1], (uint32_t)(32 - t));
+    a.w[0] <<= t;
+  }
+}
+// a - b mod 2^256; returns the borrow out
+__device__ __forceinline__ unsigned u256_subb(U256& d, const U256& a, const U256& b) {
+  unsigned c = 0;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) d.w[l] = __builtin_subc(a.w[l], b.w[l], c, &c);
+  return c;
+}
+__device__ __noinline__ U256 fq_inv(const U256& am, const PairingConsts&) {
   if (Fq::is_zero(am)) return u256_zero();  // no inverse (callers never pass 0)
-  // gcd(a, q) = 1: each round removes >= 1 bit from u or v, so <= 2 * 256 rounds; the cap
-  // only guards the exit
-  for (int round = 0; round < 1024 && !u256_is_one(u) && !u256_is_one(v); ++round) {
-    while (!(u.w[0] & 1)) { u256_shr1(u); fq_half(x1); }
-    while (!(v.w[0] & 1)) { u256_shr1(v); fq_half(x2); }
-    if (u256_geq(u, v)) {
-      u = u256_sub_raw(u, v);
-      x1 = Fq::sub(x1, x2);
-    } else {
-      v = u256_sub_raw(v, u);
-      x2 = Fq::sub(x2, x1);
+  U256 u, v = am, r = u256_zero(), s = u256_zero(), d;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) u.w[i] = Bn254FqParams::P[i];
+  s.w[0] = 1;
+  int k = u256_ctz(v);
+  u256_shr(v, k);
+  u256_shl(r, k);  // r = 0: a no-op, kept for the invariant's reading
+  for (int guard = 0; guard < 1024; ++guard) {  // u, v odd here; <= 2 x 254 bits to strip
+    if (u256_subb(d, u, v) == 0 && !u256_zero_p(d)) {  // u > v: u = (u - v) / 2^t, r += s, s <<= t
+      const int t = u256_ctz(d);
+      u256_shr(d, t);
+      u = d;
+      r = u256_add_raw(r, s);
+      u256_shl(s, t);
+      k += t;
+    } else {  // v = (v - u) / 2^t, s += r, r <<= t
+      u256_subb(d, v, u);
+      s = u256_add_raw(s, r);
+      if (u256_zero_p(d)) {  // u = v = 1: done
+        u256_shl(r, 1);
+        ++k;
+        break;
+      }
+      const int t = u256_ctz(d);
+      u256_shr(d, t);
+      v = d;
+      u256_shl(r, t);
+      k += t;
     }
   }
-  return Fq::mul(u256_is_one(u) ? x1 : x2, k.r3);
+  U256 q;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q.w[i] = Bn254FqParams::P[i];
+  r = Fq::reduce_once(r);  // r < 2q
+  u256_subb(d, q, r);      // x = q - r
+  return Fq::mul(d, g_inv2k[k & 511]);
 }
 __device__ __forceinline__ Fq2 f2_inv(const Fq2& a, const PairingConsts& k) {
   const U256 ni = fq_inv(Fq::add(Fq::mul(a.c0, a.c0), Fq::mul(a.c1, a.c1)), k);
@@ -177,19 +219,110 @@ __device__ __forceinline__ Fq2 f2_inv(const Fq2& a, const PairingConsts& k) {
 }
 
 // ---------------------------------------------------------------- lane-parallel Fq12 engine
-// A pairing product runs in one workgroup of PT threads (two waves on two SIMDs). Fq12
-// values live in LDS in the flat w-basis (g[k] = coefficient of w^k, an Fq2). On gfx950 a
-// lone wave's Fq product costs ~2250 cycles (136 v_mad_u64_u32 at ~16 cycles each,
-// scripts/ubench/pairing_lat.hip) whatever the lanes hold, so the engine puts ONE Fq product
-// on each lane per round: an Fq12 product is
-//   round 1  the 108 Fq products of 36 Karatsuba Fq2 products x_i y_j (one per lane),
-//   round 2  36 lanes recombine each Fq2 product (x xi where i + j >= 6: w^6 = xi),
-//   round 3  12 lanes sum the six Fq2 products of each output coefficient (component),
-// about one Fq-product latency plus a few additions, where a lane-per-Fq2-product form pays
-// three Fq products in sequence. A sparse line (w^0, w^1, w^3) is the same with 18 pairs.
+// A pairing product runs in one workgroup of PT threads (four waves on four SIMDs). Fq12
+// values live in LDS in the flat w-basis (g[k] = coefficient of w^k, an Fq2); a register
+// holds g[0..5] and, in slots 6..11, xi g[0..5]. On gfx950 a lone wave's Fq product costs
+// ~2250 cycles (136 v_mad_u64_u32 at ~16 cycles each, scripts/ubench/pairing_lat.hip) whatever
+// the lanes hold, so the engine puts ONE Fq product on each lane per round: an Fq12 product is
+//   round 1  the 108 Fq products of 36 Karatsuba Fq2 products x_i y_j, one per lane; where
+//            i + j >= 6 (w^6 = xi) the lane takes xi x_i from the register's second half, so
+//            no product is multiplied by xi afterwards;
+//   round 2  18 lanes (k, c) sum the Karatsuba parts t_c of the six products of output
+//            coefficient k, S_c, in 288-bit accumulators without reductions;
+//   round 3  lane k of wave (h, c) forms component c of g_k (h = 0) or of xi g_k (h = 1) as a
+//            small integer combination of S_0, S_1, S_2 and reduces it once,
+// where the form before round 5 (Karatsuba recombination and a product by xi per Fq2
+// product, then sums of reduced Fq2) paid ~10 reduced Fq additions in sequence (round 2 +
+// round 3: 4.2 k cycles; now ~2.4-3.2 k, scripts/ubench/r2lat.hip). A sparse line (w^0, w^1,
+// w^3) is the same with 18 pairs.
 // Every function is called by all PT threads and ends with a barrier; operands are LDS
-// Fq12 (6 Fq2) and may alias the result.
-constexpr int PT = 128;
+// Fq12 registers (12 Fq2) and may alias the result.
+constexpr int PT = 256;
+
+// Lazy sums: 9 x 32-bit limbs (< 2^288) through __builtin_addc / __builtin_subc carry chains
+// (v_add_co / v_addc with SGPR-pair carries; the compiler interleaves independent chains and
+// places the carry wait states).
+struct L9 {
+  uint32_t w[9];
+};
+__device__ __forceinline__ L9 l9_of(const U256& x) {
+  L9 r;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) r.w[l] = x.w[l];
+  r.w[8] = 0;
+  return r;
+}
+__device__ __forceinline__ void l9_add(L9& a, const U256& x) {
+  unsigned c = 0;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) a.w[l] = __builtin_addc(a.w[l], x.w[l], c, &c);
+  a.w[8] += c;
+}
+__device__ __forceinline__ void l9_add(L9& a, const L9& b) {
+  unsigned c = 0;
+#pragma unroll
+  for (int l = 0; l < 9; ++l) a.w[l] = __builtin_addc(a.w[l], b.w[l], c, &c);
+}
+__device__ __forceinline__ void l9_sub(L9& a, const L9& b) {  // requires a >= b
+  unsigned c = 0;
+#pragma unroll
+  for (int l = 0; l < 9; ++l) a.w[l] = __builtin_subc(a.w[l], b.w[l], c, &c);
+}
+template <int S>
+__device__ __forceinline__ L9 l9_shl(const L9& a) {  // a << S (no overflow for our bounds)
+  L9 r;
+  r.w[0] = a.w[0] << S;
+#pragma unroll
+  for (int l = 1; l < 9; ++l) r.w[l] = (a.w[l] << S) | (a.w[l - 1] >> (32 - S));
+  return r;
+}
+// K q in 9 limbs, compile time
+struct L9c {
+  uint32_t w[9];
+};
+constexpr L9c l9_kq(uint32_t K) {
+  L9c r{};
+  uint64_t c = 0;
+  for (int l = 0; l < 8; ++l) {
+    const uint64_t p = (uint64_t)K * Bn254FqParams::P[l] + c;
+    r.w[l] = (uint32_t)p;
+    c = p >> 32;
+  }
+  r.w[8] = (uint32_t)c;
+  return r;
+}
+template <uint32_t K>
+__device__ __forceinline__ void l9_add_kq(L9& a) {
+  constexpr L9c k = l9_kq(K);
+  unsigned c = 0;
+#pragma unroll
+  for (int l = 0; l < 9; ++l) a.w[l] = __builtin_addc(a.w[l], k.w[l], c, &c);
+}
+// x mod q for x < 2^262 (x < 340 q): d = floor(x / q) estimated from x's top 96 bits in double
+// (relative error < 2^-50, so x / q - est < 1e-12 for x < 340 q) minus a 1e-9 margin, so that
+// d is floor(x / q) or one less: x - d q < 2q, one conditional subtraction.
+__device__ __forceinline__ U256 l9_reduce(L9 x) {
+  const double top = ((double)x.w[8] * 18446744073709551616.0 + (double)x.w[7] * 4294967296.0) + (double)x.w[6];
+  const double est = top * (1.0 / 3486998266802970666.0) - 1e-9;  // q / 2^192 = 0x30644e72e131a029.b8...
+  const uint32_t d = est > 0.0 ? (uint32_t)est : 0u;
+  L9 m;
+  uint64_t c = 0;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) {
+    const uint64_t p = (uint64_t)d * Bn254FqParams::P[l] + c;
+    m.w[l] = (uint32_t)p;
+    c = p >> 32;
+  }
+  m.w[8] = (uint32_t)c;
+  l9_sub(x, m);
+  U256 r;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) r.w[l] = x.w[l];  // < 2q < 2^255: limb 8 is 0
+  return Fq::reduce_once(r);
+}
+__device__ __forceinline__ U256 kara_raw(const Fq2& a, int r) {
+  return u256_add_raw(r == 1 ? a.c1 : a.c0, r == 2 ? a.c1 : u256_zero());
+}
 
 // Miller-step slots: T = (X : Y : Z), the affine point added (xq, yq), the line's w^3
 // coefficient, temporaries from SL_T
@@ -225,14 +358,17 @@ struct PrepLine {
 };
 
 constexpr int LCHUNK = 2;  // pairs whose evaluated lines sit in LDS at once
+constexpr int NREG = 32;   // Fq12 registers (the final exponentiation's program names them)
+constexpr int LB = PT / 27;  // steps per batch of pair_line_products
 struct PL {
   U256 t[PT];          // round-1 Fq products
-  Fq2 pp[36];          // round-2 Fq2 products
-  Fq2 reg[16][6];      // Fq12 registers
+  L9 acc[2][6][3];     // round-2 sums (two products: w_mul_dual)
+  Fq2 pp[9 * LB];      // Fq2 products of pair_line_products
+  Fq2 reg[NREG][12];   // Fq12 registers: g[0..5], xi g[0..5]
   Fq2 sl[SL_N];        // Miller-step slots
   Fq2 Qa[3][2];        // Q, pi(Q), -pi^2(Q) affine
-  Fq2 frob1[6];        // lane-indexed constants (a lane-indexed kernel argument would be
-  U256 frob2[6];       // copied to scratch)
+  Fq2 frob1[12];       // lane-indexed constants: FROB1[k], xi FROB1[k] (a lane-indexed kernel
+  U256 frob2[6];       // argument would be copied to scratch)
   U256 px[LCHUNK], py[LCHUNK];
   int skip[LCHUNK];
   Fq2 le[NSTEP][LCHUNK][3];  // lines evaluated at P (w^0, w^1, w^3); two lines -> their product (w^0..w^4)
@@ -242,7 +378,9 @@ __device__ __forceinline__ void load_consts(const PairingConsts& k, PL& L, int t
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     if (tid == i) {
-      L.frob1[i] = Fq2{k.frob1[i][0], k.frob1[i][1]};
+      const Fq2 f{k.frob1[i][0], k.frob1[i][1]};
+      L.frob1[i] = f;
+      L.frob1[6 + i] = f2_mul_xi(f);
       L.frob2[i] = k.frob2[i];
     }
   }
@@ -270,131 +408,149 @@ struct WShape {
   __device__ __forceinline__ static int j(int jj) { return MODE == W_LINE ? line_j(jj) : jj; }
 };
 
-// dst = x * y
-template <int MODE>
-__device__ __forceinline__ void w_mul(Fq2* dst, const Fq2* x, const Fq2* y, PL& L, int tid) {
+// dst = x * y (x a register: its xi half feeds the wrapped products; y: NJ coefficients).
+// Karatsuba parts of x_i y_j: t0 = x0 y0, t1 = x1 y1, t2 = (x0 + x1)(y0 + y1), the product
+// (t0 - t1) + (t2 - t0 - t1) u and xi times it (10 t0 - 8 t1 - t2) + (9 t2 - 8 t0 - 10 t1) u.
+// Sums of at most six canonical t are < 6q, so the offsets 6q, 12q, 54q, 108q keep every
+// combination non-negative and below 162 q. The three rounds are split out so that two
+// independent products can share them (w_mul_dual).
+//
+// round 1 on `lane` < 3 NP: t[lane]; NEGY: y's odd coefficients negated (x conj(y)): the
+// product of a pair with odd j changes sign, so each of its three parts does
+template <int MODE, bool NEGY>
+__device__ __forceinline__ void wm_r1(const Fq2* x, const Fq2* y, U256* t, int lane) {
   using Sh = WShape<MODE>;
   constexpr int NJ = Sh::NJ, NP = 6 * NJ;
-  if (tid < 3 * NP) {
-    const int q = tid / 3, r = tid - 3 * q, i = q / NJ, jj = q - NJ * i;
-    L.t[tid] = Fq::mul(kara_operand(x[i], r), kara_operand(y[jj], r));
+  if (lane < 3 * NP) {
+    const int q = lane / 3, r = lane - 3 * q, i = q / NJ, jj = q - NJ * i, j = Sh::j(jj);
+    const Fq2& xa = x[i + (i + j >= 6 ? 6 : 0)];
+    U256 v = Fq::mul(kara_raw(xa, r), kara_raw(y[jj], r));
+    if (NEGY && (j & 1)) v = Fq::sub(u256_zero(), v);
+    t[lane] = v;
   }
-  bsync();
-  if (tid < NP) {
-    const int i = tid / NJ, jj = tid - NJ * i, j = Sh::j(jj);
-    Fq2 p = kara_combine(L.t[3 * tid], L.t[3 * tid + 1], L.t[3 * tid + 2]);
-    if (i + j >= 6) p = f2_mul_xi(p);
-    L.pp[tid] = p;
-  }
-  bsync();
-  if (tid < 12) {
-    const int k = tid >> 1, c = tid & 1;
-    U256 s[NJ];
+}
+// round 2 on `lane` < 18: S_c of output k, lane (k, c)
+template <int MODE>
+__device__ __forceinline__ void wm_r2(const U256* t, L9 (*acc)[3], int lane) {
+  using Sh = WShape<MODE>;
+  constexpr int NJ = Sh::NJ;
+  if (lane < 18) {
+    const int k = lane / 3, c = lane - 3 * k;
+    L9 s;
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
       const int j = Sh::j(jj);
       const int i = k - j < 0 ? k - j + 6 : k - j;
-      const Fq2& p = L.pp[i * NJ + jj];
-      s[jj] = c ? p.c1 : p.c0;
+      const U256 v = t[3 * (i * NJ + jj) + c];
+      if (jj == 0) s = l9_of(v);
+      else l9_add(s, v);
     }
-    U256 v;
-    if constexpr (NJ == 3) {
-      v = Fq::add(Fq::add(s[0], s[1]), s[2]);
-    } else if constexpr (NJ == 5) {
-      v = Fq::add(Fq::add(Fq::add(s[0], s[1]), Fq::add(s[2], s[3])), s[4]);
-    } else {
-      v = Fq::add(Fq::add(Fq::add(s[0], s[1]), Fq::add(s[2], s[3])), Fq::add(s[4], s[5]));
-    }
-    if (c) dst[k].c1 = v; else dst[k].c0 = v;
+    acc[k][c] = s;
+  }
+}
+// round 3 for output k < 6 in wave wv = (h, c): component c of g_k (h = 0) or of xi g_k (h = 1)
+__device__ __forceinline__ void wm_r3(Fq2* dst, L9 (*acc)[3], int wv, int k) {
+  L9 s[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s[c] = acc[k][c];
+  L9 v;
+  if (wv == 0) {  // t0 - t1
+    v = s[0];
+    l9_add_kq<6>(v);
+    l9_sub(v, s[1]);
+  } else if (wv == 1) {  // t2 - t0 - t1
+    v = s[2];
+    l9_add_kq<12>(v);
+    l9_sub(v, s[0]);
+    l9_sub(v, s[1]);
+  } else if (wv == 2) {  // 10 t0 - 8 t1 - t2
+    L9 f = l9_shl<2>(s[0]);
+    l9_add(f, s[0]);
+    v = l9_shl<1>(f);
+    l9_add_kq<54>(v);
+    l9_sub(v, l9_shl<3>(s[1]));
+    l9_sub(v, s[2]);
+  } else {  // 9 t2 - 8 t0 - 10 t1
+    v = l9_shl<3>(s[2]);
+    l9_add(v, s[2]);
+    l9_add_kq<108>(v);
+    L9 u = s[0];
+    l9_add(u, s[1]);
+    l9_sub(v, l9_shl<3>(u));
+    l9_sub(v, l9_shl<1>(s[1]));
+  }
+  const U256 r = l9_reduce(v);
+  Fq2& d = dst[k + (wv >> 1) * 6];
+  if (wv & 1) d.c1 = r; else d.c0 = r;
+}
+template <int MODE>
+__device__ __forceinline__ void w_mul(Fq2* dst, const Fq2* x, const Fq2* y, PL& L, int tid) {
+  wm_r1<MODE, false>(x, y, L.t, tid);
+  bsync();
+  wm_r2<MODE>(L.t, L.acc[0], tid);
+  bsync();
+  const int wv = tid >> 6, k = tid & 63;
+  if (k < 6) wm_r3(dst, L.acc[0], wv, k);
+  bsync();
+}
+// Two independent dense products in the same three rounds (216 of the 256 lanes in round 1):
+// dA = xA yA and dB = xB yB (NEGB: xB conj(yB)). Either destination may alias any operand:
+// round 1 reads every operand before round 3 writes.
+template <bool NEGB>
+__device__ __forceinline__ void w_mul_dual(Fq2* dA, const Fq2* xA, const Fq2* yA, Fq2* dB, const Fq2* xB, const Fq2* yB,
+                                           PL& L, int tid) {
+  if (tid < 128) wm_r1<W_DENSE, false>(xA, yA, L.t, tid);
+  else wm_r1<W_DENSE, NEGB>(xB, yB, L.t + 128, tid - 128);
+  bsync();
+  const int wv = tid >> 6, k = tid & 63;
+  if (wv == 0) wm_r2<W_DENSE>(L.t, L.acc[0], k);
+  else if (wv == 1) wm_r2<W_DENSE>(L.t + 128, L.acc[1], k);
+  bsync();
+  if ((k & 31) < 6) {  // lanes 0..5: product A, 32..37: product B (one code path)
+    const bool b = k >= 32;
+    wm_r3(b ? dB : dA, L.acc[b ? 1 : 0], wv, k & 31);
   }
   bsync();
 }
 
-// dst = x^2 for x in the cyclotomic subgroup (Granger-Scott): with s = w^3 (s^2 = xi),
-// A_m = g_m + g_(m+3) s in Fq4 = Fq2[s],
-//   x^2 = (3 A0^2 - 2 conj A0) + (3 s A2^2 + 2 conj A1) w + (3 A1^2 - 2 conj A2) w^2,
-// conj(y0 + y1 s) = y0 - y1 s (checked against the generic product in
-// tests/test_bn254_pairing_oracle.py). 21 Fq products in round 1 instead of 108.
-__device__ __forceinline__ void w_csqr(Fq2* dst, const Fq2* x, PL& L, int tid) {
-  if (tid < 21) {
-    // per A_m (y0 = x[m], y1 = x[m+3]): y0^2 = ((a0+a1)(a0-a1), 2 a0 a1), y1^2 likewise,
-    // y0 y1 by Karatsuba: operands lhs = L1 + L2, rhs = (R1 + R2) - R3
-    const int m = tid / 7, r = tid - 7 * m;
-    const Fq2 a = x[m], b = x[m + 3];
-    const U256 z = u256_zero();
-    U256 l1, l2 = z, r1, r2 = z, r3 = z;
-    switch (r) {
-      case 0: l1 = a.c0; l2 = a.c1; r1 = a.c0; r3 = a.c1; break;
-      case 1: l1 = a.c0; r1 = a.c1; break;
-      case 2: l1 = b.c0; l2 = b.c1; r1 = b.c0; r3 = b.c1; break;
-      case 3: l1 = b.c0; r1 = b.c1; break;
-      case 4: l1 = a.c0; r1 = b.c0; break;
-      case 5: l1 = a.c1; r1 = b.c1; break;
-      default: l1 = a.c0; l2 = a.c1; r1 = b.c0; r2 = b.c1; break;
-    }
-    L.t[tid] = Fq::mul(Fq::add(l1, l2), Fq::sub(Fq::add(r1, r2), r3));
-  }
-  bsync();
-  if (tid < 6) {
-    // A_m^2 = (y0^2 + xi y1^2) + 2 y0 y1 s: lane m -> the s^0 part, lane 3 + m -> the s part
-    // (s A2^2 needs xi times A2^2's s part): one xi product on every lane, no divergence in it
-    const int m = tid < 3 ? tid : tid - 3;
-    const U256* t = L.t + 7 * m;
-    const bool lo = tid < 3;
-    const Fq2 y0sq{t[0], Fq::add(t[1], t[1])};
-    const Fq2 u = lo ? Fq2{t[2], Fq::add(t[3], t[3])} : f2_dbl(kara_combine(t[4], t[5], t[6]));
-    const Fq2 xu = f2_mul_xi(u);
-    L.pp[tid] = lo ? f2_add(y0sq, xu) : (m == 2 ? xu : u);
-  }
-  bsync();
-  if (tid < 12) {
-    // output Fq2 k (flat w^k), component c: 3 S -/+ 2 g_k
-    //   k = 0: S = A0^2 s^0 (pp0), minus   k = 3: A0^2 s (pp3), plus
-    //   k = 1: S = xi (A2^2 s)  (pp5), plus k = 4: A2^2 s^0 (pp2), minus
-    //   k = 2: S = A1^2 s^0 (pp1), minus   k = 5: A1^2 s (pp4), plus
-    const int k = tid >> 1, c = tid & 1;
-    const int src[6] = {0, 5, 1, 3, 2, 4};
-    const Fq2& S = L.pp[src[k]];
-    const U256 sv = c ? S.c1 : S.c0;
-    const U256 g = c ? x[k].c1 : x[k].c0;
-    const U256 s3 = Fq::add(Fq::add(sv, sv), sv), g2 = Fq::add(g, g);
-    const bool minus = (k == 0 || k == 2 || k == 4);
-    const U256 v = minus ? Fq::sub(s3, g2) : Fq::add(s3, g2);
-    if (c) dst[k].c1 = v; else dst[k].c0 = v;
-  }
+// the xi half of a register from its first half (after a value was written by one lane)
+__device__ __forceinline__ void w_fill_xi(Fq2* d, int tid) {
+  if (tid < 6) d[6 + tid] = f2_mul_xi(d[tid]);
   bsync();
 }
-
 __device__ __forceinline__ void w_copy(Fq2* dst, const Fq2* x, int tid) {
-  if (tid < 6) dst[tid] = x[tid];
+  if (tid < 12) dst[tid] = x[tid];
   bsync();
 }
-// x^(q^6): w -> -w
+// x^(q^6): w -> -w (the xi half likewise)
 __device__ __forceinline__ void w_conj(Fq2* dst, const Fq2* x, int tid) {
-  if (tid < 6) dst[tid] = (tid & 1) ? f2_neg(x[tid]) : x[tid];
+  if (tid < 12) dst[tid] = (tid & 1) ? f2_neg(x[tid]) : x[tid];
   bsync();
 }
-// x^q: g_k -> conj(g_k) FROB1[k]; Fq-level: lane (k, role) computes one Karatsuba product
+// x^q: g_k -> conj(g_k) FROB1[k], and xi times it = conj(g_k) (xi FROB1[k]); lane (h, k, role)
+// computes one Karatsuba product
 __device__ __forceinline__ void w_frob1(Fq2* dst, const Fq2* x, PL& L, int tid) {
-  if (tid < 18) {
-    const int k = tid / 3, r = tid - 3 * k;
-    L.t[tid] = Fq::mul(kara_operand(f2_conj(x[k]), r), kara_operand(L.frob1[k], r));
+  if (tid < 36) {
+    const int q = tid / 3, r = tid - 3 * q, k = q % 6;
+    L.t[tid] = Fq::mul(kara_operand(f2_conj(x[k]), r), kara_operand(L.frob1[q], r));
   }
   bsync();
-  if (tid < 6) dst[tid] = kara_combine(L.t[3 * tid], L.t[3 * tid + 1], L.t[3 * tid + 2]);
+  if (tid < 12) dst[tid] = kara_combine(L.t[3 * tid], L.t[3 * tid + 1], L.t[3 * tid + 2]);
   bsync();
 }
-// x^(q^2): g_k -> g_k FROB2[k]
+// x^(q^2): g_k -> g_k FROB2[k] (FROB2 in Fq, so the xi half scales the same way)
 __device__ __forceinline__ void w_frob2(Fq2* dst, const Fq2* x, PL& L, int tid) {
-  if (tid < 12) {
-    const int k = tid >> 1;
-    const U256 v = Fq::mul((tid & 1) ? x[k].c1 : x[k].c0, L.frob2[k]);
-    if (tid & 1) dst[k].c1 = v; else dst[k].c0 = v;
+  if (tid < 24) {
+    const int e = tid >> 1;
+    const U256 v = Fq::mul((tid & 1) ? x[e].c1 : x[e].c0, L.frob2[e % 6]);
+    if (tid & 1) dst[e].c1 = v; else dst[e].c0 = v;
   }
   bsync();
 }
 __device__ __forceinline__ void w_one(Fq2* dst, const PairingConsts& k, int tid) {
-  if (tid < 6) dst[tid] = Fq2{tid == 0 ? k.one : u256_zero(), u256_zero()};
+  if (tid < 12) dst[tid] = Fq2{tid == 0 ? k.one : u256_zero(), u256_zero()};
+  bsync();
+  if (tid == 0) dst[6] = f2_mul_xi(dst[0]);
   bsync();
 }
 // In-place inverse of the Fq6 element n0 + n1 v + n2 v^2 held at flat slots 0, 2, 4 of n
@@ -417,25 +573,142 @@ __device__ __noinline__ void fq6_inv_flat(Fq2* n, const PairingConsts& k) {
 
 // The final exponentiation as a program over the LDS Fq12 registers, run by one
 // interpreter loop: one inlined copy of each primitive and no calls (a call would save and
-// restore the callee's VGPRs through scratch every time).
-enum : uint8_t { FE_MUL, FE_CSQR, FE_CONJ, FE_FROB1, FE_FROB2, FE_COPY, FE_INVN };
+// restore the callee's VGPRs through scratch every time). FE_DUAL runs two independent
+// products in one set of rounds (w_mul_dual): the program pairs them wherever the chain allows.
+enum : uint8_t { FE_MUL, FE_DUAL, FE_CONJ, FE_FROB1, FE_FROB2, FE_COPY, FE_INVN, FE_CSQR };
 struct FeOp {
-  uint8_t op, dst, a, b;
+  uint8_t op, dst, a, b;      // FE_MUL / FE_DUAL product A: dst = a b
+  uint8_t dst2, a2, b2, neg;  // FE_DUAL product B: dst2 = a2 b2 (neg: a2 conj(b2))
 };
 constexpr int FE_MAX = 320;
 struct FeProg {
   FeOp ops[FE_MAX];
-  int n;
+  int n, products;  // ops; product rounds (FE_MUL + FE_DUAL)
 };
-// registers: 0 f (in/out), 1 a = f^u, 2 b = f^u^2, 3 c = f^u^3, 4..11 temporaries, 12, 13
-// inverse, 14 conj of the base of a power by u
+struct FeMul {  // a product waiting for a slot
+  int d, a, b;
+};
+// Registers (all distinct, so that products of independent chains can share rounds):
+enum : int {
+  R_F, R_A, R_B, R_C, R_S,                     // f, a = f^u, b = a^u, c = b^u, a power's running square
+  R_E1, R_E2, R_E3, R_E4,                      // easy part
+  R_A2, R_A4, R_A6, R_A12, R_A18,              // a^2 .. a^18
+  R_B2, R_B4, R_B6, R_B12, R_B18, R_B24, R_B30,  // b^2 .. b^30
+  R_C2, R_C4, R_C36, R_F2, R_L2, R_X5, R_X4, R_T7, R_FQ1, R_FQ3, R_Y, R_COUNT
+};
+static_assert(R_COUNT <= NREG, "register file");
 constexpr FeProg make_fe_prog() {
   FeProg p{};
-  int n = 0;
-  auto op = [&](uint8_t o, int d, int a, int b) { p.ops[n++] = FeOp{o, (uint8_t)d, (uint8_t)a, (uint8_t)b}; };
+  int n = 0, np = 0;
+  auto op = [&](uint8_t o, int d, int a, int b) {
+    p.ops[n++] = FeOp{o, (uint8_t)d, (uint8_t)a, (uint8_t)b, 0, 0, 0, 0};
+  };
+  auto mul = [&](int d, int a, int b) { op(FE_MUL, d, a, b); ++np; };
+  auto dual = [&](int d, int a, int b, int d2, int a2, int b2, bool neg) {
+    p.ops[n++] = FeOp{FE_DUAL, (uint8_t)d, (uint8_t)a, (uint8_t)b, (uint8_t)d2, (uint8_t)a2, (uint8_t)b2, (uint8_t)neg};
+    ++np;
+  };
+  // d = x^u, right to left over the NAF of u (x^-1 = conj x in the cyclotomic subgroup): the
+  // running square S and the product d read the same S in each round, so the squaring and the
+  // multiplication share it; rounds without a multiplication take the next of `side` (a
+  // dependent chain of products on values ready before this power starts), in order.
+  auto powu = [&](int d, int x, const FeMul* side, int ns) {
+    int8_t naf[66] = {};
+    int len = 0;
+    for (uint64_t e = K_BN_U; e; e >>= 1) {
+      int8_t z = 0;
+      if (e & 1) {
+        z = (int8_t)(2 - (int)(e & 3));
+        e = z > 0 ? e - 1 : e + 1;
+      }
+      naf[len++] = z;
+    }
+    int si = 0;
+    bool have = false;
+    op(FE_COPY, R_S, x, 0);
+    for (int i = 0; i < len; ++i) {
+      const int z = naf[i];
+      if (i == len - 1) {  // the top digit (+1): d = d S
+        if (si < ns) {
+          dual(d, d, R_S, side[si].d, side[si].a, side[si].b, false);
+          ++si;
+        } else {
+          mul(d, d, R_S);
+        }
+        break;
+      }
+      const bool m = z != 0 && have;
+      if (z != 0 && !have) {  // the lowest digit: d = S^z, no product
+        op(z > 0 ? FE_COPY : FE_CONJ, d, R_S, 0);
+        have = true;
+      }
+      if (m) {
+        dual(R_S, R_S, R_S, d, d, R_S, z < 0);
+      } else if (si < ns) {
+        dual(R_S, R_S, R_S, side[si].d, side[si].a, side[si].b, false);
+        ++si;
+      } else {
+        mul(R_S, R_S, R_S);
+      }
+    }
+    for (; si < ns; ++si) mul(side[si].d, side[si].a, side[si].b);  // (never: enough free rounds)
+  };
+  // easy part: f^(q^6-1) = conj(f)^2 / (f conj(f)), then ^(q^2+1)
+  op(FE_CONJ, R_E1, R_F, 0);
+  dual(R_E2, R_F, R_E1, R_E3, R_E1, R_E1, false);  // N = f conj(f) (in Fq6); conj(f)^2
+  op(FE_INVN, R_E2, 0, 0);
+  mul(R_F, R_E3, R_E2);    // f^(q^6-1)
+  op(FE_FROB2, R_E4, R_F, 0);
+  mul(R_F, R_E4, R_F);     // f^((q^6-1)(q^2+1)): the hard part's base, in the cyclotomic subgroup
+  // hard part: f^(l0 + l1 q + l2 q^2 + q^3) (see file header)
+  op(FE_FROB1, R_FQ1, R_F, 0);
+  op(FE_FROB2, R_FQ3, R_FQ1, 0);  // f^(q^3)
+  const FeMul s1[] = {{R_F2, R_F, R_F}};
+  powu(R_A, R_F, s1, 1);
+  const FeMul s2[] = {{R_A2, R_A, R_A}, {R_A4, R_A2, R_A2}, {R_A6, R_A4, R_A2}, {R_A12, R_A6, R_A6}, {R_A18, R_A12, R_A6}};
+  powu(R_B, R_A, s2, 5);
+  const FeMul s3[] = {{R_B2, R_B, R_B},     {R_B4, R_B2, R_B2},    {R_B6, R_B4, R_B2},    {R_B12, R_B6, R_B6},
+                      {R_B18, R_B12, R_B6}, {R_B24, R_B12, R_B12}, {R_B30, R_B24, R_B6}, {R_L2, R_B6, R_F}};
+  powu(R_C, R_B, s3, 8);
+  // c^36 = c^32 c^4, beside it Y = frob2(f^l2) f^(q^3)
+  op(FE_FROB2, R_T7, R_L2, 0);
+  dual(R_C2, R_C, R_C, R_Y, R_T7, R_FQ3, false);
+  mul(R_C4, R_C2, R_C2);
+  mul(R_C2, R_C4, R_C4);  // c^8
+  mul(R_C2, R_C2, R_C2);  // c^16
+  mul(R_C2, R_C2, R_C2);  // c^32
+  mul(R_C36, R_C2, R_C4);
+  // f^l1 = conj(c^36 b^18 a^12) f, f^l0 = conj(c^36 b^30 a^18 f^2)
+  dual(R_X5, R_C36, R_B18, R_X4, R_C36, R_B30, false);
+  dual(R_X5, R_X5, R_A12, R_X4, R_X4, R_A18, false);
+  op(FE_CONJ, R_X5, R_X5, 0);
+  dual(R_X5, R_X5, R_F, R_X4, R_X4, R_F2, false);
+  op(FE_CONJ, R_X4, R_X4, 0);
+  op(FE_FROB1, R_T7, R_X5, 0);
+  mul(R_X4, R_X4, R_T7);  // f^l0 frob1(f^l1)
+  mul(R_F, R_X4, R_Y);    // times frob2(f^l2) f^(q^3)
+  p.n = n;
+  p.products = np;
+  return p;
+}
+__constant__ FeProg c_fe_prog = make_fe_prog();
+static_assert(make_fe_prog().n <= FE_MAX, "program size");
+
+// The lane engine's program: the same chain as one product per step, left to right over the
+// NAF of u, squarings in the hard part marked FE_CSQR (Granger-Scott per lane: 21 Fq products
+// instead of 36), 16 registers (the lane engine keeps them in scratch): 0 f (in/out),
+// 1 a = f^u, 2 b = f^u^2, 3 c = f^u^3, 4..11 temporaries, 12, 13 inverse, 14 conj of the base
+// of a power by u
+constexpr FeProg make_fe_seq() {
+  FeProg p{};
+  int n = 0, np = 0;
+  auto op = [&](uint8_t o, int d, int a, int b) {
+    p.ops[n++] = FeOp{o, (uint8_t)d, (uint8_t)a, (uint8_t)b, 0, 0, 0, 0};
+    if (o == FE_MUL || o == FE_CSQR) ++np;
+  };
   auto mul = [&](int d, int a, int b) { op(FE_MUL, d, a, b); };
-  auto sqr = [&](int d, int a) { op(FE_CSQR, d, a, 0); };  // hard part: cyclotomic subgroup
-  auto powu = [&](int d, int x) {  // d = x^u by the NAF of u (x^-1 = conj x in the subgroup)
+  auto sqr = [&](int d, int a) { op(FE_CSQR, d, a, 0); };
+  auto powu = [&](int d, int x) {
     int8_t naf[66] = {};
     int len = 0;
     for (uint64_t e = K_BN_U; e; e >>= 1) {
@@ -454,7 +727,6 @@ constexpr FeProg make_fe_prog() {
       if (naf[i] == -1) mul(d, d, 14);
     }
   };
-  // easy part: f^(q^6-1) = conj(f) / f (f^-1 = conj(f) * (f conj(f))^-1), then ^(q^2+1)
   op(FE_CONJ, 12, 0, 0);
   mul(13, 0, 12);
   op(FE_INVN, 13, 0, 0);
@@ -462,7 +734,6 @@ constexpr FeProg make_fe_prog() {
   mul(0, 12, 4);           // conj(f) f^-1
   op(FE_FROB2, 4, 0, 0);
   mul(0, 4, 0);
-  // hard part: l0 + l1 q + l2 q^2 + q^3 (see file header)
   powu(1, 0);
   powu(2, 1);
   powu(3, 2);
@@ -481,10 +752,12 @@ constexpr FeProg make_fe_prog() {
   op(FE_FROB2, 7, 6, 0); mul(4, 4, 7);
   op(FE_FROB1, 7, 0, 0); op(FE_FROB2, 8, 7, 0); mul(0, 4, 8);
   p.n = n;
+  p.products = np;
   return p;
 }
-__constant__ FeProg c_fe_prog = make_fe_prog();
-static_assert(make_fe_prog().n <= FE_MAX, "program size");
+constexpr int FE_SEQ_REGS = 16;
+__constant__ FeProg c_fe_seq = make_fe_seq();
+static_assert(make_fe_seq().n <= FE_MAX, "program size");
 
 // result = f^((q^12-1)/r), f in L.reg[0]; result in L.reg[0]
 __device__ __forceinline__ void final_exp_w(const PairingConsts& k, PL& L, int tid) {
@@ -495,7 +768,10 @@ __device__ __forceinline__ void final_exp_w(const PairingConsts& k, PL& L, int t
     const Fq2* a = L.reg[o.a];
     switch (o.op) {
       case FE_MUL: w_mul<W_DENSE>(d, a, L.reg[o.b], L, tid); break;
-      case FE_CSQR: w_mul<W_DENSE>(d, a, a, L, tid); break;  // (w_csqr measured slower: DESIGN 3.6)
+      case FE_DUAL:
+        if (o.neg) w_mul_dual<true>(d, a, L.reg[o.b], L.reg[o.dst2], L.reg[o.a2], L.reg[o.b2], L, tid);
+        else w_mul_dual<false>(d, a, L.reg[o.b], L.reg[o.dst2], L.reg[o.a2], L.reg[o.b2], L, tid);
+        break;
       case FE_CONJ: w_conj(d, a, tid); break;
       case FE_FROB1: w_frob1(d, a, L, tid); break;
       case FE_FROB2: w_frob2(d, a, L, tid); break;
@@ -503,6 +779,7 @@ __device__ __forceinline__ void final_exp_w(const PairingConsts& k, PL& L, int t
       default:  // FE_INVN
         if (tid == 0) fq6_inv_flat(d, k);
         bsync();
+        w_fill_xi(d, tid);
         break;
     }
   }
@@ -706,7 +983,6 @@ __device__ __forceinline__ void eval_lines(const uint64_t* g1, const PrepLine* l
 // path: all steps are independent): l m = a0 b0 + xi a3 b3 + (a0 b1 + a1 b0) w + a1 b1 w^2
 // + (a0 b3 + a3 b0) w^3 + (a1 b3 + a3 b1) w^4, written to le[st][0][0..2], le[st][1][0..1]
 // (the flat w^0..w^4 of a W_FIVE operand). LB steps per batch of three rounds.
-constexpr int LB = PT / 27;
 __device__ __forceinline__ void pair_line_products(PL& L, int tid) {
   // the 9 products (index into l, index into m) and their output coefficient
   constexpr int8_t PA[9] = {0, 2, 0, 1, 1, 0, 2, 1, 2}, PB[9] = {0, 2, 1, 0, 1, 2, 0, 2, 1};
@@ -754,7 +1030,7 @@ __global__ void __launch_bounds__(PT) pairing_product_kernel(const uint64_t* g1,
   const size_t b1 = b0 + per < n ? b0 + per : n;
   load_consts(k, L, tid);
   Fq2* f = L.reg[0];
-  Fq2* F = L.reg[15];
+  Fq2* F = L.reg[NREG - 1];
   for (size_t c = b0; c < b1; c += LCHUNK) {
     const int m = (int)(b1 - c < (size_t)LCHUNK ? b1 - c : (size_t)LCHUNK);
     eval_lines(g1, lines, qinf, c, m, k, L, tid);
@@ -854,7 +1130,7 @@ __device__ __forceinline__ Fq12 f12_frob2(const Fq12& a, const PairingConsts& k)
   return {{f2_muls(a.c0.c0, k.frob2[0]), f2_muls(a.c0.c1, k.frob2[2]), f2_muls(a.c0.c2, k.frob2[4])},
           {f2_muls(a.c1.c0, k.frob2[1]), f2_muls(a.c1.c1, k.frob2[3]), f2_muls(a.c1.c2, k.frob2[5])}};
 }
-// Granger-Scott squaring in the cyclotomic subgroup (the workgroup engine's w_csqr, per lane):
+// Granger-Scott squaring in the cyclotomic subgroup (per lane):
 // A_m = g_m + g_(m+3) s (s = w^3, s^2 = xi), A_m^2 = (a^2 + xi b^2) + 2 a b s; flat outputs
 // 3 S -/+ 2 g_k
 __device__ __noinline__ Fq12 f12_csqr(const Fq12& x) {
@@ -888,8 +1164,8 @@ __device__ __forceinline__ Fq6 f6_inv(const Fq6& n, const PairingConsts& k) {
 // (the value is in the cyclotomic subgroup there, so they are the same field elements)
 __device__ __noinline__ void f12_final_exp(Fq12* R, const PairingConsts& k) {
   const Fq2 z{u256_zero(), u256_zero()};
-  for (int pc = 0; pc < c_fe_prog.n; ++pc) {
-    const FeOp o = c_fe_prog.ops[pc];
+  for (int pc = 0; pc < c_fe_seq.n; ++pc) {
+    const FeOp o = c_fe_seq.ops[pc];
     const Fq12 a = R[o.op == FE_INVN ? o.dst : o.a];
     Fq12 d;
     switch (o.op) {
@@ -957,7 +1233,7 @@ __global__ void __launch_bounds__(64) pairing_lane_kernel(const uint64_t* g1, co
     }
     f = f12_mul_line(f, f2_muls(la, yp), f2_muls(lb, xp), lc);
   }
-  Fq12 R[16];
+  Fq12 R[FE_SEQ_REGS];
   R[0] = f;
   f12_final_exp(R, k);
   f = R[0];
@@ -1033,6 +1309,42 @@ static PairingConsts make_consts() {
   return k;
 }
 
+// g_inv2k on `device` (once per device): 2^-k R^3 mod q for k < 512, plain, from K_R3 and
+// Montgomery products by 2^-1 (the host's Fq::mul)
+static int ensure_inv2k(int device) {
+  static std::mutex mu;
+  static bool done[256];
+  std::lock_guard<std::mutex> g(mu);
+  if (device < 0 || device >= 256) return fail(1, "device index out of range");
+  if (done[device]) return 0;
+  U256 inv2{};  // (q + 1) / 2
+  {
+    uint64_t c = 1;
+    U256 q1;
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t t = (uint64_t)Bn254FqParams::P[i] + c;
+      q1.w[i] = (uint32_t)t;
+      c = t >> 32;
+    }
+    for (int i = 0; i < 8; ++i) inv2.w[i] = (q1.w[i] >> 1) | (i < 7 ? (q1.w[i + 1] << 31) : 0);
+  }
+  const U256 inv2m = Fq::to_mont(inv2);
+  std::vector<U256> t(512);
+  U256 c = u256_from_u64(K_R3);
+  for (int k = 0; k < 512; ++k) {
+    t[k] = c;
+    c = Fq::mul(c, inv2m);  // c 2^-1 R R^-1
+  }
+  int cur = 0;
+  PBF_HIP(hipGetDevice(&cur));
+  PBF_HIP(hipSetDevice(device));
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_inv2k), t.data(), t.size() * sizeof(U256));
+  PBF_HIP(hipSetDevice(cur));
+  if (e != hipSuccess) return fail(PBF_EDEVICE, "hipMemcpyToSymbol(g_inv2k) failed");
+  done[device] = true;
+  return 0;
+}
+
 // canonical-input validation on the host (x, y < q for every coordinate)
 static bool canonical_fq(const uint64_t* l) {
   static const uint64_t QL[4] = {0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
@@ -1071,6 +1383,8 @@ static int prep_lines(pbf_ctx* ctx, const uint64_t* d_g2, size_t n, hipStream_t 
 // pair (the latency form)
 static int pairing_values(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_g2, size_t n, uint64_t* d_out,
                           hipStream_t s) {
+  int rc = ensure_inv2k(ctx->device);
+  if (rc) return rc;
   const PairingConsts k = make_consts();
   const char* lane_env = getenv("PBF_PAIR_LANE");  // A/B: 1 forces the lane engine, 0 the workgroup one
   const bool lane = lane_env ? lane_env[0] == '1' : (n >= PAIR_LANE_MIN && !getenv("PBF_PAIR_WG"));
@@ -1081,7 +1395,7 @@ static int pairing_values(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_
   }
   PrepLine* lines;
   uint8_t* qinf;
-  int rc = prep_lines(ctx, d_g2, n, s, k, &lines, &qinf);
+  rc = prep_lines(ctx, d_g2, n, s, k, &lines, &qinf);
   if (rc) return rc;
   hipLaunchKernelGGL(pairing_product_kernel, dim3((uint32_t)n), dim3(PT), 0, s, d_g1, (const PrepLine*)lines,
                      (const uint8_t*)qinf, n, 1u, d_out, (int*)nullptr, k);
@@ -1138,6 +1452,7 @@ int pbf::pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_
   DevBuf &b1 = ctx->buf("pc.g1"), &b2 = ctx->buf("pc.g2"), &b3 = ctx->buf("pc.ok");
   DevBuf &cl = ctx->buf("pc.lines"), &cq = ctx->buf("pc.qinf");
   if ((rc = b1.ensure(n * 64)) || (rc = b2.ensure(n * 128)) || (rc = b3.ensure(64))) return rc;
+  if ((rc = ensure_inv2k(ctx->device))) return rc;
   const PairingConsts k = make_consts();
   auto& key = ctx->pair_g2_key;
   const bool hit = key.size() == 16 * n && memcmp(key.data(), g2, n * 128) == 0 && cl.p && cq.p;
@@ -1170,6 +1485,7 @@ extern "C" int pbf_g2_bn254_mul(pbf_ctx* ctx, const uint64_t* pts, const uint64_
   if (!ctx || (n && (!pts || !scalars || !out))) return fail(1, "null argument");
   if (n == 0) return 0;
   int rc = check_coords(pts, 4 * n);
+  if (!rc) rc = ensure_inv2k(ctx->device);
   if (rc) return rc;
   hipStream_t s = ctx->host_stream();
   if ((rc = ctx->io0.ensure(n * 128)) || (rc = ctx->io1.ensure(n * 32)) || (rc = ctx->io2.ensure(n * 128))) return rc;

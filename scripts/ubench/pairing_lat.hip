@@ -6,35 +6,35 @@
 
 using namespace pbf;
 
-// the three rounds of w_mul<false> separately
-__device__ __forceinline__ void r1(const Fq2* x, const Fq2* y, PL& L, int tid) {
+// the two rounds of w_mul<W_DENSE> separately (copies of its halves)
+__device__ __forceinline__ void r1_dense(const Fq2* x, const Fq2* y, PL& L, int tid) {
   if (tid < 108) {
     const int q = tid / 3, r = tid - 3 * q, i = q / 6, jj = q - 6 * i;
-    L.t[tid] = Fq::mul(kara_operand(x[i], r), kara_operand(y[jj], r));
+    const Fq2& xa = x[i + (i + jj >= 6 ? 6 : 0)];
+    L.t[tid] = Fq::mul(kara_raw(xa, r), kara_raw(y[jj], r));
   }
   bsync();
 }
-__device__ __forceinline__ void r2(PL& L, int tid) {
-  if (tid < 36) {
-    const int i = tid / 6, j = tid - 6 * i;
-    Fq2 p = kara_combine(L.t[3 * tid], L.t[3 * tid + 1], L.t[3 * tid + 2]);
-    if (i + j >= 6) p = f2_mul_xi(p);
-    L.pp[tid] = p;
-  }
-  bsync();
-}
-__device__ __forceinline__ void r3(Fq2* dst, PL& L, int tid) {
-  if (tid < 12) {
-    const int k = tid >> 1, c = tid & 1;
-    U256 s[6];
+__device__ __forceinline__ void r2_dense(Fq2* dst, PL& L, int tid) {
+  const int wv = tid >> 6, k = tid & 63;
+  if (k < 6) {
+    L9 s[3];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int i = k - j < 0 ? k - j + 6 : k - j;
-      const Fq2& p = L.pp[i * 6 + j];
-      s[j] = c ? p.c1 : p.c0;
+    for (int jj = 0; jj < 6; ++jj) {
+      const int i = k - jj < 0 ? k - jj + 6 : k - jj;
+      const U256* t = L.t + 3 * (i * 6 + jj);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (jj == 0) s[c] = l9_of(t[c]);
+        else l9_add(s[c], t[c]);
+      }
     }
-    const U256 v = Fq::add(Fq::add(Fq::add(s[0], s[1]), Fq::add(s[2], s[3])), Fq::add(s[4], s[5]));
-    if (c) dst[k].c1 = v; else dst[k].c0 = v;
+    L9 v = s[wv & 1];
+    l9_add_kq<108>(v);
+    l9_sub(v, s[2]);
+    const U256 r = l9_reduce(v);
+    Fq2& d = dst[k + (wv >> 1) * 6];
+    if (wv & 1) d.c1 = r; else d.c0 = r;
   }
   bsync();
 }
@@ -45,25 +45,45 @@ __global__ void __launch_bounds__(PT) k_lat(int what, int iters, const uint64_t*
   load_consts(k, L, lane);
   U256 x = Fq::to_mont(u256_from_u64(seed)), y = Fq::to_mont(u256_from_u64(seed + 4));
   Fq2 a{x, y}, b{y, x};
-  if (lane < 6) {
+  if (lane < 12) {
     L.reg[0][lane] = Fq2{x, y};
     L.reg[1][lane] = Fq2{y, x};
+    L.reg[2][lane] = Fq2{y, y};
   }
-  if (lane < 32) L.sl[lane] = Fq2{x, y};
+  for (int e = lane; e < NSTEP * LCHUNK * 3; e += PT) (&L.le[0][0][0])[e] = Fq2{x, y};
+  if (lane < 26) L.sl[lane] = Fq2{x, y};
   __syncthreads();
   uint64_t t0 = clock64(), w0 = wall_clock64();
   switch (what) {
     case 0: for (int i = 0; i < iters; ++i) x = Fq::mul(x, y); break;
     case 1: for (int i = 0; i < iters; ++i) a = f2_mul(a, b); break;
-    case 2: for (int i = 0; i < iters; ++i) w_mul<false>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
-    case 3: for (int i = 0; i < iters; ++i) w_csqr(L.reg[0], L.reg[0], L, lane); break;
-    case 4: for (int i = 0; i < iters; ++i) w_mul<true>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
+    case 2: for (int i = 0; i < iters; ++i) w_mul<W_DENSE>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
+    case 3: for (int i = 0; i < iters; ++i) w_mul<W_FIVE>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
+    case 4: for (int i = 0; i < iters; ++i) w_mul<W_LINE>(L.reg[0], L.reg[0], L.reg[1], L, lane); break;
     case 5: for (int i = 0; i < iters; ++i) x = Fq::add(x, y); break;
-    case 9: for (int i = 0; i < iters; ++i) r1(L.reg[0], L.reg[1], L, lane); break;
-    case 10: for (int i = 0; i < iters; ++i) r2(L, lane); break;
-    case 11: for (int i = 0; i < iters; ++i) r3(L.reg[0], L, lane); break;
+    case 9: for (int i = 0; i < iters; ++i) { if (lane == 0) fq6_inv_flat(L.reg[2], k); bsync(); } break;
+    case 10: for (int i = 0; i < iters; ++i) final_exp_w(k, L, lane); break;
+    case 11: for (int i = 0; i < iters; ++i) pair_line_products(L, lane); break;
     case 12: for (int i = 0; i < iters; ++i) bsync(); break;
     case 13: for (int i = 0; i < iters; ++i) { if (lane < 64) x = Fq::mul(x, y); bsync(); } break;
+    case 14: for (int i = 0; i < iters; ++i) w_frob1(L.reg[0], L.reg[0], L, lane); break;
+    case 16: for (int i = 0; i < iters; ++i) { x = Fq::mul(x, y); bsync(); } break;
+    case 17: for (int i = 0; i < iters; ++i) { if (lane < 128) x = Fq::mul(x, y); bsync(); } break;
+    case 18: for (int i = 0; i < iters; ++i) r1_dense(L.reg[0], L.reg[1], L, lane); break;
+    case 19: for (int i = 0; i < iters; ++i) r2_dense(L.reg[0], L, lane); break;
+    case 20: {  // the waves' hardware ids: SIMD of each wave (HW_ID bits 5:4 on gfx9)
+      uint32_t hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      if ((lane & 63) == 0) L.t[lane >> 6].w[0] = hw;
+      bsync();
+      if (lane == 0) x.w[0] = (L.t[0].w[0] >> 4 & 3) | (L.t[1].w[0] >> 4 & 3) << 4 | (L.t[2].w[0] >> 4 & 3) << 8 | (L.t[3].w[0] >> 4 & 3) << 12;
+      break;
+    }
+    case 15: {
+      L9 v = l9_of(x);
+      for (int i = 0; i < iters; ++i) { l9_add_kq<100>(v); x = l9_reduce(v); v = l9_of(x); }
+      break;
+    }
     case 6: {  // one dependent v_mad_u64_u32 chain
       uint64_t acc = x.w[0];
       for (int i = 0; i < iters; ++i) acc = (uint64_t)(uint32_t)acc * y.w[1] + (acc >> 7);
@@ -92,7 +112,7 @@ __global__ void __launch_bounds__(PT) k_lat(int what, int iters, const uint64_t*
   if (lane == 0) {
     out[0] = t1 - t0;
     out[1] = w1 - w0;
-    out[2] = x.w[0] ^ a.c0.w[0] ^ L.reg[0][0].c0.w[0];
+    out[2] = what == 20 ? x.w[0] : (x.w[0] ^ a.c0.w[0] ^ L.reg[0][0].c0.w[0]);
   }
 }
 
@@ -116,9 +136,12 @@ int main() {
   hipMemcpy(d_seed, seed, 64, hipMemcpyHostToDevice);
   int wclk = 0;
   hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, 0);  // kHz
-  const char* names[] = {"fq_mul", "fq2_mul", "fq12_mul(lanes)", "fq12_cyc_sqr", "fq12_mul_line", "fq_add", "mad_u64_dep", "mad_u64_x4", "mul_add_u32_dep", "w_mul round1", "w_mul round2", "w_mul round3", "barrier", "fq_mul+barrier"};
-  const int iters[] = {4096, 2048, 256, 256, 256, 4096, 65536, 65536, 65536, 256, 256, 256, 4096, 1024};
-  for (int w = 0; w < 14; ++w) {
+  const char* names[] = {"fq_mul", "fq2_mul", "w_mul dense", "w_mul five", "w_mul line", "fq_add", "mad_u64_dep",
+                         "mad_u64_x4", "mul_add_u32_dep", "fq6_inv_flat", "final_exp_w", "pair_line_products",
+                         "barrier", "fq_mul+barrier", "w_frob1", "l9_reduce", "fq_mul x4 waves", "fq_mul x2 waves",
+                         "w_mul round1", "w_mul round2"};
+  const int iters[] = {4096, 2048, 256, 256, 256, 4096, 65536, 65536, 65536, 16, 2, 8, 4096, 1024, 256, 1024, 1024, 1024, 256, 256};
+  for (int w = 0; w < 20; ++w) {
     for (int rep = 0; rep < 2; ++rep) {  // first launch warms the code
       hipLaunchKernelGGL(k_lat, dim3(1), dim3(PT), 0, 0, w, iters[w], d_seed, d_out, make_consts());
       hipMemcpy(h, d_out, 24, hipMemcpyDeviceToHost);
@@ -126,6 +149,9 @@ int main() {
     printf("%-18s %10.1f cycles  %8.3f us   per op\n", names[w], (double)h[0] / iters[w],
            (double)h[1] / iters[w] * 1e3 / wclk);
   }
+  hipLaunchKernelGGL(k_lat, dim3(1), dim3(PT), 0, 0, 20, 1, d_seed, d_out, make_consts());
+  hipMemcpy(h, d_out, 24, hipMemcpyDeviceToHost);
+  printf("SIMD of waves 0..3 (4 bits each): %04llx\n", (unsigned long long)(h[2] & 0xffff));
   {
     const int blocks = 256 * 8, iters = 256;  // 8 workgroups (32 waves) per CU
     hipEvent_t e0, e1;
