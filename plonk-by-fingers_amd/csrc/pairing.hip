@@ -320,6 +320,34 @@ __device__ __forceinline__ U256 l9_reduce(L9 x) {
   for (int l = 0; l < 8; ++l) r.w[l] = x.w[l];  // < 2q < 2^255: limb 8 is 0
   return Fq::reduce_once(r);
 }
+// 16-byte LDS accesses (ds_read_b128 / ds_write_b128: PL is 16-byte aligned and every member
+// a multiple of 16 bytes; U256's own alignment is 4, so the compiler would split them)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ U256 ld16_u256(const U256* p) {
+  const u32x4* v = (const u32x4*)__builtin_assume_aligned(p, 16);
+  const u32x4 a = v[0], b = v[1];
+  return U256{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+}
+__device__ __forceinline__ void st16_u256(U256* p, const U256& x) {
+  u32x4* v = (u32x4*)__builtin_assume_aligned(p, 16);
+  v[0] = u32x4{x.w[0], x.w[1], x.w[2], x.w[3]};
+  v[1] = u32x4{x.w[4], x.w[5], x.w[6], x.w[7]};
+}
+__device__ __forceinline__ Fq2 ld16_fq2(const Fq2* p) { return Fq2{ld16_u256(&p->c0), ld16_u256(&p->c1)}; }
+struct alignas(16) L9s {  // an L9 in LDS, padded to 48 bytes
+  uint32_t w[12];
+};
+__device__ __forceinline__ void st16_l9(L9s* p, const L9& x) {
+  u32x4* v = (u32x4*)p;
+  v[0] = u32x4{x.w[0], x.w[1], x.w[2], x.w[3]};
+  v[1] = u32x4{x.w[4], x.w[5], x.w[6], x.w[7]};
+  v[2] = u32x4{x.w[8], 0u, 0u, 0u};
+}
+__device__ __forceinline__ L9 ld16_l9(const L9s* p) {
+  const u32x4* v = (const u32x4*)p;
+  const u32x4 a = v[0], b = v[1], c = v[2];
+  return L9{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x}};
+}
 __device__ __forceinline__ U256 kara_raw(const Fq2& a, int r) {
   return u256_add_raw(r == 1 ? a.c1 : a.c0, r == 2 ? a.c1 : u256_zero());
 }
@@ -360,9 +388,9 @@ struct PrepLine {
 constexpr int LCHUNK = 2;  // pairs whose evaluated lines sit in LDS at once
 constexpr int NREG = 32;   // Fq12 registers (the final exponentiation's program names them)
 constexpr int LB = PT / 27;  // steps per batch of pair_line_products
-struct PL {
+struct alignas(16) PL {
   U256 t[PT];          // round-1 Fq products
-  L9 acc[2][6][3];     // round-2 sums (two products: w_mul_dual)
+  L9s acc[2][6][3];    // round-2 sums (two products: w_mul_dual)
   Fq2 pp[9 * LB];      // Fq2 products of pair_line_products
   Fq2 reg[NREG][12];   // Fq12 registers: g[0..5], xi g[0..5]
   Fq2 sl[SL_N];        // Miller-step slots
@@ -370,8 +398,8 @@ struct PL {
   Fq2 frob1[12];       // lane-indexed constants: FROB1[k], xi FROB1[k] (a lane-indexed kernel
   U256 frob2[6];       // argument would be copied to scratch)
   U256 px[LCHUNK], py[LCHUNK];
-  int skip[LCHUNK];
   Fq2 le[NSTEP][LCHUNK][3];  // lines evaluated at P (w^0, w^1, w^3); two lines -> their product (w^0..w^4)
+  int skip[LCHUNK];
 };
 
 __device__ __forceinline__ void load_consts(const PairingConsts& k, PL& L, int tid) {
@@ -423,15 +451,15 @@ __device__ __forceinline__ void wm_r1(const Fq2* x, const Fq2* y, U256* t, int l
   constexpr int NJ = Sh::NJ, NP = 6 * NJ;
   if (lane < 3 * NP) {
     const int q = lane / 3, r = lane - 3 * q, i = q / NJ, jj = q - NJ * i, j = Sh::j(jj);
-    const Fq2& xa = x[i + (i + j >= 6 ? 6 : 0)];
-    U256 v = Fq::mul(kara_raw(xa, r), kara_raw(y[jj], r));
+    const Fq2 xa = ld16_fq2(x + i + (i + j >= 6 ? 6 : 0)), ya = ld16_fq2(y + jj);
+    U256 v = Fq::mul(kara_raw(xa, r), kara_raw(ya, r));
     if (NEGY && (j & 1)) v = Fq::sub(u256_zero(), v);
-    t[lane] = v;
+    st16_u256(t + lane, v);
   }
 }
 // round 2 on `lane` < 18: S_c of output k, lane (k, c)
 template <int MODE>
-__device__ __forceinline__ void wm_r2(const U256* t, L9 (*acc)[3], int lane) {
+__device__ __forceinline__ void wm_r2(const U256* t, L9s (*acc)[3], int lane) {
   using Sh = WShape<MODE>;
   constexpr int NJ = Sh::NJ;
   if (lane < 18) {
@@ -441,18 +469,18 @@ __device__ __forceinline__ void wm_r2(const U256* t, L9 (*acc)[3], int lane) {
     for (int jj = 0; jj < NJ; ++jj) {
       const int j = Sh::j(jj);
       const int i = k - j < 0 ? k - j + 6 : k - j;
-      const U256 v = t[3 * (i * NJ + jj) + c];
+      const U256 v = ld16_u256(t + 3 * (i * NJ + jj) + c);
       if (jj == 0) s = l9_of(v);
       else l9_add(s, v);
     }
-    acc[k][c] = s;
+    st16_l9(&acc[k][c], s);
   }
 }
 // round 3 for output k < 6 in wave wv = (h, c): component c of g_k (h = 0) or of xi g_k (h = 1)
-__device__ __forceinline__ void wm_r3(Fq2* dst, L9 (*acc)[3], int wv, int k) {
+__device__ __forceinline__ void wm_r3(Fq2* dst, L9s (*acc)[3], int wv, int k) {
   L9 s[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) s[c] = acc[k][c];
+  for (int c = 0; c < 3; ++c) s[c] = ld16_l9(&acc[k][c]);
   L9 v;
   if (wv == 0) {  // t0 - t1
     v = s[0];
@@ -480,8 +508,8 @@ __device__ __forceinline__ void wm_r3(Fq2* dst, L9 (*acc)[3], int wv, int k) {
     l9_sub(v, l9_shl<1>(s[1]));
   }
   const U256 r = l9_reduce(v);
-  Fq2& d = dst[k + (wv >> 1) * 6];
-  if (wv & 1) d.c1 = r; else d.c0 = r;
+  Fq2* d = dst + k + (wv >> 1) * 6;
+  st16_u256((wv & 1) ? &d->c1 : &d->c0, r);
 }
 template <int MODE>
 __device__ __forceinline__ void w_mul(Fq2* dst, const Fq2* x, const Fq2* y, PL& L, int tid) {
