@@ -297,8 +297,11 @@ COLL_DEVICE = "cuda"  # where bench-side collectives (max over ranks, proof agre
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # defaults: 200 untimed warm-up steps (~70 ms) let the GPU reach its steady clocks before the
+    # timed region (2^20 x 32: 0.371-0.375 ms per step after 3 warm-up steps, 0.320-0.323 after 50
+    # or 200, profiles/r05/warm_ab.log), then 100 timed steps (~32 ms)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--log-n", type=int, default=20, help="per-GPU transform size (2^log_n)")
     ap.add_argument("--batch", type=int, default=32, help="polynomials per step")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU baseline work")
@@ -533,7 +536,7 @@ def ntt_2p24(ctx, sp, steps: int) -> dict:
     timed like the headline (HIP events around `steps` back-to-back steps)."""
     n, B = 1 << 24, 2
     step, _ = _single_gpu(ctx, n, B, sp)
-    for _ in range(3):
+    for _ in range(50):  # steady clocks (see --warmup)
         step()
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
