@@ -346,8 +346,11 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
   if (inverse == 2) p->n_inv = Fr::mul(p->n_inv, Fr::to_mont(Fr::to_mont(Fr::one_plain())));  // n^-1 R
   if (inverse) wm = h_inv(wm);
   if (n <= 2048) return up256(p->small_tw, h_powers(wm, n));
-  // passes of radix <= 2^9 (LDS tile 2048 x 32 B)
-  const int P = (log_n + 8) / 9;
+  // passes of radix <= 2^9 (LDS tile 2048 x 32 B); PBF_NTT256_MAXR (4..9) lowers the largest
+  // radix (A/B: more, lighter passes)
+  int maxr = 9;
+  if (const char* e = getenv("PBF_NTT256_MAXR")) maxr = atoi(e) < 4 ? 4 : (atoi(e) > 9 ? 9 : atoi(e));
+  const int P = (log_n + maxr - 1) / maxr;
   p->logr.assign(P, log_n / P);
   for (int i = 0; i < (int)(log_n % P); ++i) p->logr[i] += 1;
   p->tw_bits = (log_n + 1) / 2;
