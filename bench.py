@@ -463,7 +463,7 @@ _NOTE_KEYS = ("sample", "note", "peak_source", "proving_key", "rounds_note", "so
 # north-star and per-config headline entries come last
 _EXTRA_ORDER = ("notes", "cpu_baselines_configs_3_5", "config1_plonk_by_hand", "config5_prove_2p20_mode0",
                 "config5_prove_2p20_4_streams", "config5_prove_2p20", "config4_bn254_msm_2p20", "config4_pairing_check",
-                "config4_pairings_batch", "config4_pairings_batch_65536", "config4_kzg_commit_2p20", "config3_bn254_polymul_2p22", "ntt_2p24",
+                "config4_pairings_batch", "config4_pairings_batch_65536", "config4_pairings_batch_262144", "config4_kzg_commit_2p20", "config3_bn254_polymul_2p22", "ntt_2p24",
                 "config5_prove_2p24", "config5_prove_sharded")
 
 
@@ -707,7 +707,7 @@ def other_configs(ctx, sp) -> dict:
     qs = ctx.g2_bn254_mul([G2G] * nq, [int(x) for x in rng2.integers(1, 1 << 62, size=nq)])
     g2l = pbf.ints_to_limbs([c for q in qs for c in (q[0][0], q[0][1], q[1][0], q[1][1])])
     fq_pp = pairing_fq_products()
-    for npair in (4096, 65536):
+    for npair in (4096, 65536, 262144):
         sc = rng2.integers(0, 1 << 62, size=(npair, 4), dtype=np.uint64)
         sc[:, 3] = 0
         dsc = torch.from_numpy(sc.reshape(-1).view(np.int64)).cuda()
@@ -722,7 +722,8 @@ def other_configs(ctx, sp) -> dict:
             t, pairings_per_s=npair / (t["ms"] / 1e3), batch=npair,
             roofline={"bound": "valu (Fq products)", "achieved": ach, "peak": FQ_MUL_PEAK, "unit": "Fq products/s",
                       "frac": ach / FQ_MUL_PEAK, "fq_products_per_pairing": fq_pp},
-            note="one lane per pairing (pairing_lane_kernel); a batch of 4096 fills 64 of 1024 SIMDs")
+            note="one lane per pairing (pairing_lane_kernel): 4096 fill 64 of 1024 SIMDs, 65536 one wave "
+                 "per SIMD, 262144 four (the kernel built for two waves per SIMD from two)")
         del d1, d2, dout, dsc
     # config 5: generalised PLONK prove (+ verify) of the synthetic mul circuit, 2^20 gates on
     # one GPU (scripts/bench_prover.py; 2^24 gates: profiles/r01/session2/prover_2p22_2p24.log)

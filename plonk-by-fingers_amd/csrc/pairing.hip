@@ -1211,7 +1211,12 @@ __device__ __noinline__ void f12_final_exp(Fq12* R, const PairingConsts& k) {
 
 constexpr size_t PAIR_LANE_MIN = 64;  // batches from this size take the lane engine
 
-__global__ void __launch_bounds__(64) pairing_lane_kernel(const uint64_t* g1, const uint64_t* g2, size_t n,
+// WPE: waves per SIMD the compiler must allow. One lane per pairing puts a batch of 65536 at
+// one wave per SIMD, where the unconstrained build (256 VGPRs) is fastest; from two waves per
+// SIMD the build held at 2 (more scratch, two waves hiding each other's latency) is faster:
+// 262144 pairings 1.89 -> 2.41 M/s, 65536 1.83 -> 1.78 M/s (profiles/r05/lanew_ab.log)
+template <int WPE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) pairing_lane_kernel(const uint64_t* g1, const uint64_t* g2, size_t n,
                                                           uint64_t* out, PairingConsts k) {
   const size_t i0 = (size_t)blockIdx.x * 64 + threadIdx.x;
   const size_t i = i0 < n ? i0 : n - 1;  // surplus lanes repeat the last pair and store nothing
@@ -1417,7 +1422,15 @@ static int pairing_values(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_
   const char* lane_env = getenv("PBF_PAIR_LANE");  // A/B: 1 forces the lane engine, 0 the workgroup one
   const bool lane = lane_env ? lane_env[0] == '1' : (n >= PAIR_LANE_MIN && !getenv("PBF_PAIR_WG"));
   if (lane) {
-    hipLaunchKernelGGL(pairing_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, d_g1, d_g2, n, d_out, k);
+    const uint32_t waves = (uint32_t)((n + 63) / 64);
+    int dev_cus = 0;
+    PBF_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    bool two = waves >= (uint32_t)(8 * dev_cus);  // at least two waves per SIMD (four SIMDs per CU)
+    if (const char* w = getenv("PBF_PAIR_LANE_WPE")) two = w[0] == '2';  // A/B and tests: force a build
+    if (two)
+      hipLaunchKernelGGL(pairing_lane_kernel<2>, dim3(waves), dim3(64), 0, s, d_g1, d_g2, n, d_out, k);
+    else
+      hipLaunchKernelGGL(pairing_lane_kernel<1>, dim3(waves), dim3(64), 0, s, d_g1, d_g2, n, d_out, k);
     PBF_HIP(hipGetLastError());
     return 0;
   }

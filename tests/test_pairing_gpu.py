@@ -87,6 +87,25 @@ def test_lane_engine_matches_workgroup_engine(ctx, monkeypatch):
     assert lane == wg
 
 
+def test_lane_engine_two_wave_build_matches(ctx, monkeypatch):
+    """The lane kernel built for two waves per SIMD (taken from 2 x 4 x CUs waves, i.e. batches of
+    >= 131072 on MI355X) against the unconstrained build, bit for bit, on a ragged batch with
+    identities (PBF_PAIR_LANE_WPE forces either build)."""
+    rng = random.Random(47)
+    n = 150
+    ps = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(n)]
+    qs = ctx.g2_bn254_mul([B.G2_GEN] * n, [rng.randrange(1, B.R) for _ in range(n)])
+    ps[3] = None
+    qs[100] = None
+    monkeypatch.setenv("PBF_PAIR_LANE", "1")
+    monkeypatch.setenv("PBF_PAIR_LANE_WPE", "1")
+    one = ctx.pairing_bn254(ps, qs)
+    monkeypatch.setenv("PBF_PAIR_LANE_WPE", "2")
+    two = ctx.pairing_bn254(ps, qs)
+    assert one == two
+    assert one[7] == B.f12_flat(B.pairing(ps[7], qs[7]))
+
+
 def test_g2_mul_matches_oracle(ctx):
     rng = random.Random(9)
     ks = [0, 1, 2, B.R - 1, rng.randrange(B.R), rng.randrange(B.R)]
