@@ -79,6 +79,18 @@ __global__ void __launch_bounds__(PT) k_lat(int what, int iters, const uint64_t*
       if (lane == 0) x.w[0] = (L.t[0].w[0] >> 4 & 3) | (L.t[1].w[0] >> 4 & 3) << 4 | (L.t[2].w[0] >> 4 & 3) << 8 | (L.t[3].w[0] >> 4 & 3) << 12;
       break;
     }
+    case 21: case 22: case 23: case 24: {  // G1 XYZZ chains on one wave: quad add / quad dbl / lane add / lane dbl
+      const U256 one = Fq::to_mont(Fq::one_plain());
+      Xyzz P{x, y, one, one}, Q{y, x, one, one};
+      for (int i = 0; i < iters; ++i) {
+        if (what == 21) P = G1Quad::add(P, Q);
+        else if (what == 22) P = G1Quad::dbl(P);
+        else if (what == 23) P = G1::add2(P, Q);
+        else P = G1::dbl2(P);
+      }
+      x = P.X;
+      break;
+    }
     case 15: {
       L9 v = l9_of(x);
       for (int i = 0; i < iters; ++i) { l9_add_kq<100>(v); x = l9_reduce(v); v = l9_of(x); }
@@ -139,9 +151,11 @@ int main() {
   const char* names[] = {"fq_mul", "fq2_mul", "w_mul dense", "w_mul five", "w_mul line", "fq_add", "mad_u64_dep",
                          "mad_u64_x4", "mul_add_u32_dep", "fq6_inv_flat", "final_exp_w", "pair_line_products",
                          "barrier", "fq_mul+barrier", "w_frob1", "l9_reduce", "fq_mul x4 waves", "fq_mul x2 waves",
-                         "w_mul round1", "w_mul round2"};
-  const int iters[] = {4096, 2048, 256, 256, 256, 4096, 65536, 65536, 65536, 16, 2, 8, 4096, 1024, 256, 1024, 1024, 1024, 256, 256};
-  for (int w = 0; w < 20; ++w) {
+                         "w_mul round1", "w_mul round2", "(hw id)", "G1Quad::add", "G1Quad::dbl", "G1::add2 (lane)",
+                         "G1::dbl2 (lane)"};
+  const int iters[] = {4096, 2048, 256, 256, 256, 4096, 65536, 65536, 65536, 16, 2, 8, 4096, 1024, 256, 1024, 1024, 1024, 256, 256, 1, 128, 128, 128, 128};
+  for (int w = 0; w < 25; ++w) {
+    if (w == 20) continue;
     for (int rep = 0; rep < 2; ++rep) {  // first launch warms the code
       hipLaunchKernelGGL(k_lat, dim3(1), dim3(PT), 0, 0, w, iters[w], d_seed, d_out, make_consts());
       hipMemcpy(h, d_out, 24, hipMemcpyDeviceToHost);
