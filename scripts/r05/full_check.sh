@@ -11,6 +11,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/r05/pytest_gpu_$TAG.log | head -20; exit 1; }
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05/smoke_$TAG.log 2>&1 || { cat gpurun_out/r05/smoke_$TAG.log; exit 1; }
 fi
+[ "${SKIP_BENCH:-0}" = 1 ] && exit 0
 start=$(date +%s)
 timeout -k 10 900 python bench.py > gpurun_out/r05/bench_$TAG.json 2> gpurun_out/r05/bench_$TAG.err &
 pid=$!
