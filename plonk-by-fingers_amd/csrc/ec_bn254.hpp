@@ -333,32 +333,38 @@ struct G1Quad {
     if constexpr (N > 2) *out[2] = bcast<2>(r);
     if constexpr (N > 3) *out[3] = bcast<3>(r);
   }
+  // dbl-2008-s-1 in three product rounds (round 5; four before, with M (S - X3) on one lane
+  // after the third): M^2 joins the second round, M (S - X3) the third. Measured level on one
+  // wave (13.3 k against 13.0 k cycles, profiles/r05/pairing_lat_g1*.log): the selects, DPP
+  // broadcasts and reduced add / sub chains around the products, not the product rounds, set
+  // a quad operation's latency
   __device__ __forceinline__ static Xyzz dbl(const Xyzz& p) {
     if (G1::is_identity(p)) return p;
     const U256 U = G1::dbl_f(p.Y);
-    U256 V, xx, W, S, ZZ3, MM, WY, ZZZ3;
+    U256 V, xx, W, S, ZZ3, MM, MSX, WY, ZZZ3;
     {
       const U256* x[2] = {&U, &p.X};
       const U256* y[2] = {&U, &p.X};
       U256* o[2] = {&V, &xx};
       mulN<2>(x, y, o);
     }
-    {
-      const U256* x[3] = {&U, &p.X, &V};
-      const U256* y[3] = {&V, &V, &p.ZZ};
-      U256* o[3] = {&W, &S, &ZZ3};
-      mulN<3>(x, y, o);
-    }
     const U256 M = F::add(G1::dbl_f(xx), xx);
     {
-      const U256* x[3] = {&M, &W, &W};
-      const U256* y[3] = {&M, &p.Y, &p.ZZZ};
-      U256* o[3] = {&MM, &WY, &ZZZ3};
-      mulN<3>(x, y, o);
+      const U256* x[4] = {&U, &p.X, &V, &M};
+      const U256* y[4] = {&V, &V, &p.ZZ, &M};
+      U256* o[4] = {&W, &S, &ZZ3, &MM};
+      mulN<4>(x, y, o);
     }
     Xyzz r;
     r.X = F::sub(MM, G1::dbl_f(S));
-    r.Y = F::sub(F::mul(M, F::sub(S, r.X)), WY);
+    const U256 SX = F::sub(S, r.X);
+    {
+      const U256* x[3] = {&M, &W, &W};
+      const U256* y[3] = {&SX, &p.Y, &p.ZZZ};
+      U256* o[3] = {&MSX, &WY, &ZZZ3};
+      mulN<3>(x, y, o);
+    }
+    r.Y = F::sub(MSX, WY);
     r.ZZ = ZZ3;
     r.ZZZ = ZZZ3;
     return r;
