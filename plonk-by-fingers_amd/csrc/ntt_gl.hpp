@@ -235,6 +235,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
                                         uint32_t next) {
   using Sh = GlShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
+  (void)YP;
   static_assert(Sh::NSUB_C * C == GL_STORES, "stores per thread");
   static_assert(RG == 0 || (LOGR == 8 && TILE == 4096 && !PERSIST && !BLK && FIRST == (RG == 1)), "RG shape");
   const FieldArgs f{};

@@ -131,6 +131,8 @@ __device__ __forceinline__ void ip_tile(const IpArgs& a, uint64_t* lds, const ui
                                         uint64_t* v) {
   using Sh = IpShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP, R = Sh::R;
+  (void)LOGC;
+  (void)YP;
   constexpr bool ROW = KIND == 2;
   const FieldArgs f{};
   using G = Goldilocks;
@@ -200,6 +202,7 @@ template <int LOGR, int E64, int KIND, int TILE>
 __device__ __forceinline__ void ip_tile_bc(const IpArgs& a, uint64_t* lds, const uint64_t* tcl, uint32_t tile, int t) {
   using Sh = IpShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
+  (void)YP;
   constexpr bool ROW = KIND == 2;
   const FieldArgs f{};
   using G = Goldilocks;

@@ -1164,7 +1164,6 @@ __device__ __forceinline__ Fq12 f12_frob2(const Fq12& a, const PairingConsts& k)
 __device__ __noinline__ Fq12 f12_csqr(const Fq12& x) {
   const Fq2 g[6] = {x.c0.c0, x.c1.c0, x.c0.c1, x.c1.c1, x.c0.c2, x.c1.c2};  // flat w^0..w^5
   Fq2 lo[3], hi[3];
-#pragma unroll
   for (int m = 0; m < 3; ++m) {
     const Fq2 a = g[m], b = g[m + 3];
     lo[m] = f2_add(f2_sqr(a), f2_mul_xi(f2_sqr(b)));
