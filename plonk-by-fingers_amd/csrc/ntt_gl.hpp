@@ -270,13 +270,21 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   }
   // RG 3: the stage-B general twiddle T3[q1][a0][j] (a0 = r2 + 4 s2), loaded now (in flight
   // during stage A) in the stage-B thread mapping
+  // (geometric form, twpass null: t3[s2] = C[r2][X] D[X]^s2, X = 65536 q1 + j; only C and D are
+  // loaded here, the powers are formed in stage B)
   uint64_t t3[RG == 3 ? 16 : 1];
   if constexpr (RG == 3) {
     const int wave = t >> 6, q1 = wave / Sh::WPQ, rw = (wave % Sh::WPQ) * 64 + (t & 63);
     const int r2 = rw / W, w = rw % W;
-    const uint64_t* tb = a.twpass + ((uint64_t)(q1 * 64 + r2) << 16) + j0 + w;
+    if (a.twpass) {
+      const uint64_t* tb = a.twpass + ((uint64_t)(q1 * 64 + r2) << 16) + j0 + w;
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) t3[s2] = tb[(uint64_t)(4 * s2) << 16];
+      for (int s2 = 0; s2 < 16; ++s2) t3[s2] = tb[(uint64_t)(4 * s2) << 16];
+    } else {
+      const uint64_t X = ((uint64_t)q1 << 16) + j0 + w;
+      t3[0] = a.tws_a[((uint64_t)r2 << 18) + X];
+      t3[1] = a.tws_b[X];
+    }
   }
   if constexpr (!FIRST && RG != 3) if (!a.skip_pass_tw) {
     const uint64_t kmask = (1ull << a.log_ns) - 1;
@@ -335,8 +343,18 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
 #ifndef PBF_GL_NOMATH
     if constexpr (RG == 3) {
+      if (a.twpass) {
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) v[s2] = G::mul(v[s2], t3[s2], f);
+        for (int s2 = 0; s2 < 16; ++s2) v[s2] = G::mul(v[s2], t3[s2], f);
+      } else {
+        uint64_t p = t3[0];
+        const uint64_t d = t3[1];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+          v[s2] = G::mul(v[s2], p, f);
+          if (s2 < 15) p = G::mul(p, d, f);
+        }
+      }
     } else {
       switch (__builtin_amdgcn_readfirstlane(q1)) {
         case 1: gl_stage_b_twiddle<E64, 1>(v); break;

@@ -787,7 +787,26 @@ static int ensure_rg_tables(const NttPlan& p) {
       uint64_t* row = t3.data() + ((fq * 64 + a0) << 16);
       for (uint64_t j = 0; j < 65536; ++j) { row[j] = y; y = hmul(y, st, m); }
     }
-  if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_t3, t3))) return rc;
+  // the last pass's twiddle w^(a0 X) (a0 = r2 + 4 s2, X = 65536 f + j) as C[r2][X] D[X]^s2 with
+  // C = w^(r2 X) (n^-1 folded in for the inverse), D = w^(4 X): 10 MiB instead of 128
+  std::vector<uint64_t> tgc(4ull << 18), tgb(1ull << 18);
+  {
+    const uint64_t w4 = hpow(w, 4, m);
+    uint64_t x1 = 1, x4 = 1;
+    for (uint64_t X = 0; X < (1ull << 18); ++X) {
+      tgb[X] = x4;
+      uint64_t c = scale;
+      for (uint64_t r2 = 0; r2 < 4; ++r2) {
+        tgc[(r2 << 18) + X] = c;
+        c = hmul(c, x1, m);
+      }
+      x1 = hmul(x1, w, m);
+      x4 = hmul(x4, w4, m);
+    }
+  }
+  if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_t3, t3)) ||
+      (rc = upload(p.rg_tgc, tgc)) || (rc = upload(p.rg_tgb, tgb)))
+    return rc;
   p.rg_built = true;
   return 0;
 }
@@ -929,6 +948,15 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
     if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
     if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
+    // round 5: the last pass forms its twiddles as C[r2][X] D[X]^s2 from 10 MiB of tables instead
+    // of reading the 128 MiB T3 (one more product per element): 2 x 2^24 0.390-0.392 against
+    // 0.411-0.412 ms, three alternations (profiles/r05/t3geo_ab.log); PBF_NTT_T3GEO=0 reads T3
+    const char* geo_env = getenv("PBF_NTT_T3GEO");
+    if (rg && i == 2 && !(geo_env && geo_env[0] == '0')) {
+      a.twpass = nullptr;
+      a.tws_a = (const uint64_t*)p.rg_tgc.p;
+      a.tws_b = (const uint64_t*)p.rg_tgb.p;
+    }
     // the regrouped 2^24 plan takes the XCD-blocked order in every pass (round 4: 2 x 2^24
     // 0.433-0.437 ms against 0.447-0.453 k-major, 0.462-0.466 linear, five alternations on one
     // box, profiles/r04/ntt_order24_ab.log); the 2-pass plans keep k-major (2^20 x 32: 0.352-0.355

@@ -138,11 +138,13 @@ def test_alternative_pass_plans_2p24(passes, monkeypatch, vectors):
 
 
 @pytest.mark.parametrize("inverse", [False, True])
-def test_regrouped_2p24_matches_stockham(monkeypatch, inverse):
+@pytest.mark.parametrize("other", [{"PBF_NTT_NO_RG": "1"}, {"PBF_NTT_T3GEO": "0"}])
+def test_regrouped_2p24_matches_stockham(monkeypatch, inverse, other):
     """The regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel: general twiddles only between
-    64-point blocks, the default for 8,8,8) against the round-2 passes (PBF_NTT_NO_RG=1), batch
-    of 2 (XCD k-major tiles sharing the 2^24-entry table), forward and inverse, bit-exact, and
-    polynomial 0 against the oracle's iterative transform."""
+    64-point blocks, the default for 8,8,8; its last pass forming w^(a0 X) as C[r2][X] D[X]^s2)
+    against the round-2 passes (PBF_NTT_NO_RG=1) and against its last pass reading the full
+    2^24-entry table (PBF_NTT_T3GEO=0), batch of 2 (XCD k-major tiles), forward and inverse,
+    bit-exact, and polynomial 0 against the oracle's iterative transform."""
     import torch
 
     n, batch = 1 << 24, 2
@@ -150,7 +152,7 @@ def test_regrouped_2p24_matches_stockham(monkeypatch, inverse):
     host = np.stack([oracle.splitmix_field(GOLD, 900 + i, n) for i in range(batch)])
     stream = torch.cuda.current_stream().cuda_stream
     outs = []
-    for env in ({}, {"PBF_NTT_NO_RG": "1"}):
+    for env in ({}, other):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         c = pbf.Context(0)
