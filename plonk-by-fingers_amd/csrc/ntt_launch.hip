@@ -966,7 +966,10 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     // XCD, so each slice of its 128 MiB T3 table is read into one L2 once, not once per XCD of
     // each polynomial): calibrated traffic 1.886 -> 1.753 GB per 2 x 2^24 step, time level
     // (0.4375-0.4433 against 0.4362-0.4379 ms, profiles/r05/order24.log)
-    if (rg && i == 2 && batch > 1 && tiles % 8 == 0) a.xcd_kmajor = 1;
+    // With the geometric last pass (below) there is no T3 to share: XCD-blocked again (orders 222
+    // 0.3867-0.3868 against 221 0.3918-0.3930 ms, profiles/r05/order_geo.log)
+    const char* geo_off = getenv("PBF_NTT_T3GEO");
+    if (rg && i == 2 && batch > 1 && tiles % 8 == 0 && geo_off && geo_off[0] == '0') a.xcd_kmajor = 1;
     if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
       const uint32_t ord = (uint32_t)atoi(o);
       a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
