@@ -100,6 +100,7 @@ struct NttPlan {
   mutable bool rg_built = false;
   mutable DevBuf rg_tc1, rg_t2, rg_t3;
   mutable DevBuf rg_tgc, rg_tgb;  // geometric last-pass twiddles (PBF_NTT_T3GEO): [r2][X], [X]
+  mutable DevBuf rg_t2d;          // middle pass: w^(16384 a1), a1 < 64 (PBF_NTT_T2GEO)
   // two-pass 4096 x 4096 plan for 2^24-point standard-root transforms (ntt_r4k.hpp; opt-in
   // PBF_NTT_R4K=1): stage tables of both passes and the inter-pass [j][k] table, built lazily
   bool r4k = false;

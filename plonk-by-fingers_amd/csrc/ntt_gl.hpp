@@ -608,8 +608,8 @@ ntt_gl_dual_kernel(GlPassArgs second, GlPassArgs first) {
 #ifndef PBF_RG2_WPE
 #define PBF_RG2_WPE 4
 #endif
-template <int E64>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_RG2_WPE))) ntt_gl_rg2_kernel(GlPassArgs a) {
+template <int E64, bool GEO = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GEO ? 5 : PBF_RG2_WPE))) ntt_gl_rg2_kernel(GlPassArgs a) {
   constexpr int W = 16;
   // 32 KiB; four waves per SIMD (PBF_RG2_WPE): at five the 96-VGPR budget spills 28 B per
   // lane and the pass runs ~2 % slower (profiles/r03/ntt_lds_ab.log)
@@ -627,9 +627,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_RG
   uint64_t v[16], tw[16];
 #pragma unroll
   for (int a2l = 0; a2l < 16; ++a2l) v[a2l] = in[j + (uint64_t)(a2l * 16 + a1h) * stride];
-  {
-    // T2[a1][K] = w^(64 a1 K), a1 = a1l + 4 a1h, K = b0 + 64 b1 = (j mod 256) + 256 d
-    const uint64_t* t2 = a.twpass + ((uint64_t)(a1l + 4 * a1h) << 12) + (j & 255);
+  // T2[a1][K] = w^(64 a1 K), a1 = a1l + 4 a1h, K = b0 + 64 b1 = (j mod 256) + 256 d; geometric
+  // in d (GEO, PBF_NTT_T2GEO: tws_b = w^(16384 a1)): T2[a1][j mod 256] (w^(16384 a1))^d, two loads
+  // and 15 products instead of 16 loads, 16 fewer live registers (five waves per SIMD)
+  constexpr bool geo = GEO;
+  const uint64_t* t2 = a.twpass + ((uint64_t)(a1l + 4 * a1h) << 12) + (j & 255);
+  if constexpr (geo) {
+    tw[0] = t2[0];
+    tw[1] = a.tws_b[a1l + 4 * a1h];
+  } else {
 #pragma unroll
     for (int d = 0; d < 16; ++d) tw[d] = t2[256 * d];
   }
@@ -640,8 +646,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PBF_RG
     default: break;
   }
   dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output d at v[bitrev4(d)]
+  if constexpr (geo) {
+    uint64_t p = tw[0];
+    const uint64_t dd = tw[1];
 #pragma unroll
-  for (int d = 0; d < 16; ++d) lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
+    for (int d = 0; d < 16; ++d) {
+      lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], p, f);
+      if (d < 15) p = G::mul(p, dd, f);
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < 16; ++d) lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
+  }
   __syncthreads();
   const int d2 = t / W;
 #pragma unroll

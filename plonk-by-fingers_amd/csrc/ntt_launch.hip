@@ -578,7 +578,7 @@ static GlPassFn gl_fn_blk(int logr, bool first) {
 template <int E>
 static GlPassFn gl_fn_rg(int pass) {
   if (pass == 0) return ntt_gl_pass_kernel<8, E, true, 4096, false, 1>;
-  if (pass == 1) return ntt_gl_rg2_kernel<E>;
+  if (pass == 1) return getenv("PBF_NTT_T2GEO") ? ntt_gl_rg2_kernel<E, true> : ntt_gl_rg2_kernel<E, false>;
   return ntt_gl_pass_kernel<8, E, false, 4096, false, 3>;
 }
 
@@ -804,8 +804,10 @@ static int ensure_rg_tables(const NttPlan& p) {
       x4 = hmul(x4, w4, m);
     }
   }
+  std::vector<uint64_t> t2d(64);
+  for (uint64_t a1 = 0; a1 < 64; ++a1) t2d[a1] = hpow(w, (16384 * a1) % n, m);
   if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_t3, t3)) ||
-      (rc = upload(p.rg_tgc, tgc)) || (rc = upload(p.rg_tgb, tgb)))
+      (rc = upload(p.rg_tgc, tgc)) || (rc = upload(p.rg_tgb, tgb)) || (rc = upload(p.rg_t2d, t2d)))
     return rc;
   p.rg_built = true;
   return 0;
@@ -947,6 +949,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     if (a.post_tw && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) a.xcd_kmajor = 1;
     if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
     if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
+    if (rg && i == 1 && getenv("PBF_NTT_T2GEO")) a.tws_b = (const uint64_t*)p.rg_t2d.p;  // A/B (ntt_gl_rg2_kernel)
     if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
     // round 5: the last pass forms its twiddles as C[r2][X] D[X]^s2 from 10 MiB of tables instead
     // of reading the 128 MiB T3 (one more product per element): 2 x 2^24 0.390-0.392 against
