@@ -315,10 +315,15 @@ struct G1Quad {
     for (int i = 0; i < 8; ++i) r.w[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.w[i], ctrl, 0xF, 0xF, false);
     return r;
   }
+  // lane l's operand, branch-free: hipcc compiled the nested ternary into divergent branches
+  // per limb (~2 k cycles per product round on one wave, as much as the product itself;
+  // masks: 2.36 k cycles for select + product against 4.37 k, scripts/ubench/quad_lat.hip)
   __device__ __forceinline__ static U256 sel(uint32_t l, const U256& a, const U256& b, const U256& c, const U256& d) {
+    const uint32_t m0 = 0u - (uint32_t)(l == 0), m1 = 0u - (uint32_t)(l == 1), m2 = 0u - (uint32_t)(l == 2),
+                   m3 = 0u - (uint32_t)(l == 3);
     U256 r;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r.w[i] = l == 0 ? a.w[i] : (l == 1 ? b.w[i] : (l == 2 ? c.w[i] : d.w[i]));
+    for (int i = 0; i < 8; ++i) r.w[i] = (a.w[i] & m0) | (b.w[i] & m1) | (c.w[i] & m2) | (d.w[i] & m3);
     return r;
   }
   // out_i = x_i * y_i for i < N (N = 2, 3 or 4), product i on lane i of the quad
