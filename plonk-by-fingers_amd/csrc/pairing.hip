@@ -398,7 +398,9 @@ struct alignas(16) PL {
   Fq2 frob1[12];       // lane-indexed constants: FROB1[k], xi FROB1[k] (a lane-indexed kernel
   U256 frob2[6];       // argument would be copied to scratch)
   U256 px[LCHUNK], py[LCHUNK];
-  Fq2 le[NSTEP][LCHUNK][3];  // lines evaluated at P (w^0, w^1, w^3); two lines -> their product (w^0..w^4)
+  // per step: the lines evaluated at P, pair p's (w^0, w^1, w^3) at [3p .. 3p + 2]; for two pairs
+  // then their product as a register: w^0..w^4 at [0..4], 0 at [5], xi times them at [6..11]
+  Fq2 le[NSTEP][12];
   int skip[LCHUNK];
 };
 
@@ -986,7 +988,7 @@ __device__ __forceinline__ void eval_lines(const uint64_t* g1, const PrepLine* l
   for (int j = tid; j < jobs; j += PT) {
     const int pp = j / (NSTEP * 4), rem = j - pp * (NSTEP * 4), st = rem >> 2, w = rem & 3;
     const PrepLine& ln = lines[(p0 + pp) * NSTEP + st];
-    Fq2* le = L.le[st][pp];
+    Fq2* le = L.le[st] + 3 * pp;
     if (L.skip[pp]) {
       const U256 v = w == 0 ? k.one : u256_zero();
       if (w == 0) le[0].c0 = v;
@@ -1009,16 +1011,16 @@ __device__ __forceinline__ void eval_lines(const uint64_t* g1, const PrepLine* l
 
 // The two lines of every step multiplied together in place (off the Miller loop's critical
 // path: all steps are independent): l m = a0 b0 + xi a3 b3 + (a0 b1 + a1 b0) w + a1 b1 w^2
-// + (a0 b3 + a3 b0) w^3 + (a1 b3 + a3 b1) w^4, written to le[st][0][0..2], le[st][1][0..1]
-// (the flat w^0..w^4 of a W_FIVE operand). LB steps per batch of three rounds.
+// + (a0 b3 + a3 b0) w^3 + (a1 b3 + a3 b1) w^4, written to le[st][0..4] (the flat w^0..w^4 of a
+// W_FIVE operand) with le[st][5] = 0 and xi times them at [6..11]. LB steps per batch.
 __device__ __forceinline__ void pair_line_products(PL& L, int tid) {
   // the 9 products (index into l, index into m) and their output coefficient
   constexpr int8_t PA[9] = {0, 2, 0, 1, 1, 0, 2, 1, 2}, PB[9] = {0, 2, 1, 0, 1, 2, 0, 2, 1};
   for (int st0 = 0; st0 < NSTEP; st0 += LB) {
     const int sb = tid / 27, rem = tid - 27 * sb, q = rem / 3, r = rem - 3 * q;
     if (sb < LB && st0 + sb < NSTEP) {
-      const Fq2* ln = L.le[st0 + sb][0];
-      const Fq2* mn = L.le[st0 + sb][1];
+      const Fq2* ln = L.le[st0 + sb];
+      const Fq2* mn = L.le[st0 + sb] + 3;
       L.t[tid] = Fq::mul(kara_operand(ln[PA[q]], r), kara_operand(mn[PB[q]], r));
     }
     bsync();
@@ -1037,11 +1039,39 @@ __device__ __forceinline__ void pair_line_products(PL& L, int tid) {
       const U256 x0 = c ? P[ia].c1 : P[ia].c0;
       const U256 x1 = e == 2 ? u256_zero() : (c ? P[ia + 1].c1 : P[ia + 1].c0);
       const U256 v = Fq::add(x0, x1);
-      Fq2* o = &L.le[st0 + sb2][0][0] + e;
+      Fq2* o = L.le[st0 + sb2] + e;
       if (c) o->c1 = v; else o->c0 = v;
     }
     bsync();
+    // the register form's xi half (a line product is the x operand of a merged step's product,
+    // pairing_product_kernel) and its zero slot 5
+    if (tid < 6 * LB && st0 + tid / 6 < NSTEP) {
+      const int sb2 = tid / 6, e = tid % 6;
+      Fq2* o = L.le[st0 + sb2];
+      const Fq2 v = e == 5 ? Fq2{u256_zero(), u256_zero()} : o[e];
+      if (e == 5) o[5] = v;
+      o[6 + e] = f2_mul_xi(v);
+    }
+    bsync();
   }
+}
+
+// dA = xA yA (MA) and dB = xB yB (MB) in one set of rounds (w_mul_dual with mixed shapes)
+template <int MA, int MB>
+__device__ __forceinline__ void w_mul_pair(Fq2* dA, const Fq2* xA, const Fq2* yA, Fq2* dB, const Fq2* xB, const Fq2* yB,
+                                           PL& L, int tid) {
+  if (tid < 128) wm_r1<MA, false>(xA, yA, L.t, tid);
+  else wm_r1<MB, false>(xB, yB, L.t + 128, tid - 128);
+  bsync();
+  const int wv = tid >> 6, k = tid & 63;
+  if (wv == 0) wm_r2<MA>(L.t, L.acc[0], k);
+  else if (wv == 1) wm_r2<MB>(L.t + 128, L.acc[1], k);
+  bsync();
+  if ((k & 31) < 6) {
+    const bool b = k >= 32;
+    wm_r3(b ? dB : dA, L.acc[b ? 1 : 0], wv, k & 31);
+  }
+  bsync();
 }
 
 // One workgroup multiplies the Miller values of pairs [g per, (g+1) per) (one shared
@@ -1064,10 +1094,53 @@ __global__ void __launch_bounds__(PT) pairing_product_kernel(const uint64_t* g1,
     eval_lines(g1, lines, qinf, c, m, k, L, tid);
     if (m == 2) pair_line_products(L, tid);
     w_one(f, k, tid);
-    for (int st = 0; st < NSTEP; ++st) {
-      if (c_steps.kind[st] == ST_DBL && st > 0) w_mul<W_DENSE>(f, f, f, L, tid);  // f = 1 before step 0
-      if (m == 2) w_mul<W_FIVE>(f, f, &L.le[st][0][0], L, tid);
-      else w_mul<W_LINE>(f, f, L.le[st][0], L, tid);
+    if (m == 2) {
+      // Round 5: a doubling step followed by an addition step multiplies f by the product of the
+      // two steps' line products, M = LL(st) LL(st + 1), formed beside the doubling's squaring
+      // (w_mul_pair): one dense product per addition step instead of a line product; likewise
+      // pi(Q) and -pi^2(Q)'s lines, merged in the first squaring round without an addition
+      Fq2* M = L.reg[1];
+      Fq2* MP = L.reg[2];
+      bool pi_done = false;
+      for (int st = 0; st < NSTEP; ++st) {
+        const int kind = c_steps.kind[st];
+        if (kind == ST_ADD_PI) {  // the last two steps, merged
+          if (!pi_done) w_mul<W_FIVE>(MP, L.le[st], L.le[st + 1], L, tid);
+          w_mul<W_DENSE>(f, f, MP, L, tid);
+          break;
+        }
+        const bool merge = kind == ST_DBL && st + 1 < NSTEP && c_steps.kind[st + 1] == ST_ADD_Q;
+        if (st == 0) {  // f = 1
+          if (merge) {
+            w_mul<W_FIVE>(M, L.le[0], L.le[1], L, tid);
+            w_copy(f, M, tid);
+            ++st;
+          } else {
+            w_mul<W_FIVE>(f, f, L.le[0], L, tid);
+          }
+          continue;
+        }
+        if (kind == ST_DBL) {
+          if (merge) w_mul_pair<W_DENSE, W_FIVE>(f, f, f, M, L.le[st], L.le[st + 1], L, tid);
+          else if (!pi_done) {
+            w_mul_pair<W_DENSE, W_FIVE>(f, f, f, MP, L.le[NSTEP - 2], L.le[NSTEP - 1], L, tid);
+            pi_done = true;
+          } else {
+            w_mul<W_DENSE>(f, f, f, L, tid);
+          }
+        }
+        if (merge) {
+          w_mul<W_DENSE>(f, f, M, L, tid);
+          ++st;
+        } else {
+          w_mul<W_FIVE>(f, f, L.le[st], L, tid);
+        }
+      }
+    } else {
+      for (int st = 0; st < NSTEP; ++st) {
+        if (c_steps.kind[st] == ST_DBL && st > 0) w_mul<W_DENSE>(f, f, f, L, tid);  // f = 1 before step 0
+        w_mul<W_LINE>(f, f, L.le[st], L, tid);
+      }
     }
     if (c == b0) w_copy(F, f, tid);
     else w_mul<W_DENSE>(F, F, f, L, tid);

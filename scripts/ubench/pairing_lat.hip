@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(PT) k_lat(int what, int iters, const uint64_t*
     L.reg[1][lane] = Fq2{y, x};
     L.reg[2][lane] = Fq2{y, y};
   }
-  for (int e = lane; e < NSTEP * LCHUNK * 3; e += PT) (&L.le[0][0][0])[e] = Fq2{x, y};
+  for (int e = lane; e < NSTEP * 12; e += PT) (&L.le[0][0])[e] = Fq2{x, y};
   if (lane < 26) L.sl[lane] = Fq2{x, y};
   __syncthreads();
   uint64_t t0 = clock64(), w0 = wall_clock64();
