@@ -868,7 +868,32 @@ __device__ __forceinline__ Xyzz fx_bucket_into(Xyzz acc, uint32_t k, const Xyzz*
   for (uint32_t u = o + 1; u <= e; ++u) acc = G1::add2(acc, head[u].acc);
   return acc;
 }
-template <int SEQ>
+// Every bucket spanning chunks resolved to one sum in buckets[k] (one lane per bucket; its tail
+// run plus its continuations as fx_bucket_into adds them): the C and D sums then add one value
+// per bucket each, where each of them added the bucket's ~3 parts (wide windows, ~100 entries
+// per bucket over 43-entry chunks).
+__global__ void __launch_bounds__(256) msm_fx_resolve(Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
+                                                      const uint32_t* start, const uint32_t* end, uint32_t nb,
+                                                      uint32_t cap) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nb) return;
+  const uint32_t bs = start[k], be = end[k];
+  if (be <= bs) return;
+  const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
+  if (o == e) return;  // already whole in buckets[k]
+  Xyzz acc = tail[o].acc;
+  if (e - o > cap) {
+    acc = G1::add2(acc, head[o + 1].acc);
+  } else {
+    for (uint32_t u = o + 1; u <= e; ++u) acc = G1::add2(acc, head[u].acc);
+  }
+  buckets[k] = acc;
+}
+__device__ __forceinline__ Xyzz fx_bucket_resolved(Xyzz acc, uint32_t k, const Xyzz* buckets, const uint32_t* start,
+                                                   const uint32_t* end) {
+  return end[k] <= start[k] ? acc : G1::add2(acc, buckets[k]);
+}
+template <int SEQ, bool RES>
 __global__ void __launch_bounds__(256) msm_fxg_cd_seq(const Xyzz* buckets, const ChunkPart* head,
                                                       const ChunkPart* tail, const uint32_t* start,
                                                       const uint32_t* end, Xyzz* cd, int lb, int hb, uint32_t cap) {
@@ -880,12 +905,16 @@ __global__ void __launch_bounds__(256) msm_fxg_cd_seq(const Xyzz* buckets, const
   uint32_t lanes, outi;
   if (g < gC) {
     const uint32_t h = g * vc + t / lc, per = L / lc, l0 = (t % lc) * per;
-    for (uint32_t i = 0; i < per; ++i) acc = fx_bucket_into(acc, L * h + l0 + i, buckets, head, tail, start, end, cap);
+    for (uint32_t i = 0; i < per; ++i)
+      acc = RES ? fx_bucket_resolved(acc, L * h + l0 + i, buckets, start, end)
+                : fx_bucket_into(acc, L * h + l0 + i, buckets, head, tail, start, end, cap);
     lanes = lc;
     outi = h;
   } else {
     const uint32_t l = (g - gC) * vd + t / ld, per = NH / ld, h0 = (t % ld) * per;
-    for (uint32_t i = 0; i < per; ++i) acc = fx_bucket_into(acc, L * (h0 + i) + l, buckets, head, tail, start, end, cap);
+    for (uint32_t i = 0; i < per; ++i)
+      acc = RES ? fx_bucket_resolved(acc, L * (h0 + i) + l, buckets, start, end)
+                : fx_bucket_into(acc, L * (h0 + i) + l, buckets, head, tail, start, end, cap);
     lanes = ld;
     outi = NH + l;
   }
@@ -1548,14 +1577,18 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
                          (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb);
     } else {
       const uint32_t cap_seq = g.c > 16 && fx_chunk_join() ? FX_SEQ_CAP : 1;
-      if (env_default_off("PBF_MSM_CD_SEQ32"))  // read per call: an A/B knob
-        hipLaunchKernelGGL(msm_fxg_cd_seq<32>, dim3(fxg_cd_seq_groups(g, 32)), dim3(256), 0, a,
-                           (const Xyzz*)buckets.p, (const ChunkPart*)head.p, (const ChunkPart*)tail.p,
-                           (const uint32_t*)start.p, (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
-      else
-        hipLaunchKernelGGL(msm_fxg_cd_seq<8>, dim3(fxg_cd_seq_groups(g, 8)), dim3(256), 0, a, (const Xyzz*)buckets.p,
-                           (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
-                           (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
+      // resolve the spanning buckets once (default; PBF_MSM_CD_RESOLVE=0: the C and D sums each
+      // add the parts, A/B)
+      const bool res = env_default_on("PBF_MSM_CD_RESOLVE");  // read per call: an A/B knob
+      if (res)
+        hipLaunchKernelGGL(msm_fx_resolve, dim3(NB / 256), dim3(256), 0, a, (Xyzz*)buckets.p, (const ChunkPart*)head.p,
+                           (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, NB, cap_seq);
+      const bool s32 = env_default_off("PBF_MSM_CD_SEQ32");  // read per call: an A/B knob
+      auto* cdk = s32 ? (res ? msm_fxg_cd_seq<32, true> : msm_fxg_cd_seq<32, false>)
+                      : (res ? msm_fxg_cd_seq<8, true> : msm_fxg_cd_seq<8, false>);
+      hipLaunchKernelGGL(cdk, dim3(fxg_cd_seq_groups(g, s32 ? 32 : 8)), dim3(256), 0, a, (const Xyzz*)buckets.p,
+                         (const ChunkPart*)head.p, (const ChunkPart*)tail.p, (const uint32_t*)start.p,
+                         (const uint32_t*)end.p, (Xyzz*)shares.p, g.lb, g.hb, cap_seq);
     }
     hipLaunchKernelGGL(msm_fxg_subsets_q<128>, dim3(g.lb + g.hb + 1), dim3(512), 0, a, (const Xyzz*)shares.p,
                        (Xyzz*)parts.p, g.lb, g.hb);
