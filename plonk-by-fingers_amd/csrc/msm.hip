@@ -109,6 +109,41 @@ __global__ void msm_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* st
     if (j == m - 1 || keys[j + 1] != k) end[k] = (uint32_t)(j + 1);
   }
 }
+// The same bounds, four sorted keys per thread from one 16-B load and no grid-stride loop: the
+// loop above kept one load in flight per wave and iteration (~48 dependent iterations per
+// thread at 2^28 entries: latency-bound, ~1.3 TB/s).
+__global__ void __launch_bounds__(256) msm_bucket_bounds4(const uint32_t* keys, uint64_t m, uint32_t* start,
+                                                          uint32_t* end, uint32_t sent) {
+  const uint64_t j0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j0 >= m) return;
+  uint32_t k[6];
+  if (j0 + 4 <= m) {
+    const uint4 v = *(const uint4*)(keys + j0);
+    k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k[1 + i] = j0 + i < m ? keys[j0 + i] : sent;
+  }
+  k[0] = j0 ? keys[j0 - 1] : sent;
+  k[5] = j0 + 4 < m ? keys[j0 + 4] : sent;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t j = j0 + i;
+    const uint32_t kk = k[1 + i];
+    if (j >= m || kk == sent) continue;
+    if (j == 0 || k[i] != kk) start[kk] = (uint32_t)j;
+    if (j == m - 1 || k[i + 2] != kk) end[kk] = (uint32_t)(j + 1);
+  }
+}
+static void launch_bucket_bounds(const uint32_t* keys, uint64_t m, uint32_t* start, uint32_t* end, uint32_t sent,
+                                 hipStream_t s) {
+  if (env_default_off("PBF_MSM_BOUNDS1"))  // read per call: an A/B knob (the grid-stride form)
+    hipLaunchKernelGGL(msm_bucket_bounds, dim3((uint32_t)(((m + 255) / 256) > 16384 ? 16384 : (m + 255) / 256)),
+                       dim3(256), 0, s, keys, m, start, end, sent);
+  else
+    hipLaunchKernelGGL(msm_bucket_bounds4, dim3((uint32_t)((m + 1023) / 1024)), dim3(256), 0, s, keys, m, start, end,
+                       sent);
+}
 
 #ifndef PBF_MSM_CH
 #define PBF_MSM_CH 43
@@ -536,17 +571,31 @@ static_assert(FX_NB - 1 <= 0x7FFF, "a 16-bit digit code holds |d| - 1 in 15 bits
 // waves of a step hold only adding lanes (a per-chunk grid kept every wave busy at every
 // step for a shrinking share of active lanes).
 // the largest number of chunks a bucket spans (bounds the tree steps that do any work)
+constexpr uint32_t MSM_SPAN_PER = 8;  // buckets per thread of msm_max_span
 __global__ void __launch_bounds__(256) msm_max_span(const uint32_t* start, const uint32_t* end, uint32_t nb,
                                                     uint32_t* span) {
-  // one global atomic per workgroup (2^19 buckets of the windowed form on one address: 93 us)
+  // MSM_SPAN_PER buckets per thread, a wave max, one LDS atomic per wave and one global atomic per
+  // workgroup (one bucket per thread and one global atomic per 256 buckets: ~97 us at 2^21 buckets,
+  // the atomics on one address serialised)
   __shared__ uint32_t bmax;
   if (threadIdx.x == 0) bmax = 0;
   __syncthreads();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nb && end[k] > start[k]) atomicMax(&bmax, (end[k] - 1) / MSM_CH - start[k] / MSM_CH);
+  uint32_t mx = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < MSM_SPAN_PER; ++i) {
+    const uint32_t k = blockIdx.x * (256 * MSM_SPAN_PER) + i * 256 + threadIdx.x;
+    if (k < nb) {
+      const uint32_t bs = start[k], be = end[k];
+      if (be > bs) mx = max(mx, (be - 1) / MSM_CH - bs / MSM_CH);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(&bmax, mx);
   __syncthreads();
   if (threadIdx.x == 0 && bmax) atomicMax(span, bmax);
 }
+static uint32_t max_span_groups(uint32_t nb) { return (nb + 256 * MSM_SPAN_PER - 1) / (256 * MSM_SPAN_PER); }
 // cap: buckets spanning more than `cap` chunks are left to msm_join_chunks (the fixed-base form;
 // ~0u: none), so the pair slots per bucket follow min(largest span, cap), not the largest span
 __global__ void __launch_bounds__(256) msm_join_step(ChunkPart* head, const uint32_t* start, const uint32_t* end,
@@ -1155,8 +1204,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   }
   PBF_HIP(hipMemsetAsync(w.start.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
   PBF_HIP(hipMemsetAsync(w.end.p, 0, (uint64_t)MSM_NW * MSM_NB * 4, s));
-  hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, s, (const uint32_t*)w.keys2.p, m,
-                     (uint32_t*)w.start.p, (uint32_t*)w.end.p, MSM_SENTINEL);
+  launch_bucket_bounds((const uint32_t*)w.keys2.p, m, (uint32_t*)w.start.p, (uint32_t*)w.end.p, MSM_SENTINEL, s);
   // the valid (non-sentinel) prefix of the sorted list: the sentinel sorts last; its
   // length is known only on the device, so chunks past it return at once. No bucket memset:
   // the reduction reads only the buckets the accumulation wrote (fx_bucket).
@@ -1183,7 +1231,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
                        (ChunkPart*)w.head.p, (ChunkPart*)w.tail.p, MSM_SENTINEL, (const uint32_t*)nullptr,
                        (uint32_t*)hk.p, (uint32_t*)tk.p);
   }
-  hipLaunchKernelGGL(msm_max_span, dim3(NBT / 256), dim3(256), 0, s, (const uint32_t*)w.start.p,
+  hipLaunchKernelGGL(msm_max_span, dim3(max_span_groups(NBT)), dim3(256), 0, s, (const uint32_t*)w.start.p,
                      (const uint32_t*)w.end.p, NBT, (uint32_t*)w.span.p);
   const uint64_t mean_span = m / ((uint64_t)NBT * MSM_CH) + 2;
   for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP; step <<= 1) {
@@ -1487,8 +1535,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   }
   hipLaunchKernelGGL(msm_fx_clear, dim3(NB / 256), dim3(256), 0, q, (uint32_t*)start.p, (uint32_t*)end.p,
                      (uint32_t*)spb.p);
-  hipLaunchKernelGGL(msm_bucket_bounds, dim3(grid1(m)), dim3(256), 0, q, (const uint32_t*)keys2.p, m,
-                     (uint32_t*)start.p, (uint32_t*)end.p, NB);
+  launch_bucket_bounds((const uint32_t*)keys2.p, m, (uint32_t*)start.p, (uint32_t*)end.p, NB, q);
   if (use_prep) {
     PBF_HIP(hipGetLastError());
     PBF_HIP(hipEventRecord(tl.prep_done[ps], q));
@@ -1513,7 +1560,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
                        (const uint32_t*)end.p, (uint32_t)m, (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p,
                        NB, (const uint32_t*)nullptr, (uint32_t*)hk.p, (uint32_t*)tk.p);
   }
-  hipLaunchKernelGGL(msm_max_span, dim3(NB / 256), dim3(256), 0, s, (const uint32_t*)start.p,
+  hipLaunchKernelGGL(msm_max_span, dim3(max_span_groups(NB)), dim3(256), 0, s, (const uint32_t*)start.p,
                      (const uint32_t*)end.p, NB, (uint32_t*)spb.p);
   PBF_HIP(hipGetLastError());
   if (use_prep) {  // prep slot ps is free once the accumulation has read keys2 / vals2
