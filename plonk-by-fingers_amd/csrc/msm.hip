@@ -672,6 +672,56 @@ __global__ void __launch_bounds__(256) msm_join_rest_g(ChunkPart* head, const ui
   head[o + 1].acc = acc;
 }
 
+// Round 5, the wide-window join in two launches instead of ~13 tree steps that each scanned every
+// chunk: msm_heavy_list lists the buckets spanning more than `cap` chunks (one atomic per wave),
+// msm_join_heavy sums each one's continuations with HJ_LPB lanes (a strided sequence per lane,
+// then a shuffle tree inside the lane group) into head[o + 1], as the tree steps did.
+// Buckets spanning more than HJ_MAX chunks (skewed scalars: ~6100 at 2^18 equal scalars) are
+// left to the tree steps, which the lane groups' sequences would take too long for.
+constexpr uint32_t HJ_LPB = 16;    // lanes per heavy bucket (divides 64)
+constexpr uint32_t HJ_MAX = 1024;  // at most 64 continuations per lane
+__global__ void __launch_bounds__(256) msm_heavy_list(const uint32_t* start, const uint32_t* end, uint32_t nb,
+                                                      uint32_t cap, uint32_t hmax, uint32_t* list, uint32_t* count) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  bool h = false;
+  if (k < nb) {
+    const uint32_t bs = start[k], be = end[k];
+    const uint32_t sp = be > bs ? (be - 1) / MSM_CH - bs / MSM_CH : 0;
+    h = sp > cap && sp <= hmax;
+  }
+  const uint64_t mask = __ballot(h);
+  if (!mask) return;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63, lead = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane == lead) base = atomicAdd(count, (uint32_t)__popcll(mask));
+  base = (uint32_t)__shfl((int)base, (int)lead);
+  if (h) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1))] = k;
+}
+__device__ __forceinline__ Xyzz xyzz_shfl_xor(const Xyzz& v, int off) {
+  Xyzz r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.X.w[i] = (uint32_t)__shfl_xor((int)v.X.w[i], off);
+    r.Y.w[i] = (uint32_t)__shfl_xor((int)v.Y.w[i], off);
+    r.ZZ.w[i] = (uint32_t)__shfl_xor((int)v.ZZ.w[i], off);
+    r.ZZZ.w[i] = (uint32_t)__shfl_xor((int)v.ZZZ.w[i], off);
+  }
+  return r;
+}
+__global__ void __launch_bounds__(256) msm_join_heavy(ChunkPart* head, const uint32_t* list, const uint32_t* count,
+                                                      const uint32_t* start, const uint32_t* end) {
+  const uint32_t cnt = *count, sub = threadIdx.x % HJ_LPB, per_block = 256 / HJ_LPB;
+  for (uint32_t b = blockIdx.x * per_block + threadIdx.x / HJ_LPB; b < cnt; b += gridDim.x * per_block) {
+    // b is uniform over the lane group: the group's shuffles below see only its own lanes
+    const uint32_t k = list[b];
+    const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH;
+    Xyzz acc = G1::identity();
+    for (uint32_t u = o + 1 + sub; u <= e; u += HJ_LPB) acc = G1::add2(acc, head[u].acc);
+    for (int off = HJ_LPB / 2; off > 0; off >>= 1) acc = G1::add2(acc, xyzz_shfl_xor(acc, off));
+    if (sub == 0) head[o + 1].acc = acc;  // every lane of the group has read its parts by now
+  }
+}
+
 // Bucket b's full sum after the join: a bucket spanning chunks o < e is its chunk-o tail run
 // plus the joined continuations head[o + 1]; any other bucket was written whole (or is
 // empty: never read).
@@ -1586,6 +1636,23 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
     uint32_t cap = 2;
     while (cap < 2 * mean_span && cap < FX_JOIN_GROUP_C) cap <<= 1;
     if (wide) cap = FX_SEQ_CAP;
+    // wide windows: the heavy buckets listed and joined in two launches (PBF_MSM_HEAVY_JOIN=0:
+    // the tree steps below, A/B)
+    const bool heavy = wide && env_default_on("PBF_MSM_HEAVY_JOIN");  // read per call: an A/B knob
+    if (heavy) {
+      DevBuf& hl = ctx->buf(pre + "hlist");
+      if (hl.bytes < (uint64_t)NB * 4 + 4 && tl.used[slot]) PBF_HIP(hipEventSynchronize(tl.done[slot]));
+      if ((rc = hl.ensure((uint64_t)NB * 4 + 4))) return rc;
+      uint32_t* cnt = (uint32_t*)hl.p + NB;
+      PBF_HIP(hipMemsetAsync(cnt, 0, 4, a));
+      hipLaunchKernelGGL(msm_heavy_list, dim3(NB / 256), dim3(256), 0, a, (const uint32_t*)start.p,
+                         (const uint32_t*)end.p, NB, cap, HJ_MAX, (uint32_t*)hl.p, cnt);
+      hipLaunchKernelGGL(msm_join_heavy, dim3(1024), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)hl.p,
+                         (const uint32_t*)cnt, (const uint32_t*)start.p, (const uint32_t*)end.p);
+    }
+    // (with the heavy join the tree steps take only the buckets spanning more than HJ_MAX chunks
+    // -- skewed scalars -- and exit at once when there are none)
+    const uint32_t jcap = heavy ? HJ_MAX : cap;
     for (uint32_t step = 1; step < nchunks && step < FX_JOIN_GROUP_C; step <<= 1) {
       if (step < cap && !wide) {
         const uint64_t items = (uint64_t)NB * ((mean_span + 2 * step - 1) / (2 * step));
@@ -1594,7 +1661,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
       }
       hipLaunchKernelGGL(msm_join_chunks, dim3((uint32_t)grid1(nchunks)), dim3(256), 0, a, (ChunkPart*)head.p,
                          (const uint32_t*)hk.p, (const uint32_t*)start.p, (const uint32_t*)end.p, nchunks, step,
-                         (const uint32_t*)spb.p, NB, cap);
+                         (const uint32_t*)spb.p, NB, jcap);
     }
     hipLaunchKernelGGL(msm_join_rest_g, dim3(NB / 256), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)start.p,
                        (const uint32_t*)end.p, NB, (const uint32_t*)spb.p, FX_JOIN_GROUP_C);
