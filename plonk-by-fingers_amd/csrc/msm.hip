@@ -374,7 +374,11 @@ msm_chunk_acc_l29r(const Affine* pts, const uint32_t* keys, const uint32_t* vals
 __global__ void __launch_bounds__(256) msm_l29_finish(const uint32_t* braw, Xyzz* buckets, ChunkPart* head,
                                                       ChunkPart* tail, const uint32_t* hkey, const uint32_t* tkey,
                                                       const uint32_t* start, const uint32_t* end, uint32_t nb,
-                                                      uint32_t nchunks, uint32_t sent) {
+                                                      uint32_t nchunks, uint32_t sent, uint32_t hmax) {
+  // hmax > 0 (the fixed-base wide-window tail): only the partials of buckets spanning more than
+  // hmax chunks are converted here; msm_join_heavy and msm_fx_resolve convert the others as they
+  // read them (one read of the raw form instead of a converted write and its read)
+  auto keep = [&](uint32_t k) { return k != sent && (hmax == 0 || (end[k] - 1) / MSM_CH - start[k] / MSM_CH > hmax); };
   const uint64_t items = (uint64_t)nb + 2ull * nchunks;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += (uint64_t)gridDim.x * blockDim.x) {
     if (i < nb) {
@@ -382,10 +386,10 @@ __global__ void __launch_bounds__(256) msm_l29_finish(const uint32_t* braw, Xyzz
       if (be > bs && bs / MSM_CH == (be - 1) / MSM_CH) buckets[i] = l29::raw_to_xyzz(braw + 36 * i);
     } else if (i < (uint64_t)nb + nchunks) {
       const uint64_t t = i - nb;
-      if (hkey[t] != sent) head[t].acc = l29::raw_to_xyzz(head[t].raw);
+      if (keep(hkey[t])) head[t].acc = l29::raw_to_xyzz(head[t].raw);
     } else {
       const uint64_t t = i - nb - nchunks;
-      if (tkey[t] != sent) tail[t].acc = l29::raw_to_xyzz(tail[t].raw);
+      if (keep(tkey[t])) tail[t].acc = l29::raw_to_xyzz(tail[t].raw);
     }
   }
 }
@@ -708,15 +712,17 @@ __device__ __forceinline__ Xyzz xyzz_shfl_xor(const Xyzz& v, int off) {
   }
   return r;
 }
+// raw: the continuations are still in msm_chunk_acc_l29r's raw form (msm_l29_finish's hmax)
 __global__ void __launch_bounds__(256) msm_join_heavy(ChunkPart* head, const uint32_t* list, const uint32_t* count,
-                                                      const uint32_t* start, const uint32_t* end) {
+                                                      const uint32_t* start, const uint32_t* end, uint32_t raw) {
   const uint32_t cnt = *count, sub = threadIdx.x % HJ_LPB, per_block = 256 / HJ_LPB;
   for (uint32_t b = blockIdx.x * per_block + threadIdx.x / HJ_LPB; b < cnt; b += gridDim.x * per_block) {
     // b is uniform over the lane group: the group's shuffles below see only its own lanes
     const uint32_t k = list[b];
     const uint32_t o = start[k] / MSM_CH, e = (end[k] - 1) / MSM_CH;
     Xyzz acc = G1::identity();
-    for (uint32_t u = o + 1 + sub; u <= e; u += HJ_LPB) acc = G1::add2(acc, head[u].acc);
+    for (uint32_t u = o + 1 + sub; u <= e; u += HJ_LPB)
+      acc = G1::add2(acc, raw ? l29::raw_to_xyzz(head[u].raw) : head[u].acc);
     for (int off = HJ_LPB / 2; off > 0; off >>= 1) acc = G1::add2(acc, xyzz_shfl_xor(acc, off));
     if (sub == 0) head[o + 1].acc = acc;  // every lane of the group has read its parts by now
   }
@@ -973,18 +979,21 @@ __device__ __forceinline__ Xyzz fx_bucket_into(Xyzz acc, uint32_t k, const Xyzz*
 // per bucket over 43-entry chunks).
 __global__ void __launch_bounds__(256) msm_fx_resolve(Xyzz* buckets, const ChunkPart* head, const ChunkPart* tail,
                                                       const uint32_t* start, const uint32_t* end, uint32_t nb,
-                                                      uint32_t cap) {
+                                                      uint32_t cap, uint32_t hmax) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nb) return;
   const uint32_t bs = start[k], be = end[k];
   if (be <= bs) return;
   const uint32_t o = bs / MSM_CH, e = (be - 1) / MSM_CH;
   if (o == e) return;  // already whole in buckets[k]
-  Xyzz acc = tail[o].acc;
+  // hmax > 0: the partials of buckets spanning at most hmax chunks are still raw (msm_l29_finish);
+  // a joined head[o + 1] (span > cap) was written converted by its join
+  const bool rawp = hmax != 0 && e - o <= hmax;
+  Xyzz acc = rawp ? l29::raw_to_xyzz(tail[o].raw) : tail[o].acc;
   if (e - o > cap) {
     acc = G1::add2(acc, head[o + 1].acc);
   } else {
-    for (uint32_t u = o + 1; u <= e; ++u) acc = G1::add2(acc, head[u].acc);
+    for (uint32_t u = o + 1; u <= e; ++u) acc = G1::add2(acc, rawp ? l29::raw_to_xyzz(head[u].raw) : head[u].acc);
   }
   buckets[k] = acc;
 }
@@ -1273,7 +1282,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
     hipLaunchKernelGGL(msm_l29_finish, dim3(grid1((uint64_t)NBT + 2ull * nchunks)), dim3(256), 0, s,
                        (const uint32_t*)braw.p, (Xyzz*)w.buckets.p, (ChunkPart*)w.head.p, (ChunkPart*)w.tail.p,
                        (const uint32_t*)hk.p, (const uint32_t*)tk.p, (const uint32_t*)w.start.p,
-                       (const uint32_t*)w.end.p, NBT, nchunks, MSM_SENTINEL);
+                       (const uint32_t*)w.end.p, NBT, nchunks, MSM_SENTINEL, 0u);
   } else {
     hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s,
                        (const Affine*)w.pts.p, (const uint32_t*)w.keys2.p, (const uint32_t*)w.vals2.p,
@@ -1594,7 +1603,16 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
   // ---- accumulation
   // no bucket memset: msm_fx_cd reads only the buckets the accumulation wrote (fx_bucket)
   const uint32_t nchunks = (uint32_t)((m + MSM_CH - 1) / MSM_CH);
-  if (msm_l29() && msm_rawflush(g.c > 16)) {
+  const bool rawf = msm_l29() && msm_rawflush(g.c > 16);
+  // the wide-window tail converts the partials of buckets spanning <= HJ_MAX chunks as it reads
+  // them (heavy join, resolve); msm_l29_finish only the rest (PBF_MSM_DEFER_CONV=0: all, A/B).
+  // The conditions are those of the tail below: wide windows, chunk join, single-lane C / D
+  // sums, heavy join and resolve all on.
+  const bool defer = rawf && g.c > 16 && fx_chunk_join() && !env_default_off("PBF_MSM_CD_QUAD") &&
+                     env_default_on("PBF_MSM_HEAVY_JOIN") && env_default_on("PBF_MSM_CD_RESOLVE") &&
+                     env_default_on("PBF_MSM_DEFER_CONV");  // read per call: A/B knobs
+  const uint32_t hmax = defer ? HJ_MAX : 0u;
+  if (rawf) {
     if ((rc = braw.ensure((uint64_t)NB * 144))) return rc;
     hipLaunchKernelGGL(msm_chunk_acc_l29r, dim3((nchunks + 255) / 256), dim3(256), 0, s, table,
                        (const uint32_t*)keys2.p, (const uint32_t*)vals2.p, (const uint32_t*)start.p,
@@ -1603,7 +1621,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
     hipLaunchKernelGGL(msm_l29_finish, dim3(grid1((uint64_t)NB + 2ull * nchunks)), dim3(256), 0, s,
                        (const uint32_t*)braw.p, (Xyzz*)buckets.p, (ChunkPart*)head.p, (ChunkPart*)tail.p,
                        (const uint32_t*)hk.p, (const uint32_t*)tk.p, (const uint32_t*)start.p, (const uint32_t*)end.p,
-                       NB, nchunks, NB);
+                       NB, nchunks, NB, hmax);
   } else {
     hipLaunchKernelGGL(msm_l29() ? msm_chunk_acc_l29 : msm_chunk_acc, dim3((nchunks + 255) / 256), dim3(256), 0, s,
                        table, (const uint32_t*)keys2.p, (const uint32_t*)vals2.p, (const uint32_t*)start.p,
@@ -1648,7 +1666,7 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
       hipLaunchKernelGGL(msm_heavy_list, dim3(NB / 256), dim3(256), 0, a, (const uint32_t*)start.p,
                          (const uint32_t*)end.p, NB, cap, HJ_MAX, (uint32_t*)hl.p, cnt);
       hipLaunchKernelGGL(msm_join_heavy, dim3(1024), dim3(256), 0, a, (ChunkPart*)head.p, (const uint32_t*)hl.p,
-                         (const uint32_t*)cnt, (const uint32_t*)start.p, (const uint32_t*)end.p);
+                         (const uint32_t*)cnt, (const uint32_t*)start.p, (const uint32_t*)end.p, (uint32_t)defer);
     }
     // (with the heavy join the tree steps take only the buckets spanning more than HJ_MAX chunks
     // -- skewed scalars -- and exit at once when there are none)
@@ -1696,7 +1714,8 @@ int msm_fixed_device(pbf_ctx* ctx, const Affine* table, uint64_t n_table, uint64
       const bool res = env_default_on("PBF_MSM_CD_RESOLVE");  // read per call: an A/B knob
       if (res)
         hipLaunchKernelGGL(msm_fx_resolve, dim3(NB / 256), dim3(256), 0, a, (Xyzz*)buckets.p, (const ChunkPart*)head.p,
-                           (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, NB, cap_seq);
+                           (const ChunkPart*)tail.p, (const uint32_t*)start.p, (const uint32_t*)end.p, NB, cap_seq,
+                           hmax);
       const bool s32 = env_default_off("PBF_MSM_CD_SEQ32");  // read per call: an A/B knob
       auto* cdk = s32 ? (res ? msm_fxg_cd_seq<32, true> : msm_fxg_cd_seq<32, false>)
                       : (res ? msm_fxg_cd_seq<8, true> : msm_fxg_cd_seq<8, false>);
