@@ -370,3 +370,32 @@ def test_fixed_base_heavy_buckets(ctx, monkeypatch, c):
         want = ctx.msm_g1_dev(pts.data_ptr(), ds.data_ptr(), m)
         assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want, c
     ctx.release_caches()
+
+
+@pytest.mark.parametrize("knob", ["PBF_MSM_CD_RESOLVE=0", "PBF_MSM_HEAVY_JOIN=0", "PBF_MSM_DEFER_CONV=0",
+                                  "PBF_MSM_CD_SEQ32=1", "PBF_MSM_CHUNK_JOIN=0"])
+def test_wide_tail_forms_agree(ctx, monkeypatch, knob):
+    """The round-5 wide-window tail (buckets resolved once, heavy buckets joined by lane groups,
+    partials converted as read) against its A/B forms: c = 22, random scalars (light buckets,
+    the narrow top window's heavy ones) and small scalars (a few thousand heavy buckets), each
+    form equal to the windowed MSM."""
+    import torch
+
+    monkeypatch.setenv("PBF_MSM_FX_C", "22")
+    m = 1 << 17
+    t = bn254.random_limbs(m, 900)
+    dt = torch.from_numpy(t.view(np.int64)).cuda()
+    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
+    ctx.g1_mul_base_dev(dt.data_ptr(), pts.data_ptr(), m)
+    rng = np.random.default_rng(901)
+    small = np.zeros((m, 4), dtype=np.uint64)
+    small[:, 0] = rng.integers(0, 1 << 40, size=m, dtype=np.uint64)
+    for sc in (bn254.random_limbs(m, 902), small):
+        ds = torch.from_numpy(np.ascontiguousarray(sc).reshape(-1).view(np.int64)).cuda()
+        want = ctx.msm_g1_dev(pts.data_ptr(), ds.data_ptr(), m)
+        assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want
+        name, val = knob.split("=")
+        monkeypatch.setenv(name, val)
+        assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want, knob
+        monkeypatch.delenv(name)
+    ctx.release_caches()
