@@ -124,7 +124,11 @@ struct ForkSet {
   // fork, flags[i] join of stream i, each set to the call's sequence number
   uint64_t* flags = nullptr;
   uint64_t seq = 0;
+  // counters of the work-queue schedule (ntt_gl.hpp ntt_gl_queue_kernel): zero between launches
+  uint32_t* qctr = nullptr;
+  size_t qctr_n = 0;
   int ensure(int streams);               // streams 1..streams-1 and the event pair exist
+  int ensure_q(size_t n);                // >= n zeroed queue counters
   ~ForkSet();
 };
 

@@ -221,6 +221,21 @@ __device__ __forceinline__ void gl_bar() {
 
 constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
 
+// Global access forms of the work-queue schedule's hand-off (ntt_gl_queue_kernel): an `sc1`
+// (write-through) store leaves the XCD's L2 as it is written, an `sc1` load bypasses the CU's
+// L1 (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility": relaxed agent-
+// scope atomics lower to exactly these). Plain otherwise.
+template <bool SC1>
+__device__ __forceinline__ void gl_st(uint64_t* p, uint64_t v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1>
+__device__ __forceinline__ uint64_t gl_ld(const uint64_t* p) {
+  if constexpr (SC1) return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
 // One tile: stages A, B, C and the stores. PERSIST: the tile's raw input is already in LDS
 // (lds[r*W + w]); after stage C has consumed the exchange buffer and its twiddles, the
 // next tile `next` is LDS-DMA'd into it while the C-point DFTs and the stores run.
@@ -230,7 +245,9 @@ constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
 // stores 512-B runs (a wave covers 8 k x 8 j). FIRST && BLK: blocked store; !FIRST &&
 // BLK: blocked load.
 // RG (regrouped 2^24 plan, gl_rg2_tile below): 1 = its first pass, 3 = its last pass.
-template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false, int RG = 0>
+// PUB (work-queue schedule, ntt_gl_queue_kernel): >= 1 the first pass stores `sc1`; 2 the later
+// pass loads its input `sc1` too.
+template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false, int RG = 0, int PUB = 0>
 __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t,
                                         uint32_t next) {
   using Sh = GlShape<LOGR, TILE>;
@@ -265,7 +282,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
       else if constexpr (BLK && !FIRST)
         v[u * 4 + s1] = in[(uint64_t)kb * TILE + r * W + w];
       else
-        v[u * 4 + s1] = in[(j0 + w) + (uint64_t)r * stride];
+        v[u * 4 + s1] = gl_ld<!FIRST && PUB == 2>(in + (j0 + w) + (uint64_t)r * stride);
     }
   }
   // RG 3: the stage-B general twiddle T3[q1][a0][j] (a0 = r2 + 4 s2), loaded now (in flight
@@ -514,7 +531,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
         for (int k2 = 0; k2 < C; ++k2)
           if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
-            o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
+            gl_st<(PUB >= 1)>(o + base + k1 + 64 * k2, x[u * C + bitrev_c(k2, LOGC)]);
       }
     }
   } else {
@@ -586,6 +603,97 @@ ntt_gl_dual_kernel(GlPassArgs second, GlPassArgs first) {
     gl_tile<LOGR, E64, true, TILE, false>(first, lds, tile, first.blocks_per_poly * first.batch, threadIdx.x, 0);
   else
     gl_tile<LOGR, E64, false, TILE, false>(second, lds, tile, second.blocks_per_poly * second.batch, threadIdx.x, 0);
+}
+
+// ---- work-queue schedule of a two-pass plan (round 6) -----------------------------------
+// Both passes of a whole batch in ONE launch, one tile per workgroup, so pass 1 of one
+// polynomial group runs beside pass 2 of the group before it without a second stream, a
+// fork/join or a kernel boundary between the passes. The batch is cut into groups of G
+// polynomials; the work is a sequence of classes, each one pass of one group:
+//   P1(0) .. P1(L-1), then P1(g+L), P2(g) for g = 0 .., then the last P2s   (lag L groups)
+// dealt to 8 queues (queue x = blockIdx mod 8: the blocks that share an XCD), each queue
+// holding 1/8 of every class in the same order: item i of a class in queue x is tile
+// 8 i + x of that pass (XCD k-major tile coordinates, gl_tile_coords 1). A workgroup takes the
+// next item of its queue with one atomic add, so items start in queue order whatever the
+// dispatch order. P2(g) waits until all of P1(g)'s tiles have been published; P1 tiles wait
+// for nothing, and every P1 tile a P2 item needs sits earlier in every queue, so each wait
+// ends (the items it waits on were taken by running workgroups).
+// Hand-off (MI355X_MICROARCH.md "inter-workgroup visibility", Valid forms): every storing wave
+// waits vmcnt(0), a workgroup barrier, then one lane publishes: PUB 0 plain stores + agent
+// release fence before the counter add; PUB 1/2 write-through (`sc1`) stores, no fence. The
+// consumer polls the counter with relaxed agent-scope loads (`sc1`), then PUB 0/1 one agent
+// acquire, PUB 2 none (its input loads are `sc1` too), a barrier, then the tile.
+// Counters (ctr, u32): [0, 8) queue heads, [8] finished workgroups, [9 + g] P1 tiles of group g
+// published. The last workgroup to finish zeroes them for the next launch (after every other
+// workgroup's last counter access: each finishes its own returning adds first).
+struct GlQueueArgs {
+  GlPassArgs p1, p2;  // group 0's passes (batch = G polynomials, XCD k-major tiles)
+  uint32_t* ctr;
+  uint64_t in_gs, scr_gs, out_gs;  // elements from one group to the next: input, scratch, output
+  uint32_t per_class;              // items per queue per class (G x tiles per polynomial / 8)
+  uint32_t groups, lag, total;     // total = workgroups of the launch = items
+};
+
+template <int LOGR, int E64, int TILE, int PUB>
+__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_gl_queue_kernel(GlQueueArgs q) {
+  gl_shape_checks<LOGR, TILE>();
+  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
+  __shared__ uint32_t s_pos;
+  const int t = threadIdx.x;
+  const uint32_t x = blockIdx.x & 7;
+  if (t == 0) s_pos = __hip_atomic_fetch_add(q.ctr + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t pos = s_pos;
+  const uint32_t c = pos / q.per_class, i = pos % q.per_class;
+  // class c -> (pass, group)
+  const uint32_t L = q.lag < q.groups ? q.lag : q.groups, pairs = q.groups - L;
+  bool second;
+  uint32_t g;
+  if (c < L) {
+    second = false, g = c;
+  } else if (c - L < 2 * pairs) {
+    const uint32_t k = c - L;
+    second = (k & 1) != 0, g = (k >> 1) + ((k & 1) ? 0 : L);
+  } else {
+    second = true, g = pairs + (c - L - 2 * pairs);
+  }
+  const uint32_t tiles = q.per_class * 8, tile = i * 8 + x;
+  if (!second) {
+    GlPassArgs a = q.p1;
+    a.in += g * q.in_gs;
+    a.out += g * q.scr_gs;
+    gl_tile<LOGR, E64, true, TILE, false, false, 0, PUB>(a, lds, tile, tiles, t, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+    __syncthreads();
+    if (t == 0) {
+      if constexpr (PUB == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      (void)__hip_atomic_fetch_add(q.ctr + 9 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add has landed before the finish add
+    }
+  } else {
+    if (t == 0) {
+      while (__hip_atomic_load(q.ctr + 9 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tiles)
+        __builtin_amdgcn_s_sleep(8);
+      if constexpr (PUB < 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    GlPassArgs a = q.p2;
+    a.in += g * q.scr_gs;
+    a.out += g * q.out_gs;
+    gl_tile<LOGR, E64, false, TILE, false, false, 0, PUB>(a, lds, tile, tiles, t, 0);
+  }
+  if (t == 0) {
+    const uint32_t f = __hip_atomic_fetch_add(q.ctr + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (f + 1 == q.total) {
+      for (uint32_t k = 0; k < 9 + q.groups; ++k)
+        __hip_atomic_store(q.ctr + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ---- regrouped 2^24 plan (DESIGN.md §3.1 "Regrouped twiddles") --------------------------

@@ -628,8 +628,27 @@ int ForkSet::ensure(int streams) {
   return 0;
 }
 
+int ForkSet::ensure_q(size_t n) {
+  if (n <= qctr_n) return 0;
+  if (qctr) {
+    PBF_HIP(hipDeviceSynchronize());  // a launch still using the old counters
+    PBF_HIP(hipFree(qctr));
+    qctr = nullptr;
+    qctr_n = 0;
+  }
+  PBF_HIP(hipMalloc((void**)&qctr, n * sizeof(uint32_t)));
+  PBF_HIP(hipMemset(qctr, 0, n * sizeof(uint32_t)));
+  PBF_HIP(hipDeviceSynchronize());
+  qctr_n = n;
+  return 0;
+}
+
 ForkSet::~ForkSet() {
   (void)hipSetDevice(device);
+  if (qctr) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(qctr);
+  }
   for (int i = 1; i < GL_MAX_STREAMS; ++i) {
     if (aux[i]) {
       (void)hipStreamSynchronize(aux[i]);
@@ -695,8 +714,72 @@ static int run_gl_dual(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, 
   return rc;
 }
 
+// Work-queue schedule (ntt_gl.hpp ntt_gl_queue_kernel): both passes of an equal-radix two-pass
+// plan for the whole batch in one launch on the caller's stream. Returns -1 when the plan or
+// batch has no queue form (the caller falls back to the stream schedule).
+typedef void (*GlQueueFn)(GlQueueArgs);
+template <int E>
+static GlQueueFn gl_fn_queue(int logr, int tile, int pub) {
+#define PBF_GL_Q(LR, T)                                                                                      \
+  if (logr == LR && tile == T)                                                                               \
+    return pub == 0 ? ntt_gl_queue_kernel<LR, E, T, 0> : pub == 1 ? ntt_gl_queue_kernel<LR, E, T, 1>        \
+                                                                   : ntt_gl_queue_kernel<LR, E, T, 2>;
+  PBF_GL_Q(10, 8192)
+  PBF_GL_Q(9, 4096)
+  PBF_GL_Q(8, 4096)
+#undef PBF_GL_Q
+  return nullptr;
+}
+
+static int run_gl_queue(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
+                        DevBuf& s1, hipStream_t stream, ForkSet* fork) {
+  if (!fork || p.logr.size() != 2 || p.logr[0] != p.logr[1] || p.r4k || gl_pad(p) || getenv("PBF_NTT_BLK") ||
+      getenv("PBF_NTT_PERSIST") || getenv("PBF_NTT_NO_PRETW"))
+    return -1;
+  const int tile = gl_tile(p.logr[0]);
+  const char* pe = getenv("PBF_NTT_QPUB");
+  const int pub = pe ? atoi(pe) : 1;
+  const GlQueueFn fn = p.e64 == 39 ? gl_fn_queue<39>(p.logr[0], tile, pub) : gl_fn_queue<153>(p.logr[0], tile, pub);
+  if (!fn) return -1;
+  size_t G = batch % 4 == 0 ? 4 : (batch % 2 == 0 ? 2 : 1);
+  if (const char* g = getenv("PBF_NTT_QG")) {
+    const size_t v = (size_t)atoll(g);
+    if (v >= 1 && batch % v == 0) G = v;
+  }
+  const uint64_t T = p.n / (uint64_t)tile;  // tiles per polynomial and pass
+  if ((G * T) % 8 || batch * T * 2 > 0x7fffffffull) return -1;
+  std::vector<GlLaunch> L;
+  int rc = run_gl_group(p, d_in, d_out, G, s0, s1, stream, 0, 0, &L);
+  if (rc) return rc;
+  if (L.size() != 2 || L[0].lds || L[1].lds || L[0].block != L[1].block || !L[0].a.post_tw || !L[1].a.skip_pass_tw)
+    return -1;
+  const size_t groups = batch / G;
+  if ((rc = fork->ensure_q(9 + groups))) return rc;
+  GlQueueArgs q;
+  q.p1 = L[0].a;
+  q.p2 = L[1].a;
+  q.p1.xcd_kmajor = q.p2.xcd_kmajor = 1;
+  q.ctr = fork->qctr;
+  q.in_gs = q.out_gs = G * p.n;
+  q.scr_gs = G * gl_pitch(p);
+  q.per_class = (uint32_t)(G * T / 8);
+  q.groups = (uint32_t)groups;
+  const char* le = getenv("PBF_NTT_QLAG");
+  q.lag = le ? (uint32_t)atoi(le) : 1;
+  if (q.lag < 1) q.lag = 1;
+  q.total = (uint32_t)(2 * batch * T);
+  hipLaunchKernelGGL(fn, dim3(q.total), dim3(L[0].block), 0, stream, q);
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
+
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
+  // round 6 default: the work-queue schedule (one launch, no second stream) for batches of >= 2
+  if (split_log == 0 && batch >= 2 && !env_default_off("PBF_NTT_NO_QUEUE") && !getenv("PBF_NTT_DUAL")) {
+    const int rc = run_gl_queue(p, d_in, d_out, batch, s0, s1, stream, fork);
+    if (rc != -1) return rc;
+  }
   // default schedule (measured best at 2^20 x 32): groups of 4
   // polynomials alternating over two streams once the batch has at least 8
   size_t G = batch >= 8 ? 4 : batch;
