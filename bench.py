@@ -253,9 +253,7 @@ def live_traffic(log_n: int, batch: int, steps: int = 6, fetch_scale: float = 1.
     tmp = tempfile.mkdtemp(prefix="pbf_traffic_", dir="/tmp")
     child = [sys.executable, os.path.abspath(__file__), "--steps", str(steps), "--warmup", "0", "--no-cpu",
              "--no-extra", "--no-traffic", "--log-n", str(log_n), "--batch", str(batch)]
-    # events for the NTT's stream fork / join in the profiled child (the library also switches to
-    # them under counter collection: the profiler serialises the queues a flag wait spans)
-    env = dict(os.environ, TMPDIR="/tmp", PBF_NTT_EVENTS="1")
+    env = dict(os.environ, TMPDIR="/tmp")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", tmp, "-o", counter.lower(), "--"] + child
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -408,7 +406,7 @@ def main() -> int:
                                    + (f" per GPU (global n = {world} x 2^{args.log_n}, stride-sharded)"
                                       if world > 1 else ""),
                        "n_per_gpu": n_local, "n_global": n_global, "batch": B,
-                       "passes": os.environ.get("PBF_NTT_PASSES", "default")},
+                       "passes": "default (2^20: 10,10)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.log_n, B),
                          "kernel": "ntt_gl_pass_kernel (all passes of one batched NTT, HIP events on the launch "

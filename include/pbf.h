@@ -17,8 +17,9 @@
  *     hipStream_t (void*) and are stream-ordered on that stream (NULL = the HIP null
  *     stream, as everywhere in HIP): their work starts after everything enqueued on
  *     it before the call and finishes before anything enqueued after. Two entry points
- *     also use streams private to the context, always joined back by events on the
- *     caller's stream before they return: a batched Goldilocks NTT of >= 8 polynomials
+ *     also use streams private to the context, always joined back by events (waits in
+ *     the command processor, never a spinning kernel) on the caller's stream before
+ *     they return: a batched Goldilocks NTT of >= 8 polynomials
  *     (pbf_ntt_u64_batch_dev) forks half its groups onto a second stream, and the
  *     fixed-base MSM (pbf_msm_g1_bn254_fixed_dev, and the commitments inside
  *     pbf_plonk_prove_bn254*) runs its bucket join and reduction on a side stream while
@@ -63,6 +64,28 @@ const char* pbf_last_error(void);
 /* Stream used by the synchronous host-pointer entry points (default: a private
  * non-blocking stream created with the context). `_dev` calls ignore it.     */
 int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream);
+/* Context options: select among product code paths of this context (never read from the
+ * environment). `value` NULL removes the option; unknown names return PBF_EINVAL. Every
+ * option gives the same results, bit for bit; they exist for cross-checks and tuning:
+ *   ntt.passes     "a,b,..."  radix bits per pass of u64 NTT plans (each 6..12, sum log2 n)
+ *   ntt.group      G          polynomials per group of a batched Goldilocks NTT (0: one group)
+ *   ntt.streams    k          streams the groups rotate over (1: the caller's stream only)
+ *   ntt.twmax_log  L          per-pass twiddle tables up to 2^L entries (default 24)
+ *   ntt.twsplit    1 / 0      last pass: force the split table / keep the two-level table
+ *   ntt.no_rg      1          2^24: the round-2 passes instead of the regrouped plan
+ *   ntt256.maxr    4..9       largest radix (bits) of the 256-bit NTT passes (default 9)
+ *   ntt256.twlog   L          256-bit per-pass twiddle tables up to 2^L entries (default 26)
+ *   msm.fx_c       16/20/22   fixed-base MSM window bits (default by size)
+ *   g1.mul_base    "daa"      G1 fixed-base products by double-and-add instead of the comb
+ *   pair.engine    "lane"/"wg" pairing engine (default: lanes from 4096 pairings)
+ *   pair.lane_wpe  1 / 2      lane engine built for 1 or 2 waves per SIMD (default by size)
+ *   prover.pk      0          no proving-key cache: every proof recomputes the preprocessed
+ *                             polynomials, as the reference does (plonk.rs:233-243, 339-370)
+ *   prover.timing  1          synchronise at every prover round mark (per-round times)
+ *   verifier.vk    0          no verification-key cache
+ * Options are read when used; an ntt* option also drops the context's cached NTT plans (after a
+ * device synchronisation), which are rebuilt under the new value. */
+int pbf_ctx_set_option(pbf_ctx* ctx, const char* name, const char* value);
 int pbf_device_sync(pbf_ctx* ctx);
 /* Frees the context's derived caches -- the prover's proving key, the verifier's
  * verification key, the fixed-base MSM window table, the pairing check's prepared lines

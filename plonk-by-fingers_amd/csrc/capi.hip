@@ -31,6 +31,7 @@ int pbf_ctx::plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan**
   if (it != plans.end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<NttPlan> p(new NttPlan());
   PBF_HIP(hipSetDevice(device));
+  p->opts = options;
   int rc = make_plan(m, omega, n, inverse ? 1 : 0, p.get());
   if (rc) return rc;
   *out = p.get();
@@ -120,6 +121,29 @@ int pbf_ctx_release_caches(pbf_ctx* ctx) {
   ctx->snap_words.clear();
   ctx->snap_gen.clear();
   ctx->snap_used.clear();
+  return PBF_OK;
+}
+
+// Context options (include/pbf.h): a value replaces the previous one, NULL removes the option.
+// Cached NTT plans were built under the old options, so an ntt* option drops them (after the
+// device has finished with them) and they are rebuilt on next use.
+int pbf_ctx_set_option(pbf_ctx* ctx, const char* name, const char* value) {
+  if (!ctx || !name || !*name) return fail(PBF_EINVAL, "null argument");
+  static const char* const known[] = {"ntt.passes",  "ntt.group",       "ntt.streams",   "ntt.twmax_log",
+                                      "ntt.twsplit", "ntt.no_rg",       "ntt256.maxr",   "ntt256.twlog",
+                                      "msm.fx_c",    "g1.mul_base",     "pair.engine",   "pair.lane_wpe",
+                                      "prover.pk",   "prover.timing",   "verifier.vk"};
+  bool ok = false;
+  for (const char* k : known) ok = ok || strcmp(k, name) == 0;
+  if (!ok) return fail(PBF_EINVAL, std::string("unknown option ") + name);
+  if (value) ctx->options.kv[name] = value;
+  else ctx->options.kv.erase(name);
+  if (strncmp(name, "ntt", 3) == 0) {
+    PBF_HIP(hipSetDevice(ctx->device));
+    PBF_HIP(hipDeviceSynchronize());
+    ctx->plans.clear();
+    pbf_internal_drop_plans256(ctx);
+  }
   return PBF_OK;
 }
 

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -137,6 +138,10 @@ struct Group {
   std::vector<hipStream_t> stream;  // per rank, the stream of the current call
   std::vector<RankComm> rc;
   std::unique_ptr<Barrier> bar;
+  // post_mu[r]: held by rank r's thread while it is inside RCCL calls on its communicator
+  // (group start .. group end, all-gather), and by abort_all while it aborts that communicator,
+  // so no communicator is aborted (freed) while its rank's thread is using it
+  std::unique_ptr<std::timed_mutex[]> post_mu;
   size_t capacity = 0;
 
   ~Group() {
@@ -153,13 +158,21 @@ struct Group {
   }
   // a rank failed: release every rank waiting on a host barrier and every collective in flight
   // (ncclCommAbort unblocks peers whose partner never posts its half); the group is then dropped
-  // by group_for. Ranks check `broken` before posting, so none posts on an aborted communicator
-  // once the flag is seen.
+  // by group_for. `broken` is set first, and a rank checks it under its post_mu before posting,
+  // so once abort_all holds post_mu[g], rank g is outside RCCL and never posts again: its
+  // communicator is aborted with no other thread inside it. A rank still inside a blocking RCCL
+  // call after 5 s (a rendezvous whose partner failed) is aborted anyway, which is how a blocked
+  // NCCL / RCCL call is released (the communicator is not freed under the abort of its own
+  // call: the stand-in, tests/native/fake_rccl.cpp, keeps that contract too).
   void abort_all() {
     if (bar) bar->abort();
     if (!use_rccl || broken.exchange(true)) return;
-    for (nccl_comm_t c : nccl)
-      if (c) (void)R->comm_abort(c);
+    for (uint32_t g = 0; g < G; ++g) {
+      if (!nccl[g]) continue;
+      std::unique_lock<std::timed_mutex> l(post_mu[g], std::defer_lock);
+      (void)l.try_lock_for(std::chrono::seconds(5));
+      (void)R->comm_abort(nccl[g]);
+    }
   }
   std::vector<int> devs;
   int ctx_device(uint32_t g) const { return devs[g]; }
@@ -201,6 +214,7 @@ struct Group {
       rc.push_back(RankComm{this, g});
     }
     bar.reset(new Barrier(G));
+    post_mu.reset(new std::timed_mutex[G]);
     return 0;
   }
   int ensure(size_t bytes) {
@@ -241,6 +255,8 @@ struct Group {
   int all_to_all(uint32_t r, size_t b) {
     if (!use_rccl) return copy_exchange(r, b, false);
     if (int rc = rccl_ready()) return rc;
+    std::lock_guard<std::timed_mutex> l(post_mu[r]);
+    if (broken) return fail(PBF_ECOMM, "multi-GPU group: a rank failed");
     nccl_result_t e = R->group_start();
     for (uint32_t g = 0; g < G && !e; ++g) {
       if ((e = R->send((const char*)send[r].p + (size_t)g * b, b, NCCL_UINT8, (int)g, nccl[r], stream[r]))) break;
@@ -253,6 +269,8 @@ struct Group {
   int all_gather(uint32_t r, size_t b) {
     if (!use_rccl) return copy_exchange(r, b, true);
     if (int rc = rccl_ready()) return rc;
+    std::lock_guard<std::timed_mutex> l(post_mu[r]);
+    if (broken) return fail(PBF_ECOMM, "multi-GPU group: a rank failed");
     const nccl_result_t e = R->all_gather(send[r].p, recv[r].p, b, NCCL_UINT8, nccl[r], stream[r]);
     if (e) return fail(PBF_ECOMM, std::string("ncclAllGather: ") + R->err(e));
     return 0;

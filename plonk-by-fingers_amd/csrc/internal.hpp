@@ -20,16 +20,43 @@ static const uint64_t GOLDILOCKS = 0xFFFFFFFF00000001ull;
 enum FieldKind { FIELD_GOLDILOCKS = 0, FIELD_MOD32 = 1 };
 
 void set_error(const std::string& s);
-// A/B switch that is on by default: off only when the variable parses as the integer 0
-// ("0", "00"); unset, empty or any other value keeps it on. Read per call.
+
+// Context options (pbf_ctx_set_option, include/pbf.h): named string values that select among
+// product code paths (plan shapes, schedules, the proving-key and verification-key caches),
+// set per context by the caller. The library never reads them from the environment, so a
+// stray variable cannot change what a context computes or how. A plan
+// keeps a copy of its context's options from when it was built.
+struct Options {
+  std::map<std::string, std::string> kv;
+  const char* get(const char* name) const {
+    auto it = kv.find(name);
+    return it == kv.end() ? nullptr : it->second.c_str();
+  }
+  long long num(const char* name, long long dflt) const {
+    const char* v = get(name);
+    return v && *v ? atoll(v) : dflt;
+  }
+};
+
+// A/B switches of measured-negative or diagnostic variants kept for experiments: read from the
+// environment ONLY in the A/B build (make ab: -DPBF_AB, libpbf_ab.so). The product build
+// compiles them to their defaults and ignores the environment.
+inline const char* ab_env(const char* name) {
+#ifdef PBF_AB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+// A/B switch that is on by default: off only when the variable parses as the integer 0.
 inline bool env_default_on(const char* name) {
-  const char* e = getenv(name);
+  const char* e = ab_env(name);
   return !(e && *e && atoi(e) == 0);
 }
-// A/B switch that is off by default: on only when the variable parses as a nonzero integer
-// ("1"); unset, empty or "0" keeps it off. Read per call.
+// A/B switch that is off by default: on only when the variable parses as a nonzero integer.
 inline bool env_default_off(const char* name) {
-  const char* e = getenv(name);
+  const char* e = ab_env(name);
   return e && *e && atoi(e) != 0;
 }
 int fail(int code, const std::string& s);
@@ -75,9 +102,9 @@ struct NttPlan {
   FieldArgs fa{};
   uint32_t log_n = 0;
   uint64_t n_inv = 1;
+  Options opts;            // the context's options when the plan was built
   std::vector<int> logr;   // radix per pass (empty => small kernel)
   int e64 = -1;            // w_64 = 2^e64 for a standard Goldilocks root, else -1
-  DevBuf twfull;           // w^m for m < n (A/B only, PBF_NTT_TWFULL)
   std::vector<std::shared_ptr<DevBuf>> twpass;  // per-pass [r][k] twiddles (empty buffer => two-level)
   int w = 16;              // columns per workgroup
   uint32_t tw_bits = 0;
@@ -89,27 +116,15 @@ struct NttPlan {
   // (A: R x W, B: Ns/W x R; null when unused), W = tws_w columns per tile
   std::shared_ptr<DevBuf> tws_a, tws_b;
   int tws_w = 0;
-  // round-3 schedule (ntt_ip.hpp): in-place digit slots, persistent prefetching passes;
-  // ip_r = radix bits per pass (top slot first), per-pass twiddle and stage-C tables
   // regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel): 8,8,8 passes with the general
   // twiddles between 64-point blocks only; tables tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18),
-  // t3[f][a0][j] (2^24, n^-1 folded in for the inverse)
-  // rg: the plan qualifies; the tables (~130 MiB, mostly t3) are built the first time a run
-  // takes the regrouped path (ntt_launch.hip ensure_rg_tables), never for runs that cannot
+  // and the last pass's geometric factors C[r2][X], D[X] (X < 2^18, n^-1 folded into C for the
+  // inverse). rg: the plan qualifies; the tables (~12 MiB) are built the first time a run takes
+  // the regrouped path (ntt_launch.hip ensure_rg_tables), never for runs that cannot
   bool rg = false;
   mutable bool rg_built = false;
-  mutable DevBuf rg_tc1, rg_t2, rg_t3;
-  mutable DevBuf rg_tgc, rg_tgb;  // geometric last-pass twiddles (PBF_NTT_T3GEO): [r2][X], [X]
-  mutable DevBuf rg_t2d;          // middle pass: w^(16384 a1), a1 < 64 (PBF_NTT_T2GEO)
-  // two-pass 4096 x 4096 plan for 2^24-point standard-root transforms (ntt_r4k.hpp; opt-in
-  // PBF_NTT_R4K=1): stage tables of both passes and the inter-pass [j][k] table, built lazily
-  bool r4k = false;
-  mutable bool r4k_built = false;
-  mutable DevBuf r4k_tst1, r4k_tst2, r4k_post;
-  bool ip = false;
-  std::vector<int> ip_r;
-  std::vector<std::shared_ptr<DevBuf>> ip_tw, ip_tc;
-  std::shared_ptr<DevBuf> ip_twa;  // row pass TA[x][w] (split form), null: full T[K][x]
+  mutable DevBuf rg_tc1, rg_t2;
+  mutable DevBuf rg_tgc, rg_tgb;
 };
 
 // Extra streams and events of the multi-stream NTT group schedule (ntt_launch.hip
@@ -120,15 +135,7 @@ struct ForkSet {
   int device = 0;
   hipStream_t aux[GL_MAX_STREAMS] = {};  // aux[0] unused: slot 0 is the caller's stream
   hipEvent_t fork = nullptr, join[GL_MAX_STREAMS] = {};
-  // stream memory operations instead of events (default; PBF_NTT_EVENTS=1 for events): flags[0]
-  // fork, flags[i] join of stream i, each set to the call's sequence number
-  uint64_t* flags = nullptr;
-  uint64_t seq = 0;
-  // counters of the work-queue schedule (ntt_gl.hpp ntt_gl_queue_kernel): zero between launches
-  uint32_t* qctr = nullptr;
-  size_t qctr_n = 0;
   int ensure(int streams);               // streams 1..streams-1 and the event pair exist
-  int ensure_q(size_t n);                // >= n zeroed queue counters
   ~ForkSet();
 };
 
@@ -159,8 +166,6 @@ struct MsmTail {
   ~MsmTail();  // waits for the side streams (declared after the buffers they use)
 };
 
-// Round-3 schedule of a plan with p.ip (ntt_ip.hip): the whole batch, scratch s0
-int run_ip(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0, hipStream_t stream);
 // Build a plan (validates omega's order and n^-1). Returns PBF status.
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p);
 // Enqueue a batched transform of a planned size on `stream` (d_in may equal d_out).
@@ -196,6 +201,7 @@ int pairing_check_on_stream(pbf_ctx* ctx, const uint64_t* g1, const uint64_t* g2
 
 struct pbf_ctx {
   int device = 0;
+  pbf::Options options;  // pbf_ctx_set_option
   uint64_t serial = 0;  // creation order (multi-GPU groups match contexts by pointer and serial)
   hipStream_t stream = nullptr;
   hipStream_t user_stream = nullptr;

@@ -15,6 +15,7 @@
 //      (msm_fx_cd / msm_fx_subsets / msm_fx_total, see there)
 //   6. host: Horner over the 16 window sums (2^16 steps), one inversion to affine.
 // The result is a group element, so the canonical affine output is unique.
+#include <cstring>
 #include <vector>
 #include "../../include/pbf.h"
 #include "msm.hpp"
@@ -401,7 +402,7 @@ static bool msm_l29() {
 // per bucket) flushes rarely, and the separate conversion pass costs it more than it saves
 // (2^24 points: 32.5 against 32.0 ms). PBF_MSM_RAWFLUSH=0/1 forces either (A/B).
 static bool msm_rawflush(bool short_runs = true) {
-  const char* e = getenv("PBF_MSM_RAWFLUSH");  // read per call: an A/B knob
+  const char* e = ab_env("PBF_MSM_RAWFLUSH");  // an A/B knob (PBF_AB build only)
   if (e && *e) return atoi(e) != 0;
   return short_runs;
 }
@@ -442,15 +443,14 @@ static FxGeom fx_geom_of(int c) {
   g.hb = c - 1 - g.lb;
   return g;
 }
-// default window width of a table of n points; PBF_MSM_FX_C=16/18/20/22 forces one (A/B; read at
-// the table build). Measured (profiles/r04/msm_window_*): a 2^20-point MSM is fastest at c = 16
+// default window width of a table of n points; option msm.fx_c = 16/18/20/22 forces one (read at
+// the table build: the tests build the wide tables of large sizes at small ones). Measured (profiles/r04/msm_window_*): a 2^20-point MSM is fastest at c = 16
 // (2.27 ms; c = 20: 2.69), 2^22 points at c = 20 (7.60 against 7.71 ms; in the 2^22-gate proof
 // 87.6 against 92.0 ms), 2^24 points at c = 22 (27.2 against 29.0 ms; the 2^24-gate proof 327
 // against 350 ms). Boundaries at the geometric midpoints.
-static int fx_default_c(uint64_t n) {
-  const char* e = getenv("PBF_MSM_FX_C");
-  if (e) {
-    const int v = atoi(e);
+static int fx_default_c(const pbf_ctx* ctx, uint64_t n) {
+  {
+    const int v = (int)ctx->options.num("msm.fx_c", 0);
     if (v == 16 || v == 18 || v == 20 || v == 22) return v;
   }
   if (n >= 3ull << 22) return 22;
@@ -1302,7 +1302,7 @@ static int msm_device(pbf_ctx* ctx, const uint64_t* d_pts, const uint64_t* d_sc,
   hipLaunchKernelGGL(msm_join_rest, dim3(NBT / 256), dim3(256), 0, s, (ChunkPart*)w.head.p,
                      (const uint32_t*)w.start.p, (const uint32_t*)w.end.p, NBT, (const uint32_t*)w.span.p);
   {
-    const char* e = getenv("PBF_MSM_CD_SEQ");  // read per call: an A/B knob
+    const char* e = ab_env("PBF_MSM_CD_SEQ");  // an A/B knob (PBF_AB build only)
     const int v = e ? atoi(e) : 8;
     const int cd_seq = v == 2 || v == 4 || v == 16 ? v : 8;
     auto* fn = cd_seq == 2 ? msm_fx_cd_seq<2> : cd_seq == 4 ? msm_fx_cd_seq<4> : cd_seq == 16 ? msm_fx_cd_seq<16> : msm_fx_cd_seq<8>;
@@ -1401,7 +1401,7 @@ int snapshot_check(pbf_ctx* ctx, const char* consumer, const SnapItem* items, in
 // differ from the ones it was built from, wherever they live); the table's identity flags are
 // kept with it (fixed_base.inf)
 int msm_fixed_table(pbf_ctx* ctx, const uint64_t* d_pts, uint64_t n, hipStream_t s, const Affine** out) {
-  const FxGeom g = fx_geom_of(fx_default_c(n));
+  const FxGeom g = fx_geom_of(fx_default_c(ctx, n));
   if (n == 0 || n > 0x7FFFFFFFull / g.nw) return fail(PBF_EINVAL, "fixed-base MSM: bad point count");
   const SnapItem it{"g1pts", d_pts, 8 * n};
   bool same = false;
@@ -1791,7 +1791,7 @@ int pbf_msm_g1_bn254_dev(pbf_ctx* ctx, const uint64_t* d_points, const uint64_t*
   MsmWork w = msm_work(ctx);
   int rc = msm_device(ctx, d_points, d_scalars, n, s, w);
   if (rc) return rc;
-  if (getenv("PBF_MSM_DEVICE_HORNER")) {
+  if (ab_env("PBF_MSM_DEVICE_HORNER")) {  // A/B (PBF_AB build only)
     DevBuf& res = ctx->buf("msm.horner");
     if ((rc = res.ensure(sizeof(Xyzz)))) return rc;
     hipLaunchKernelGGL(msm_horner_kernel, dim3(1), dim3(64), 0, s, (const Xyzz*)w.sums.p, (Xyzz*)res.p);
@@ -1837,7 +1837,7 @@ int pbf_msm_g1_bn254_fixed_range_dev(pbf_ctx* ctx, const uint64_t* d_points, siz
   const Affine* tbl = nullptr;
   {
     auto& fb = ctx->fixed_base;
-    const FxGeom g = fx_geom_of(fx_default_c(n_points));
+    const FxGeom g = fx_geom_of(fx_default_c(ctx, n_points));
     auto w = ctx->snap_words.find("g1pts");
     if (fb.valid && fb.n == n_points && fb.c == g.c && fb.table.p && w != ctx->snap_words.end() &&
         w->second == 8 * n_points && ctx->snap_used["fx/g1pts"] == ctx->snap_gen["g1pts"]) {
@@ -1876,7 +1876,8 @@ int pbf_g1_bn254_mul_base_dev(pbf_ctx* ctx, const uint64_t* d_scalars, uint64_t*
   if (!ctx || (n && (!d_scalars || !d_out))) return fail(PBF_EINVAL, "null argument");
   if (n == 0) return PBF_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (getenv("PBF_G1_DOUBLE_AND_ADD")) {  // A/B and cross-check of the comb
+  const char* mb = ctx->options.get("g1.mul_base");
+  if (mb && strcmp(mb, "daa") == 0) {  // option: cross-check of the comb (tests)
     hipLaunchKernelGGL(g1_mul_base_kernel, dim3(grid1(n)), dim3(256), 0, st, d_scalars, d_out, (uint64_t)n);
     PBF_HIP(hipGetLastError());
     return PBF_OK;

@@ -324,7 +324,7 @@ static std::vector<U256> h_powers(const U256& w_m, uint64_t count) {
   return t;
 }
 
-static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256* p) {
+static int make_plan256(const pbf::Options& o, const uint64_t* omega, uint64_t n, int inverse, Plan256* p) {
   if (n == 0 || (n & (n - 1))) return fail(PBF_EINVAL, "n must be a power of two");
   uint32_t log_n = 0;
   while ((1ull << log_n) < n) ++log_n;
@@ -346,10 +346,10 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
   if (inverse == 2) p->n_inv = Fr::mul(p->n_inv, Fr::to_mont(Fr::to_mont(Fr::one_plain())));  // n^-1 R
   if (inverse) wm = h_inv(wm);
   if (n <= 2048) return up256(p->small_tw, h_powers(wm, n));
-  // passes of radix <= 2^9 (LDS tile 2048 x 32 B); PBF_NTT256_MAXR (4..9) lowers the largest
-  // radix (A/B: more, lighter passes)
+  // passes of radix <= 2^9 (LDS tile 2048 x 32 B); option ntt256.maxr (4..9) lowers the largest
+  // radix (more, lighter passes: every radix family of the planner, tests/test_ntt_fr256_gpu.py)
   int maxr = 9;
-  if (const char* e = getenv("PBF_NTT256_MAXR")) maxr = atoi(e) < 4 ? 4 : (atoi(e) > 9 ? 9 : atoi(e));
+  if (const char* e = o.get("ntt256.maxr")) maxr = atoi(e) < 4 ? 4 : (atoi(e) > 9 ? 9 : atoi(e));
   const int P = (log_n + maxr - 1) / maxr;
   p->logr.assign(P, log_n / P);
   for (int i = 0; i < (int)(log_n % P); ++i) p->logr[i] += 1;
@@ -359,7 +359,7 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
   // The inverse's n^-1 rides in its last pass's twiddles (every element of a pass with Ns > 1
   // takes one twiddle product, and the pass is linear): tw1s = tw1 n^-1 for the two-level form,
   // the per-pass table scaled likewise; PBF_NTT256_SCALE_PASS=1 keeps the separate product (A/B).
-  p->fold_scale = inverse && !getenv("PBF_NTT256_SCALE_PASS");
+  p->fold_scale = inverse && !ab_env("PBF_NTT256_SCALE_PASS");
   {
     const U256 step = h_pow(wm, 1ull << p->tw_bits);
     std::vector<U256> t1 = h_powers(step, n >> p->tw_bits);
@@ -372,8 +372,8 @@ static int make_plan256(const uint64_t* omega, uint64_t n, int inverse, Plan256*
   }
   // per-pass tables up to 2^tw_log entries (32 B each); larger passes fall back to the two-level
   // tables (one extra Fr product per element). Tables past 2^20 entries are filled on the device.
-  int tw_log = 26;
-  if (const char* e = getenv("PBF_NTT256_TWLOG")) tw_log = atoi(e);
+  int tw_log = 26;  // option ntt256.twlog: the two-level path of larger passes at test sizes
+  if (const char* e = o.get("ntt256.twlog")) tw_log = atoi(e);
   uint64_t ns = 1;
   uint32_t log_ns = 0;
   for (size_t pi = 0; pi < p->logr.size(); ++pi) {
@@ -467,7 +467,7 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
     // mont(x, w R) = x w keeps canonical data canonical through every product, and the adds
     // are the same in both forms -- the first pass's to_mont and the last pass's from_mont
     // (one product per element each) are not needed (conv_* kept for A/B: PBF_NTT256_CONV=1)
-    const bool conv = getenv("PBF_NTT256_CONV") != nullptr;
+    const bool conv = ab_env("PBF_NTT256_CONV") != nullptr;
     a.conv_in = conv && i == 0;
     a.conv_out = conv && i == P - 1;
     a.scale = (p.inverse && i == P - 1 && !p.fold_scale);
@@ -619,7 +619,7 @@ int get_plan256(pbf_ctx* ctx, const uint64_t* omega, uint64_t n, int inverse, Pl
   if (it != plans256().end()) { *out = it->second.get(); return 0; }
   std::unique_ptr<Plan256> p(new Plan256());
   PBF_HIP(hipSetDevice(ctx->device));
-  int rc = make_plan256(omega, n, kind, p.get());
+  int rc = make_plan256(ctx->options, omega, n, kind, p.get());
   if (rc) return rc;
   *out = p.get();
   plans256()[k] = std::move(p);
@@ -666,7 +666,7 @@ int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, si
   if (!ctx || !omega || !out || (!a && la) || (!b && lb)) return fail(PBF_EINVAL, "null argument");
   const size_t n = la + lb;
   Plan256 *fw, *iv;
-  const bool mont = !getenv("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
+  const bool mont = !ab_env("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
   int rc = get_plan256(ctx, omega, n, 0, &fw);
   if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv, mont);
   if (rc) return rc;
@@ -695,14 +695,14 @@ int pbf_mul_ntt_fr256_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* d
                           uint64_t* d_out, size_t n, size_t batch, void* stream) {
   if (!ctx || !omega || !d_a || !d_b || !d_out) return fail(PBF_EINVAL, "null argument");
   Plan256 *fw, *iv;
-  const bool mont = !getenv("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
+  const bool mont = !ab_env("PBF_MUL_NTT_TWO_PRODUCTS");  // A/B: to_mont + product, plain inverse
   int rc = get_plan256(ctx, omega, n, 0, &fw);
   if (!rc) rc = get_plan256(ctx, omega, n, 1, &iv, mont);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   // fused (default past 2048 points): b's forward transform multiplies its last pass's outputs by
   // a's (already in d_out) and stores the product there; PBF_MUL_NTT_NO_FUSE=1: pointwise kernel
-  if (mont && n > 2048 && !getenv("PBF_MUL_NTT_NO_FUSE")) {
+  if (mont && n > 2048 && !ab_env("PBF_MUL_NTT_NO_FUSE")) {
     if ((rc = run256(*fw, (const U256*)d_a, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s))) return rc;
     if ((rc = run256(*fw, (const U256*)d_b, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, s, (const U256*)d_out)))
       return rc;

@@ -66,14 +66,10 @@ struct GlPassArgs {
   uint32_t scaled;         // tc carries n^-1: multiply every element, k1 = 0 / r2 = 0 too
   uint32_t out_split_log;  // != 0: store destination-major [n/S][batch][S] (multi-GPU send layout)
   uint32_t xcd_kmajor;     // XCD-aware column-major block order (pass-twiddle table reuse in L2)
-  uint32_t blk_log;        // BLK first pass: log2 of the blocked layout's block width W2
-  // padded intermediates (PBF_NTT_PAD): element g of a polynomial sits at g + (g >> rows_log)
-  // * pad, polynomials `pitch` elements apart (user buffers: pad 0, pitch n)
-  uint64_t in_pitch, out_pitch;
-  uint32_t in_pad, out_pad, out_rows_log;
-  // two-pass plans (default; PBF_NTT_NO_PRETW=1 for A/B): the first pass multiplies its
-  // outputs by the second pass's twiddle w^(j k) (post_tw = that pass's [r][k] table: r = this
-  // pass's column j, k its output digit) and the second pass skips its own (skip_pass_tw)
+  uint64_t in_pitch, out_pitch;  // elements from one polynomial to the next
+  // two-pass plans: the first pass multiplies its outputs by the second pass's twiddle w^(j k)
+  // (post_tw = that pass's [r][k] table: r = this pass's column j, k its output digit) and the
+  // second pass skips its own (skip_pass_tw)
   const uint64_t* post_tw;
   uint32_t skip_pass_tw;
 };
@@ -185,76 +181,17 @@ __device__ __forceinline__ void gl_tile_coords(const GlPassArgs& a, uint32_t til
   }
 }
 
-// LDS-DMA of one tile's pass input (R rows x W columns, row-major [r][w] image) into
-// `raw`: 16-B chunks, lane-linear LDS destination, per-lane global source.
-template <int LOGR, int TILE>
-__device__ __forceinline__ void gl_tile_dma(uint64_t* raw, const GlPassArgs& a, uint32_t tile, uint32_t tiles,
-                                            int t) {
-  using Sh = GlShape<LOGR, TILE>;
-  uint32_t poly, kb;
-  gl_tile_coords(a, tile, tiles, &poly, &kb);
-  const uint64_t* in = a.in + (uint64_t)poly * a.n + (uint64_t)kb * Sh::W;
-  const uint64_t stride = a.n >> LOGR;
-  const int wave = t >> 6, lane = t & 63;
-#pragma unroll
-  for (int i = 0; i < TILE / 2 / Sh::NT; ++i) {
-    const int q0 = wave * 64 + i * Sh::NT;  // first chunk of this wave-instruction
-    const int q = q0 + lane;
-    const int row = q / (Sh::W / 2), col = 2 * (q % (Sh::W / 2));
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(in + col + (uint64_t)row * stride),
-                                     (__attribute__((address_space(3))) void*)(raw + 2 * q0), 16, 0, 0);
-  }
-}
-
-// Workgroup barrier. PERSIST kernels keep an LDS-DMA in flight across the tile's stages,
-// so they use a raw s_barrier after lgkmcnt(0): __syncthreads() would also wait vmcnt(0)
-// and drain the DMA and the previous tile's stores.
-template <bool PERSIST>
-__device__ __forceinline__ void gl_bar() {
-  if constexpr (PERSIST) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  } else {
-    __syncthreads();
-  }
-}
-
 constexpr int GL_STORES = 16;  // global stores per thread per tile (NSUB_C * C)
 
-// Global access forms of the work-queue schedule's hand-off (ntt_gl_queue_kernel): an `sc1`
-// (write-through) store leaves the XCD's L2 as it is written, an `sc1` load bypasses the CU's
-// L1 (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility": relaxed agent-
-// scope atomics lower to exactly these). Plain otherwise.
-template <bool SC1>
-__device__ __forceinline__ void gl_st(uint64_t* p, uint64_t v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
-template <bool SC1>
-__device__ __forceinline__ uint64_t gl_ld(const uint64_t* p) {
-  if constexpr (SC1) return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
-}
-
-// One tile: stages A, B, C and the stores. PERSIST: the tile's raw input is already in LDS
-// (lds[r*W + w]); after stage C has consumed the exchange buffer and its twiddles, the
-// next tile `next` is LDS-DMA'd into it while the C-point DFTs and the stores run.
-// BLK (two-pass plans): the intermediate between the passes is stored blocked,
-// y(j, k) at (k / W2) * (W2 * R2) + j * W2 + (k mod W2), so the second pass reads each
-// tile as one contiguous 64-KiB block instead of 64-B runs n/R apart; the first pass
-// stores 512-B runs (a wave covers 8 k x 8 j). FIRST && BLK: blocked store; !FIRST &&
-// BLK: blocked load.
-// RG (regrouped 2^24 plan, gl_rg2_tile below): 1 = its first pass, 3 = its last pass.
-// PUB (work-queue schedule, ntt_gl_queue_kernel): >= 1 the first pass stores `sc1`; 2 the later
-// pass loads its input `sc1` too.
-template <int LOGR, int E64, bool FIRST, int TILE, bool PERSIST, bool BLK = false, int RG = 0, int PUB = 0>
-__device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t,
-                                        uint32_t next) {
+// One tile: stages A, B, C and the stores.
+// RG (regrouped 2^24 plan, ntt_gl_rg2_kernel below): 1 = its first pass, 3 = its last pass.
+template <int LOGR, int E64, bool FIRST, int TILE, int RG = 0>
+__device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint32_t tile, uint32_t tiles, int t) {
   using Sh = GlShape<LOGR, TILE>;
   constexpr int C = Sh::C, LOGC = Sh::LOGC, W = Sh::W, NT = Sh::NT, YP = Sh::YP;
   (void)YP;
   static_assert(Sh::NSUB_C * C == GL_STORES, "stores per thread");
-  static_assert(RG == 0 || (LOGR == 8 && TILE == 4096 && !PERSIST && !BLK && FIRST == (RG == 1)), "RG shape");
+  static_assert(RG == 0 || (LOGR == 8 && TILE == 4096 && FIRST == (RG == 1)), "RG shape");
   const FieldArgs f{};
   using G = Goldilocks;
   uint32_t poly, kb;
@@ -262,13 +199,9 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   if constexpr (PBF_GL_NOMEM_ON) kb &= 1, poly = 0;
   const uint64_t j0 = (uint64_t)kb * W;
   const uint64_t* in = a.in + (uint64_t)poly * a.in_pitch;
-  // input rows (r) are n/R long: a padded input adds in_pad per row
-  const uint64_t stride = (a.n >> LOGR) + a.in_pad;
+  const uint64_t stride = a.n >> LOGR;  // input rows (r) are n/R long
 
   // ---------------- stage A: load, pass twiddle, 4-point DFTs over s1
-#ifdef PBF_GL_SETPRIO
-  __builtin_amdgcn_s_setprio(3);  // A/B: issue this tile's loads ahead of other waves' math
-#endif
   uint64_t v[16];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -277,31 +210,19 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int s1 = 0; s1 < 4; ++s1) {
       const int r = 16 * C * s1 + C * s2 + r2;
-      if constexpr (PERSIST)
-        v[u * 4 + s1] = lds[r * W + w];
-      else if constexpr (BLK && !FIRST)
-        v[u * 4 + s1] = in[(uint64_t)kb * TILE + r * W + w];
-      else
-        v[u * 4 + s1] = gl_ld<!FIRST && PUB == 2>(in + (j0 + w) + (uint64_t)r * stride);
+      v[u * 4 + s1] = in[(j0 + w) + (uint64_t)r * stride];
     }
   }
-  // RG 3: the stage-B general twiddle T3[q1][a0][j] (a0 = r2 + 4 s2), loaded now (in flight
-  // during stage A) in the stage-B thread mapping
-  // (geometric form, twpass null: t3[s2] = C[r2][X] D[X]^s2, X = 65536 q1 + j; only C and D are
-  // loaded here, the powers are formed in stage B)
-  uint64_t t3[RG == 3 ? 16 : 1];
+  // RG 3: the stage-B general twiddle w^(a0 X) (a0 = r2 + 4 s2, X = 65536 q1 + j), geometric in
+  // s2: C[r2][X] D[X]^s2 with C = w^(r2 X), D = w^(4 X) (tws_a, tws_b); C and D are loaded now
+  // (in flight during stage A) in the stage-B thread mapping, the powers formed in stage B
+  uint64_t t3[RG == 3 ? 2 : 1];
   if constexpr (RG == 3) {
     const int wave = t >> 6, q1 = wave / Sh::WPQ, rw = (wave % Sh::WPQ) * 64 + (t & 63);
     const int r2 = rw / W, w = rw % W;
-    if (a.twpass) {
-      const uint64_t* tb = a.twpass + ((uint64_t)(q1 * 64 + r2) << 16) + j0 + w;
-#pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) t3[s2] = tb[(uint64_t)(4 * s2) << 16];
-    } else {
-      const uint64_t X = ((uint64_t)q1 << 16) + j0 + w;
-      t3[0] = a.tws_a[((uint64_t)r2 << 18) + X];
-      t3[1] = a.tws_b[X];
-    }
+    const uint64_t X = ((uint64_t)q1 << 16) + j0 + w;
+    t3[0] = a.tws_a[((uint64_t)r2 << 18) + X];
+    t3[1] = a.tws_b[X];
   }
   if constexpr (!FIRST && RG != 3) if (!a.skip_pass_tw) {
     const uint64_t kmask = (1ull << a.log_ns) - 1;
@@ -336,10 +257,6 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #endif
     }
   }
-#ifdef PBF_GL_SETPRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
-  if constexpr (PERSIST) gl_bar<true>();  // raw tile consumed before Z overwrites it
 #pragma unroll
   for (int u = 0; u < 4; ++u) PBF_GL_MATH((dft_reg<G, 2, sub_root_exp(E64, 2)>(v + u * 4, nullptr, f)));
 #pragma unroll
@@ -349,7 +266,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
 #pragma unroll
     for (int q1 = 0; q1 < 4; ++q1) lds[(q1 * 16 + s2) * (C * W) + rw] = v[u * 4 + bitrev_c(q1, 2)];
   }
-  gl_bar<PERSIST>();
+  __syncthreads();
 
   // ---------------- stage B: one q1 per wave; shift twiddles; 16-point DFT over s2
   {
@@ -360,17 +277,12 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     for (int s2 = 0; s2 < 16; ++s2) v[s2] = lds[(q1 * 16 + s2) * (C * W) + rw];
 #ifndef PBF_GL_NOMATH
     if constexpr (RG == 3) {
-      if (a.twpass) {
+      uint64_t p = t3[0];
+      const uint64_t d = t3[1];
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) v[s2] = G::mul(v[s2], t3[s2], f);
-      } else {
-        uint64_t p = t3[0];
-        const uint64_t d = t3[1];
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-          v[s2] = G::mul(v[s2], p, f);
-          if (s2 < 15) p = G::mul(p, d, f);
-        }
+      for (int s2 = 0; s2 < 16; ++s2) {
+        v[s2] = G::mul(v[s2], p, f);
+        if (s2 < 15) p = G::mul(p, d, f);
       }
     } else {
       switch (__builtin_amdgcn_readfirstlane(q1)) {
@@ -382,7 +294,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     }
     dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);
 #endif
-    gl_bar<PERSIST>();
+    __syncthreads();
     const int r2 = rw / W, w = rw % W;
 #pragma unroll
     for (int q2 = 0; q2 < 16; ++q2) {
@@ -390,17 +302,14 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
       lds[Sh::yidx(r2, k1, w)] = v[bitrev_c(q2, 4)];
     }
   }
-  gl_bar<PERSIST>();
+  __syncthreads();
 
   // ---------------- stage C: table twiddle w_R^(r2*k1); C-point DFT over r2
   // sub-DFT (k1, w) of thread t: FIRST pass all 64 k1 of one column per wave (512-B runs
   // of k in the output rows out[j*R + k]); later passes w fastest (W-element runs of j)
   auto c_map = [&](int u, int* k1, int* w) {
     const int idx = t + NT * u;
-    if constexpr (FIRST && BLK) {  // 8 k1 x 8 w per wave: 512-B runs of the blocked layout
-      *k1 = (idx & 7) + 8 * ((idx >> 3) / W);
-      *w = (idx >> 3) % W;
-    } else if constexpr (FIRST) {
+    if constexpr (FIRST) {
       *k1 = idx & 63;
       *w = idx >> 6;
     } else {
@@ -440,31 +349,6 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
   } else {
     uint64_t tw[Sh::NSUB_C * C];
     const int r2lo = a.scaled ? 0 : 1;  // scaled table carries n^-1: every element multiplies
-#ifdef PBF_GL_SHFL_TW
-    // A/B build (make shfltw): wavefront-shuffle twiddle broadcast. In later passes a wave's
-    // lanes need only NSUB_C x C x 64/W distinct stage-C twiddles (k1 = idx / W: W lanes share
-    // one); lane L loads twiddle L once, and every lane takes its values from the owning lanes
-    // with ds_bpermute instead of issuing NSUB_C x C broadcast-address global loads.
-    constexpr int PERW = W <= 64 ? 64 / W : 1;
-    constexpr int CNT = Sh::NSUB_C * C * PERW;  // shapes with CNT > 64 keep the loads
-    if constexpr (!FIRST && W <= 64 && CNT <= 64) {
-      const int lane = t & 63, wbase = t & ~63;
-      uint64_t mine = 1;
-      if (lane < CNT) {
-        const int u = lane / (C * PERW), r2 = (lane / PERW) % C, d = lane % PERW;
-        mine = a.tc[r2 * 64 + (wbase + NT * u) / W + d];
-      }
-#pragma unroll
-      for (int u = 0; u < Sh::NSUB_C; ++u)
-#pragma unroll
-        for (int r2 = 0; r2 < C; ++r2) {
-          const int src = ((u * C + r2) * PERW + lane / W) * 4;
-          const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)mine);
-          const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(mine >> 32));
-          tw[u * C + r2] = (r2 >= r2lo) ? (((uint64_t)hi << 32) | lo) : 1;
-        }
-    } else
-#endif
 #pragma unroll
     for (int u = 0; u < Sh::NSUB_C; ++u) {
       int k1, w;
@@ -489,13 +373,6 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
         }
     }
   }
-  if constexpr (PERSIST) {
-    // every wave has read the exchange buffer and consumed its twiddle loads: the next
-    // tile's LDS-DMA runs during the C-point DFTs and the stores (no ordinary load is
-    // consumed after it, so no compiler vmcnt wait drains it)
-    gl_bar<true>();
-    if (next < tiles) gl_tile_dma<LOGR, TILE>(lds, a, next, tiles, t);
-  }
   if constexpr (C > 1) {
 #pragma unroll
     for (int u = 0; u < Sh::NSUB_C; ++u) PBF_GL_MATH((dft_reg<G, LOGC, sub_root_exp(E64, LOGC)>(x + u * C, nullptr, f)));
@@ -508,31 +385,18 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
     for (int u = 0; u < Sh::NSUB_C; ++u) {
       int k1, w;
       c_map(u, &k1, &w);
-      if constexpr (BLK) {
-        const uint32_t bl = a.blk_log;
-        const uint64_t jw = (j0 + w) << bl;
-        const uint64_t bstride = stride << bl;  // W2 * R2 (R2 = n / R columns)
+      const uint64_t base = (j0 + w) << LOGR;
+      if (a.post_tw) {
+        uint64_t tw[C];
 #pragma unroll
-        for (int k2 = 0; k2 < C; ++k2) {
-          const uint32_t k = k1 + 64 * k2;
-          o[(uint64_t)(k >> bl) * bstride + jw + (k & ((1u << bl) - 1))] = x[u * C + bitrev_c(k2, LOGC)];
-        }
-      } else {
-        // a run of R outputs never crosses a row of the next pass (R <= n / R_next)
-        const uint64_t base0 = (j0 + w) << LOGR;
-        const uint64_t base = base0 + (base0 >> a.out_rows_log) * a.out_pad;
-        if (a.post_tw) {
-          uint64_t tw[C];
+        for (int k2 = 0; k2 < C; ++k2) tw[k2] = a.post_tw[base + k1 + 64 * k2];
 #pragma unroll
-          for (int k2 = 0; k2 < C; ++k2) tw[k2] = a.post_tw[base0 + k1 + 64 * k2];
-#pragma unroll
-          for (int k2 = 0; k2 < C; ++k2) x[u * C + bitrev_c(k2, LOGC)] = G::mul(x[u * C + bitrev_c(k2, LOGC)], tw[k2], f);
-        }
-#pragma unroll
-        for (int k2 = 0; k2 < C; ++k2)
-          if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
-            gl_st<(PUB >= 1)>(o + base + k1 + 64 * k2, x[u * C + bitrev_c(k2, LOGC)]);
+        for (int k2 = 0; k2 < C; ++k2) x[u * C + bitrev_c(k2, LOGC)] = G::mul(x[u * C + bitrev_c(k2, LOGC)], tw[k2], f);
       }
+#pragma unroll
+      for (int k2 = 0; k2 < C; ++k2)
+        if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
+          o[base + k1 + 64 * k2] = x[u * C + bitrev_c(k2, LOGC)];
     }
   } else {
     const uint64_t ns_mask = (1ull << a.log_ns) - 1;
@@ -544,13 +408,7 @@ __device__ __forceinline__ void gl_tile(const GlPassArgs& a, uint64_t* lds, uint
       c_map(u, &k1, &w);
       const uint64_t j = j0 + w;
       const uint64_t base = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & ns_mask);
-      if (sl == 0 && a.out_pad) {
-#pragma unroll
-        for (int k2 = 0; k2 < C; ++k2) {
-          const uint64_t g = base + ((uint64_t)(k1 + 64 * k2) << a.log_ns);
-          out[g + (g >> a.out_rows_log) * a.out_pad] = x[u * C + bitrev_c(k2, LOGC)];
-        }
-      } else if (sl == 0) {
+      if (sl == 0) {
 #pragma unroll
         for (int k2 = 0; k2 < C; ++k2)
           if (!PBF_GL_NOMEM_ON || x[u * C + bitrev_c(k2, LOGC)] == 0x123456789ull)
@@ -576,124 +434,16 @@ __device__ __forceinline__ void gl_shape_checks() {
 }
 
 // One tile per workgroup.
-template <int LOGR, int E64, bool FIRST, int TILE, bool BLK = false, int RG = 0>
+template <int LOGR, int E64, bool FIRST, int TILE, int RG = 0>
 // waves per SIMD the VGPR budget allows: 5 where the LDS allows five workgroups and the
 // kernel fits 96 VGPRs without spilling (first passes and the regrouped plan's), else 4
 __global__ void __launch_bounds__(TILE / 16)
-__attribute__((amdgpu_waves_per_eu((FIRST || RG) && !BLK && GlShape<LOGR, TILE>::LDS32K ? 5 : 4)))
+__attribute__((amdgpu_waves_per_eu((FIRST || RG) && GlShape<LOGR, TILE>::LDS32K ? 5 : 4)))
 ntt_gl_pass_kernel(GlPassArgs a) {
   gl_shape_checks<LOGR, TILE>();
   __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
   const uint32_t tiles = a.blocks_per_poly * a.batch;
-  gl_tile<LOGR, E64, FIRST, TILE, false, BLK, RG>(a, lds, blockIdx.x, tiles, threadIdx.x, 0);
-}
-
-// Two groups' passes in one launch (ntt_launch.hip run_gl_dual): `second` is pass 2 of one
-// polynomial group, `first` pass 1 of the next (independent data). Workgroups alternate roles
-// in runs of 8, so each role's tile ids keep their XCD (tile & 7 == blockIdx & 7, as the
-// XCD-aware tile orders assume) and both roles run together on every XCD.
-template <int LOGR, int E64, int TILE>
-__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_gl_dual_kernel(GlPassArgs second, GlPassArgs first) {
-  gl_shape_checks<LOGR, TILE>();
-  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
-  const uint32_t b = blockIdx.x, grp = b >> 3;
-  const uint32_t tile = ((grp >> 1) << 3) | (b & 7);
-  if (grp & 1)
-    gl_tile<LOGR, E64, true, TILE, false>(first, lds, tile, first.blocks_per_poly * first.batch, threadIdx.x, 0);
-  else
-    gl_tile<LOGR, E64, false, TILE, false>(second, lds, tile, second.blocks_per_poly * second.batch, threadIdx.x, 0);
-}
-
-// ---- work-queue schedule of a two-pass plan (round 6) -----------------------------------
-// Both passes of a whole batch in ONE launch, one tile per workgroup, so pass 1 of one
-// polynomial group runs beside pass 2 of the group before it without a second stream, a
-// fork/join or a kernel boundary between the passes. The batch is cut into groups of G
-// polynomials; the work is a sequence of classes, each one pass of one group:
-//   P1(0) .. P1(L-1), then P1(g+L), P2(g) for g = 0 .., then the last P2s   (lag L groups)
-// dealt to 8 queues (queue x = blockIdx mod 8: the blocks that share an XCD), each queue
-// holding 1/8 of every class in the same order: item i of a class in queue x is tile
-// 8 i + x of that pass (XCD k-major tile coordinates, gl_tile_coords 1). A workgroup takes the
-// next item of its queue with one atomic add, so items start in queue order whatever the
-// dispatch order. P2(g) waits until all of P1(g)'s tiles have been published; P1 tiles wait
-// for nothing, and every P1 tile a P2 item needs sits earlier in every queue, so each wait
-// ends (the items it waits on were taken by running workgroups).
-// Hand-off (MI355X_MICROARCH.md "inter-workgroup visibility", Valid forms): every storing wave
-// waits vmcnt(0), a workgroup barrier, then one lane publishes: PUB 0 plain stores + agent
-// release fence before the counter add; PUB 1/2 write-through (`sc1`) stores, no fence. The
-// consumer polls the counter with relaxed agent-scope loads (`sc1`), then PUB 0/1 one agent
-// acquire, PUB 2 none (its input loads are `sc1` too), a barrier, then the tile.
-// Counters (ctr, u32): [0, 8) queue heads, [8] finished workgroups, [9 + g] P1 tiles of group g
-// published. The last workgroup to finish zeroes them for the next launch (after every other
-// workgroup's last counter access: each finishes its own returning adds first).
-struct GlQueueArgs {
-  GlPassArgs p1, p2;  // group 0's passes (batch = G polynomials, XCD k-major tiles)
-  uint32_t* ctr;
-  uint64_t in_gs, scr_gs, out_gs;  // elements from one group to the next: input, scratch, output
-  uint32_t per_class;              // items per queue per class (G x tiles per polynomial / 8)
-  uint32_t groups, lag, total;     // total = workgroups of the launch = items
-};
-
-template <int LOGR, int E64, int TILE, int PUB>
-__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_gl_queue_kernel(GlQueueArgs q) {
-  gl_shape_checks<LOGR, TILE>();
-  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
-  __shared__ uint32_t s_pos;
-  const int t = threadIdx.x;
-  const uint32_t x = blockIdx.x & 7;
-  if (t == 0) s_pos = __hip_atomic_fetch_add(q.ctr + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const uint32_t pos = s_pos;
-  const uint32_t c = pos / q.per_class, i = pos % q.per_class;
-  // class c -> (pass, group)
-  const uint32_t L = q.lag < q.groups ? q.lag : q.groups, pairs = q.groups - L;
-  bool second;
-  uint32_t g;
-  if (c < L) {
-    second = false, g = c;
-  } else if (c - L < 2 * pairs) {
-    const uint32_t k = c - L;
-    second = (k & 1) != 0, g = (k >> 1) + ((k & 1) ? 0 : L);
-  } else {
-    second = true, g = pairs + (c - L - 2 * pairs);
-  }
-  const uint32_t tiles = q.per_class * 8, tile = i * 8 + x;
-  if (!second) {
-    GlPassArgs a = q.p1;
-    a.in += g * q.in_gs;
-    a.out += g * q.scr_gs;
-    gl_tile<LOGR, E64, true, TILE, false, false, 0, PUB>(a, lds, tile, tiles, t, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
-    __syncthreads();
-    if (t == 0) {
-      if constexpr (PUB == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      (void)__hip_atomic_fetch_add(q.ctr + 9 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the add has landed before the finish add
-    }
-  } else {
-    if (t == 0) {
-      while (__hip_atomic_load(q.ctr + 9 + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tiles)
-        __builtin_amdgcn_s_sleep(8);
-      if constexpr (PUB < 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    GlPassArgs a = q.p2;
-    a.in += g * q.scr_gs;
-    a.out += g * q.out_gs;
-    gl_tile<LOGR, E64, false, TILE, false, false, 0, PUB>(a, lds, tile, tiles, t, 0);
-  }
-  if (t == 0) {
-    const uint32_t f = __hip_atomic_fetch_add(q.ctr + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (f + 1 == q.total) {
-      for (uint32_t k = 0; k < 9 + q.groups; ++k)
-        __hip_atomic_store(q.ctr + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  gl_tile<LOGR, E64, FIRST, TILE, RG>(a, lds, blockIdx.x, tiles, threadIdx.x);
 }
 
 // ---- regrouped 2^24 plan (DESIGN.md §3.1 "Regrouped twiddles") --------------------------
@@ -706,21 +456,18 @@ ntt_gl_queue_kernel(GlQueueArgs q) {
 // general multiplications for the whole transform instead of 4.25 (0.75 + 1.75 + 1.75):
 //   pass 1 (RG 1): DFT-64 over a3 | w_4096^(a2 b0) (a2l = bits 12..15 of the column) | DFT-4
 //   pass 2 (this kernel): w_64^(a2l c) | DFT-16 over a2l | T2[a1][K] | DFT-16 over a1h | w_64^(a1l e)
-//   pass 3 (RG 3): DFT-4 over a1l | T3[f][a0][j] | DFT-16 | w_64^(r2 g) | DFT-4
+//   pass 3 (RG 3): DFT-4 over a1l | w^(a0 X) = C[r2][X] D[X]^s2 | DFT-16 | w_64^(r2 g) | DFT-4
 // Pass 2 needs one LDS exchange (two 16-point stages), not two. Data stays in the Stockham
 // layout of the other passes (natural order in and out).
 // Pass 2 tile: 256 rows r = 16 a2l + a1h x W = 16 columns j (Ns = 256: j mod 256 = b0 + 64 c,
 // the first pass's output digit; bits 14..15 of j = a1l); stage X thread (a1h, w), stage Y
 // thread (d, w); LDS [d][a1h ^ (d mod 4)][w] (the XOR spreads the stage-Y reads of four d per
 // wave over both halves of the banks: every bank pair is hit exactly twice, the minimum).
-#ifndef PBF_RG2_WPE
-#define PBF_RG2_WPE 4
-#endif
-template <int E64, bool GEO = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GEO ? 5 : PBF_RG2_WPE))) ntt_gl_rg2_kernel(GlPassArgs a) {
+template <int E64>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) ntt_gl_rg2_kernel(GlPassArgs a) {
   constexpr int W = 16;
-  // 32 KiB; four waves per SIMD (PBF_RG2_WPE): at five the 96-VGPR budget spills 28 B per
-  // lane and the pass runs ~2 % slower (profiles/r03/ntt_lds_ab.log)
+  // 32 KiB; four waves per SIMD: at five the 96-VGPR budget spills 28 B per lane and the pass
+  // runs ~2 % slower (profiles/r03/ntt_lds_ab.log)
   __shared__ __attribute__((aligned(16))) uint64_t lds[16 * 16 * W];
   const FieldArgs f{};
   using G = Goldilocks;
@@ -735,18 +482,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GEO ? 
   uint64_t v[16], tw[16];
 #pragma unroll
   for (int a2l = 0; a2l < 16; ++a2l) v[a2l] = in[j + (uint64_t)(a2l * 16 + a1h) * stride];
-  // T2[a1][K] = w^(64 a1 K), a1 = a1l + 4 a1h, K = b0 + 64 b1 = (j mod 256) + 256 d; geometric
-  // in d (GEO, PBF_NTT_T2GEO: tws_b = w^(16384 a1)): T2[a1][j mod 256] (w^(16384 a1))^d, two loads
-  // and 15 products instead of 16 loads, 16 fewer live registers (five waves per SIMD)
-  constexpr bool geo = GEO;
+  // T2[a1][K] = w^(64 a1 K), a1 = a1l + 4 a1h, K = b0 + 64 b1 = (j mod 256) + 256 d (2 MiB,
+  // L2-resident; the geometric form T2[a1][j mod 256] (w^(16384 a1))^d measured 1.5 % slower in
+  // round 5, profiles/r05/t2geo_ab.log)
   const uint64_t* t2 = a.twpass + ((uint64_t)(a1l + 4 * a1h) << 12) + (j & 255);
-  if constexpr (geo) {
-    tw[0] = t2[0];
-    tw[1] = a.tws_b[a1l + 4 * a1h];
-  } else {
 #pragma unroll
-    for (int d = 0; d < 16; ++d) tw[d] = t2[256 * d];
-  }
+  for (int d = 0; d < 16; ++d) tw[d] = t2[256 * d];
   switch (__builtin_amdgcn_readfirstlane(c)) {  // w_64^(a2l c)
     case 1: gl_stage_b_twiddle<E64, 1>(v); break;
     case 2: gl_stage_b_twiddle<E64, 2>(v); break;
@@ -754,18 +495,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GEO ? 
     default: break;
   }
   dft_reg<G, 4, sub_root_exp(E64, 4)>(v, nullptr, f);  // output d at v[bitrev4(d)]
-  if constexpr (geo) {
-    uint64_t p = tw[0];
-    const uint64_t dd = tw[1];
 #pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], p, f);
-      if (d < 15) p = G::mul(p, dd, f);
-    }
-  } else {
-#pragma unroll
-    for (int d = 0; d < 16; ++d) lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
-  }
+  for (int d = 0; d < 16; ++d) lds[d * 256 + (a1h ^ (d & 3)) * W + w] = G::mul(v[bitrev_c(d, 4)], tw[d], f);
   __syncthreads();
   const int d2 = t / W;
 #pragma unroll
@@ -782,31 +513,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GEO ? 
   const uint64_t base = ((j >> 8) << 16) + (j & 255);
 #pragma unroll
   for (int e = 0; e < 16; ++e) out[base + ((uint64_t)(d2 + 16 * e) << 8)] = v[bitrev_c(e, 4)];
-}
-
-// Persistent, software-pipelined (PBF_NTT_PERSIST): each workgroup walks tiles blockIdx.x,
-// +gridDim.x, ...; tile i+1's input LDS-DMA overlaps tile i's C-point DFTs and stores. The
-// counted vmcnt(GL_STORES) at the end of an iteration retires the DMA without waiting for
-// the younger stores (loads and stores share vmcnt, in issue order).
-template <int LOGR, int E64, bool FIRST, int TILE>
-__global__ void __launch_bounds__(TILE / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_gl_pass_pkernel(GlPassArgs a) {
-  gl_shape_checks<LOGR, TILE>();
-  __shared__ __attribute__((aligned(16))) uint64_t lds[GlShape<LOGR, TILE>::LDS];
-  const uint32_t tiles = a.blocks_per_poly * a.batch;
-  uint32_t tile = blockIdx.x;
-  if (tile >= tiles) return;
-  gl_tile_dma<LOGR, TILE>(lds, a, tile, tiles, threadIdx.x);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  for (; tile < tiles; tile += gridDim.x) {
-    // opaque copy of the thread index: keeps per-thread address arithmetic inside the loop
-    // (hoisted out of it, its live values would spill the 128-VGPR budget)
-    int t;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
-    gl_bar<true>();  // this tile's DMA landed in every wave
-    gl_tile<LOGR, E64, FIRST, TILE, true>(a, lds, tile, tiles, t, tile + gridDim.x);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL_STORES) : "memory");  // next tile's DMA, not the stores
-  }
 }
 
 }  // namespace pbf

@@ -30,7 +30,7 @@ struct PassArgs {
   const uint64_t* tw0;   // w^m for m < 2^tw_bits            (two-level table, low part)
   const uint64_t* tw1;   // w^(m << tw_bits) for m < n>>tw_bits (high part)
   const uint64_t* rtab;  // w_R^m = w^(m*n/R) for m < R
-  const uint64_t* twfull; // w^m for m < n (small n only; null => two-level table)
+  const uint64_t* twfull; // unused (always null; kept for the argument layout)
   const uint64_t* twpass; // this pass's twiddles T[r][k] = w^((n/(Ns*R))*r*k), or null
   uint64_t n;            // transform size
   uint64_t n_inv;        // n^-1, applied to outputs when scale != 0
@@ -158,25 +158,6 @@ __device__ __forceinline__ void tile_barrier() {
   }
 }
 
-// LDS-DMA of one tile: R rows x W columns of the pass input into buf ([r][w] image,
-// 16-B chunks, lane-linear destination, per-lane global source).
-template <int LOGR, int W, int NT>
-__device__ __forceinline__ void tile_dma(uint64_t* buf, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
-  constexpr int R = 1 << LOGR;
-  constexpr int CPR = W / 2;               // 16-B chunks per row
-  constexpr int CHUNKS = R * CPR;
-  const int wave = t >> 6, lane = t & 63;
-  const uint64_t stride = a.n >> LOGR;
-#pragma unroll
-  for (int q0 = wave * 64; q0 < CHUNKS; q0 += NT) {
-    const int q = q0 + lane;
-    const int row = q / CPR, col = 2 * (q % CPR);
-    const uint64_t* g = in + (j0 + col) + (uint64_t)row * stride;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)(buf + 2 * q0), 16, 0, 0);
-  }
-}
-
 // Raw stage-0 inputs of one tile into registers (the same thread -> element map as stage 0).
 template <int LOGR, int W, int NT, int LQ>
 __device__ __forceinline__ void tile_load(uint64_t* v, const PassArgs& a, const uint64_t* in, uint64_t j0, int t) {
@@ -196,24 +177,13 @@ __device__ __forceinline__ void tile_load(uint64_t* v, const PassArgs& a, const 
   }
 }
 
-struct NextTile {
-  bool valid;
-  uint64_t* buf;   // mode 1: LDS destination
-  const uint64_t* in;
-  uint64_t j0;
-  uint64_t* regs;  // mode 2: register destination
-};
-
 // One register/LDS stage S of the in-workgroup R-point Stockham (radix Q = 2^logq).
-// MODE: 0 = one tile per workgroup; 1 = persistent, next tile LDS-DMA'd during this one
-// (ntt_pass_db_kernel); 2 = persistent, next tile prefetched into registers during this
-// one (ntt_pass_rp_kernel). Stage 0 reads the raw tile (registers v, or the LDS image
-// `buf` in mode 1) and applies the pass twiddle; later stages read the exchange buffer
-// and apply the stage twiddle from `rt` (an LDS copy in modes 1 and 2).
-template <class F, int LOGR, int W, int NT, int LQ, int E64, int MODE, int S>
+// Stage 0 takes the raw tile (registers v) and applies the pass twiddle; later stages read
+// the exchange buffer and apply the stage twiddle from `rt`. (The LDS-DMA double-buffered and
+// register-prefetching persistent forms of rounds 1-2 measured slower; removed in round 6.)
+template <class F, int LOGR, int W, int NT, int LQ, int E64, int S>
 __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint64_t* rt, const uint64_t* wq,
-                                          const PassArgs& a, uint64_t* out, uint64_t j0, int t,
-                                          const NextTile& nx) {
+                                          const PassArgs& a, uint64_t* out, uint64_t j0, int t) {
   constexpr int R = 1 << LOGR;
   constexpr int PER = (R * W) / NT;
   constexpr int NST = ntt_nstages(LOGR, LQ);
@@ -227,15 +197,6 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
   // branches hoisted out of the unrolled loops) so all PER twiddle loads issue
   // back to back and are waited for once.
   if constexpr (S == 0) {
-    if constexpr (MODE == 1) {
-#pragma unroll
-      for (int u = 0; u < NSUB; ++u) {
-        const int sub = t + NT * u;
-        const int w = sub % W, i = sub / W;
-#pragma unroll
-        for (int c = 0; c < Q; ++c) v[u * Q + c] = buf[(i + c * (R / Q)) * W + w];
-      }
-    }
     if (a.log_ns > 0) {
       const uint64_t kmask = (1ull << a.log_ns) - 1;
       if (a.twpass) {
@@ -262,7 +223,7 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
           for (int c = 0; c < Q; ++c) {
             const uint64_t r = i + c * (R / Q);
             const uint64_t e = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (n - 1);
-            if (e) v[u * Q + c] = F::mul(v[u * Q + c], a.twfull ? a.twfull[e] : tw_pow<F>(a, e), a.f);
+            if (e) v[u * Q + c] = F::mul(v[u * Q + c], tw_pow<F>(a, e), a.f);
           }
         }
       }
@@ -280,15 +241,6 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
       }
     }
   }
-  if constexpr (MODE == 1 && S == 0) {
-    // this tile's pass-twiddle loads are consumed: start the next tile's LDS-DMA now
-    if (nx.valid) tile_dma<LOGR, W, NT>(nx.buf, a, nx.in, nx.j0, t);
-  }
-  if constexpr (MODE == 2 && S == 0) {
-    // same point for the register prefetch: its loads stay in flight through the later
-    // stages (LDS twiddles, raw barriers: nothing waits on vmcnt until the next tile)
-    if (nx.valid) tile_load<LOGR, W, NT, LQ>(nx.regs, a, nx.in, nx.j0, t);
-  }
   // ---- radix-Q DFTs in registers (wq[m] = w_QMAX^m; w_Q = w_QMAX^(QMAX/Q))
   constexpr int QMAX = 1 << LQ;
 #pragma unroll
@@ -300,7 +252,7 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
     }
     if (!PBF_DBG(a, 2)) dft_reg<F, LOGQ, sub_root_exp(E64, LOGQ)>(v + u * Q, wloc, a.f);
   }
-  if constexpr (S > 0 || MODE == 1) tile_barrier<(MODE != 0)>();  // all reads of the exchange buffer are done
+  if constexpr (S > 0) tile_barrier<false>();  // all reads of the exchange buffer are done
   // ---- scatter outputs (uniform output-mode branches hoisted out of the unrolled loops)
   if constexpr (!LAST) {
 #pragma unroll
@@ -364,8 +316,8 @@ __device__ __forceinline__ void ntt_stage(uint64_t* v, uint64_t* buf, const uint
     }
   }
   if constexpr (!LAST) {
-    tile_barrier<(MODE != 0)>();
-    ntt_stage<F, LOGR, W, NT, LQ, E64, MODE, S + 1>(v, buf, rt, wq, a, out, j0, t, nx);
+    tile_barrier<false>();
+    ntt_stage<F, LOGR, W, NT, LQ, E64, S + 1>(v, buf, rt, wq, a, out, j0, t);
   }
 }
 
@@ -437,114 +389,8 @@ ntt_pass_kernel(PassArgs a) {
   }
   uint64_t v[PER];
   tile_load<LOGR, W, NT, LQ>(v, a, in, j0, t);
-  const NextTile none{false, nullptr, nullptr, 0, nullptr};
-  ntt_stage<F, LOGR, W, NT, LQ, E64, 0, 0>(v, lds, a.rtab, wq, b, out, j0, t, none);
+  ntt_stage<F, LOGR, W, NT, LQ, E64, 0>(v, lds, a.rtab, wq, b, out, j0, t);
   if (a.log_ns == 0) store_transposed<LOGR, W, NT, false>(lds, out, j0, t, a);
-}
-
-// Double-buffered persistent pass (tiles of <= 64 KiB): each workgroup walks tiles
-// blockIdx.x, +gridDim.x, ...; the next tile is LDS-DMA'd into the other buffer while
-// this one is computed, so HBM reads overlap the arithmetic. Stage twiddles live in LDS.
-template <class F, int LOGR, int W, int NT, int LQ, int E64>
-__global__ void __launch_bounds__(NT) ntt_pass_db_kernel(PassArgs a) {
-  constexpr int R = 1 << LOGR;
-  constexpr int E = R * W;
-  constexpr int PER = E / NT;
-  constexpr int QMAX = 1 << LQ;
-  constexpr int BUF = E + W;  // element image (+pad for the transposed first-pass image)
-  static_assert(LOGR >= LQ && PER >= QMAX && PER % QMAX == 0, "bad tile shape");
-  static_assert(PER <= 63, "counted vmcnt must fit");
-  static_assert(2 * BUF + R <= 20480, "LDS budget: two tiles + stage twiddles in 160 KiB");
-  __shared__ __attribute__((aligned(16))) uint64_t lds[2 * BUF + R];
-  uint64_t* rt = lds + 2 * BUF;
-
-  const int t = threadIdx.x;
-  const uint32_t total = a.blocks_per_poly * a.batch;
-  uint32_t blk = blockIdx.x;
-  if (blk >= total) return;
-  for (int i = t; i < R; i += NT) rt[i] = a.rtab[i];
-  uint64_t wq[QMAX / 2];
-  if constexpr (E64 < 0) {
-#pragma unroll
-    for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
-  }
-  // prologue: first tile
-  tile_dma<LOGR, W, NT>(lds, a, a.in + (uint64_t)(blk / a.blocks_per_poly) * a.n,
-                        (uint64_t)(blk % a.blocks_per_poly) * W, t);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  tile_barrier<true>();
-  int cur = 0;
-  for (; blk < total; blk += gridDim.x) {
-    const uint32_t poly = blk / a.blocks_per_poly;
-    const uint64_t j0 = (uint64_t)(blk % a.blocks_per_poly) * W;
-    uint64_t* out = a.out + (uint64_t)poly * a.n;
-    PassArgs b = a;
-    b.cur_poly = poly;
-    const uint32_t nb = blk + gridDim.x;
-    NextTile nx;
-    nx.valid = nb < total;
-    nx.buf = lds + (cur ^ 1) * BUF;
-    nx.in = a.in + (uint64_t)(nb / a.blocks_per_poly) * a.n;
-    nx.j0 = (uint64_t)(nb % a.blocks_per_poly) * W;
-    uint64_t* buf = lds + cur * BUF;
-    uint64_t v[PER];
-    ntt_stage<F, LOGR, W, NT, LQ, E64, 1, 0>(v, buf, rt, wq, b, out, j0, t, nx);
-    if (a.log_ns == 0) store_transposed<LOGR, W, NT, true>(buf, out, j0, t, a);
-    // retire the next tile's LDS-DMA (issued before this tile's PER output stores)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    tile_barrier<true>();
-    cur ^= 1;
-  }
-}
-
-// Persistent pass with a register prefetch (mode 2): while a tile's stages 1.. run, the
-// next tile's inputs load into registers, so one workgroup overlaps its own HBM reads
-// with arithmetic and keeps a single LDS tile (two workgroups per CU at R*W = 8192).
-// Stage twiddles are copied to LDS so no global load waits behind the prefetch.
-template <class F, int LOGR, int W, int NT, int LQ, int E64>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ntt_waves_per_eu(W << LOGR, NT))))
-ntt_pass_rp_kernel(PassArgs a) {
-  constexpr int R = 1 << LOGR;
-  constexpr int E = R * W;
-  constexpr int PER = E / NT;
-  constexpr int QMAX = 1 << LQ;
-  static_assert(LOGR >= LQ && PER >= QMAX && PER % QMAX == 0, "bad tile shape");
-  static_assert(E + W + R <= 20480, "LDS budget");
-  __shared__ uint64_t lds[E + W + R];
-  uint64_t* rt = lds + E + W;
-  const int t = threadIdx.x;
-  const uint32_t total = a.blocks_per_poly * a.batch;
-  uint32_t blk = blockIdx.x;
-  if (blk >= total) return;
-  for (int i = t; i < R; i += NT) rt[i] = a.rtab[i];
-  uint64_t wq[QMAX / 2];
-  if constexpr (E64 < 0) {
-#pragma unroll
-    for (int m = 0; m < QMAX / 2; ++m) wq[m] = a.rtab[m * (R / QMAX)];
-  }
-  uint64_t nxt[PER];
-  tile_load<LOGR, W, NT, LQ>(nxt, a, a.in + (uint64_t)(blk / a.blocks_per_poly) * a.n,
-                             (uint64_t)(blk % a.blocks_per_poly) * W, t);
-  for (; blk < total; blk += gridDim.x) {
-    const uint32_t poly = blk / a.blocks_per_poly;
-    const uint64_t j0 = (uint64_t)(blk % a.blocks_per_poly) * W;
-    uint64_t* out = a.out + (uint64_t)poly * a.n;
-    PassArgs b = a;
-    b.cur_poly = poly;
-    uint64_t v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = nxt[i];
-    const uint32_t nb = blk + gridDim.x;
-    NextTile nx;
-    nx.valid = nb < total;
-    nx.buf = nullptr;
-    nx.in = a.in + (uint64_t)(nb / a.blocks_per_poly) * a.n;
-    nx.j0 = (uint64_t)(nb % a.blocks_per_poly) * W;
-    nx.regs = nxt;
-    ntt_stage<F, LOGR, W, NT, LQ, E64, 2, 0>(v, lds, rt, wq, b, out, j0, t, nx);
-    if (a.log_ns == 0) store_transposed<LOGR, W, NT, true>(lds, out, j0, t, a);
-    tile_barrier<true>();  // the next tile rewrites the exchange buffer
-  }
 }
 
 // Whole transform of a small n (<= 4096) inside one workgroup per polynomial:

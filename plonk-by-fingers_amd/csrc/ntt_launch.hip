@@ -4,7 +4,6 @@
 #include <mutex>
 #include "internal.hpp"
 #include "ntt_gl.hpp"
-#include "ntt_r4k.hpp"
 
 namespace pbf {
 
@@ -59,8 +58,10 @@ static int upload(DevBuf& b, const std::vector<uint64_t>& v) {
   return 0;
 }
 
-static std::vector<int> default_passes(uint32_t log_n) {
-  const char* env = getenv("PBF_NTT_PASSES");  // e.g. "12,12" (benchmarking override)
+// radix bits per pass: option "ntt.passes" (e.g. "12,12"; every radix family the planner can
+// pick, tests/test_ntt_gpu.py), else passes of at most 2^10 as equal as possible
+static std::vector<int> default_passes(uint32_t log_n, const Options& o) {
+  const char* env = o.get("ntt.passes");
   if (env && *env) {
     std::vector<int> v;
     int sum = 0;
@@ -83,111 +84,6 @@ static std::vector<int> default_passes(uint32_t log_n) {
 
 
 static int gl_tile(int logr);
-
-// ---- round-3 schedule (ntt_ip.hpp) ----------------------------------------------------
-int ip_tile_of(int r) { return r >= 10 ? 8192 : 4096; }
-int ip_w(int r) { return ip_tile_of(r) >> r; }
-
-// radix bits per pass, top slot first; empty when the schedule does not apply
-static std::vector<int> ip_radices(uint32_t L) {
-  std::vector<int> v;
-  if (const char* env = getenv("PBF_NTT_IP_PASSES")) {  // A/B override, e.g. "8,8,8"
-    int sum = 0;
-    for (const char* c = env; *c;) {
-      v.push_back(atoi(c));
-      sum += v.back();
-      while (*c && *c != ',') ++c;
-      if (*c == ',') ++c;
-    }
-    if (sum != (int)L) v.clear();
-  } else if (L >= 12 && L <= 30) {
-    const int P = L <= 20 ? 2 : 3;
-    v.assign(P, (int)L / P);
-    for (int i = 0; i < (int)(L % P); ++i) v[i] += 1;
-  }
-  if (v.size() < 2 || v.size() > 4) return {};  // IP_MAXP (ntt_ip.hpp)
-  int lo = (int)L;
-  for (size_t i = 0; i < v.size(); ++i) {
-    if (v[i] < 6 || v[i] > 10) return {};
-    lo -= v[i];
-    if (i + 1 < v.size() && (1 << lo) < ip_w(v[i])) return {};  // column blocks of W
-  }
-  if ((1 << v[0]) < ip_w(v.back())) return {};  // row pass: W consecutive K vary k_0 only
-  return v;
-}
-
-static int make_ip_plan(NttPlan* p, uint64_t w) {
-  const uint64_t m = p->m, n = p->n;
-  const uint32_t L = p->log_n;
-  p->ip_r = ip_radices(L);
-  if (p->ip_r.empty()) return 0;
-  const size_t P = p->ip_r.size();
-  std::vector<int> lo(P);
-  {
-    int l = (int)L;
-    for (size_t i = 0; i < P; ++i) { l -= p->ip_r[i]; lo[i] = l; }
-  }
-  const uint64_t scale = p->inverse ? p->n_inv : 1;
-  for (size_t i = 0; i < P; ++i) {
-    const int r = p->ip_r[i];
-    const uint64_t R = 1ull << r, C = R / 64, W = (uint64_t)ip_w(r);
-    // stage-C table w_R^(r2 k1) (unscaled: the inverse scales in the row pass's twiddles)
-    {
-      const uint64_t wr = hpow(w, n / R, m);
-      std::vector<uint64_t> tc(C * 64);
-      for (uint64_t r2 = 0; r2 < C; ++r2)
-        for (uint64_t k1 = 0; k1 < 64; ++k1) tc[r2 * 64 + k1] = hpow(wr, r2 * k1, m);
-      auto b = std::make_shared<DevBuf>();
-      int rc = upload(*b, tc);
-      if (rc) return rc;
-      p->ip_tc.push_back(b);
-    }
-    auto tb = std::make_shared<DevBuf>();
-    if (i > 0 && i + 1 < P) {
-      // column pass: T[h][x] = w^(2^lo_i x K(h)), K(h) = the earlier digits, k_0 lowest
-      const uint64_t H = 1ull << (L - lo[i] - r);
-      std::vector<uint64_t> t(H * R);
-      for (uint64_t h = 0; h < H; ++h) {
-        uint64_t K = 0, sh = 0;
-        for (size_t j = 0; j < i; ++j) {
-          const uint64_t kj = (h >> (lo[j] - lo[i] - r)) & ((1ull << p->ip_r[j]) - 1);
-          K |= kj << sh;
-          sh += (uint64_t)p->ip_r[j];
-        }
-        const uint64_t z = hpow(w, (((uint64_t)1 << lo[i]) * K) % n, m);
-        uint64_t y = 1;
-        for (uint64_t x = 0; x < R; ++x) { t[h * R + x] = y; y = hmul(y, z, m); }
-      }
-      int rc = upload(*tb, t);
-      if (rc) return rc;
-    } else if (i + 1 == P) {
-      // row pass: w^(x K) (x n^-1 for the inverse), K < n / R
-      const uint64_t NK = n / R;
-      const bool full = n <= (1ull << 21) && !getenv("PBF_NTT_IP_SPLIT");
-      std::vector<uint64_t> t(full ? NK * R : (NK / W) * R);
-      for (uint64_t kb = 0; kb < (full ? NK : NK / W); ++kb) {
-        const uint64_t z = hpow(w, full ? kb : kb * W, m);
-        uint64_t y = scale;
-        for (uint64_t x = 0; x < R; ++x) { t[kb * R + x] = y; y = hmul(y, z, m); }
-      }
-      int rc = upload(*tb, t);
-      if (rc) return rc;
-      if (!full) {
-        std::vector<uint64_t> ta(R * W);
-        for (uint64_t x = 0; x < R; ++x) {
-          const uint64_t z = hpow(w, x, m);
-          uint64_t y = 1;
-          for (uint64_t c = 0; c < W; ++c) { ta[x * W + c] = y; y = hmul(y, z, m); }
-        }
-        p->ip_twa = std::make_shared<DevBuf>();
-        if ((rc = upload(*p->ip_twa, ta))) return rc;
-      }
-    }
-    p->ip_tw.push_back(tb);
-  }
-  p->ip = true;
-  return 0;
-}
 
 int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   if (!field_for(m, &p->kind, &p->fa)) return fail(5, "unsupported modulus");
@@ -212,22 +108,14 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
     for (uint64_t i = 0; i < n; ++i) { t[i] = x; x = hmul(x, w, m); }
     return upload(p->small_tw, t);
   }
-  p->logr = default_passes(log_n);
+  p->logr = default_passes(log_n, p->opts);
   p->tw_bits = (log_n + 1) / 2;
   // standard Goldilocks root => shift twiddles in the register sub-DFTs
   p->e64 = -1;
-  if (p->kind == FIELD_GOLDILOCKS && !getenv("PBF_NTT_NO_SHIFT")) {
+  if (p->kind == FIELD_GOLDILOCKS) {
     const uint64_t w64 = hpow(w, n / 64, m);
     if (w64 == hpow(2, 39, m)) p->e64 = 39;
     else if (w64 == hpow(2, 153, m)) p->e64 = 153;
-  }
-  // scattered full twiddle table: measured slower than the two-level table (kept for A/B)
-  if (log_n <= 22 && getenv("PBF_NTT_TWFULL")) {
-    std::vector<uint64_t> tf(n);
-    uint64_t z = 1 % m;
-    for (uint64_t i = 0; i < n; ++i) { tf[i] = z; z = hmul(z, w, m); }
-    int rc0 = upload(p->twfull, tf);
-    if (rc0) return rc0;
   }
   std::vector<uint64_t> t0(1ull << p->tw_bits), t1(n >> p->tw_bits);
   uint64_t x = 1 % m;
@@ -238,19 +126,18 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   int rc = upload(p->tw0, t0);
   if (!rc) rc = upload(p->tw1, t1);
   if (rc) return rc;
-  // per-pass [r][k] twiddle tables while R*Ns <= 2^PBF_NTT_TWMAX_LOG (default 24: the last
+  // per-pass [r][k] twiddle tables while R*Ns <= 2^ntt.twmax_log (default 24: the last
   // pass of a 2^24 transform reads a 128 MiB table, shared by every polynomial of a batch,
   // in 128-B runs like its data; the two-level table's two random gathers per element were
   // bound by the texture unit: 2^24 x 2 0.545 -> 0.490 ms); larger passes
   // use the two-level table
   {
     uint64_t ns = 1;
-    const char* tm = getenv("PBF_NTT_TWMAX_LOG");
-    const int twmax = tm ? atoi(tm) : 24;
+    const int twmax = (int)p->opts.num("ntt.twmax_log", 24);
     for (size_t i = 0; i < p->logr.size(); ++i) {
       const uint64_t R = 1ull << p->logr[i];
       auto b = std::make_shared<DevBuf>();
-      if (ns > 1 && R * ns <= (1ull << twmax) && !getenv("PBF_NTT_TWO_LEVEL")) {
+      if (ns > 1 && R * ns <= (1ull << twmax)) {
         const uint64_t step = n / (ns * R);
         std::vector<uint64_t> t(R * ns);
         for (uint64_t r = 0; r < R; ++r) {
@@ -263,10 +150,12 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
       }
       p->twpass.push_back(b);
       // the last pass of a standard-root plan whose [r][k] table is not built: split table
-      // (A/B: PBF_NTT_TWSPLIT=1 also replaces a built one)
+      // (option ntt.twsplit=1 also replaces a built one, =0 keeps the two-level table: the
+      // paths of n > 2^24 exercised at test sizes)
       const bool last = i + 1 == p->logr.size();
-      const bool split = getenv("PBF_NTT_TWSPLIT") != nullptr;
-      if (last && ns > 1 && p->e64 >= 0 && !getenv("PBF_NTT_NO_TWSPLIT") && p->logr[i] >= 6 && p->logr[i] <= 10 && (!b->p || split)) {
+      const long long ts = p->opts.num("ntt.twsplit", -1);
+      const bool split = ts == 1;
+      if (last && ns > 1 && p->e64 >= 0 && ts != 0 && p->logr[i] >= 6 && p->logr[i] <= 10 && (!b->p || split)) {
         const uint64_t W = (uint64_t)gl_tile(p->logr[i]) >> p->logr[i];
         if (ns % W == 0) {
           if (split) p->twpass.back() = std::make_shared<DevBuf>();
@@ -304,7 +193,7 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   }
   // ntt_gl_pass_kernel (standard Goldilocks roots, radices 2^6..2^10): stage-C tables
   // tc[r2][k1] = w_R^(r2*k1), r2 < R/64, k1 < 64; the last pass of an inverse carries n^-1
-  p->gl = p->e64 >= 0 && !getenv("PBF_NTT_LEGACY");
+  p->gl = p->e64 >= 0;
   for (int lr : p->logr) p->gl = p->gl && lr >= 6 && lr <= 10;
   if (p->gl) {
     for (size_t i = 0; i < p->logr.size(); ++i) {
@@ -323,17 +212,10 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
       p->tc.push_back(b);
     }
   }
-  // regrouped 2^24 plan (default for 8,8,8 standard-root plans; PBF_NTT_NO_RG=1 restores the
-  // round-2 passes): three twiddle layers of order 4096, 2^18 and 2^24
-  if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && !getenv("PBF_NTT_NO_RG")) p->rg = true;
-  // two-pass 4096 x 4096 plan (ntt_r4k.hpp)
-  if (p->gl && log_n == 24 && getenv("PBF_NTT_R4K")) p->r4k = true;
-  // round-3 in-place schedule: opt-in (PBF_NTT_IP=1) while it measures slower than the
-  // round-2 Stockham plan
-  if (p->gl && getenv("PBF_NTT_IP") && !getenv("PBF_NTT_V2")) {
-    int rc2 = make_ip_plan(p, w);
-    if (rc2) return rc2;
-  }
+  // regrouped 2^24 plan (default for 8,8,8 standard-root plans; option ntt.no_rg=1 keeps the
+  // round-2 passes, the tests' cross-check): three twiddle layers of order 4096, 2^18 and 2^24
+  // 
+  if (p->gl && log_n == 24 && p->logr == std::vector<int>{8, 8, 8} && p->opts.num("ntt.no_rg", 0) == 0) p->rg = true;
   return 0;
 }
 
@@ -346,42 +228,20 @@ static int cols_for(int logr) {
   return logr < 10 ? 16 : (logr == 10 ? 8 : (logr == 11 ? 8 : 4));
 }
 
-// Kernel configuration of one pass: W columns, register radix 2^LQ, double-buffered
-// persistent (DB) or one tile per workgroup.
+// Kernel configuration of one pass: W columns, register radix 2^LQ, one tile per workgroup
+// (the LDS-DMA double-buffered and register-prefetching persistent forms of rounds 1-2 measured
+// slower and were removed in round 6: DESIGN.md §3.2)
 struct PassCfg {
-  int w, lq, db, nt;  // nt != 0: threads per workgroup other than R*W/2^lq
+  int w, lq;
 };
 
-static PassCfg pass_cfg(int logr) {
-  // default: one tile per workgroup (measured faster than the LDS-DMA
-  // double-buffered kernel, whose two tiles halve occupancy: DESIGN.md "NTT")
-  PassCfg def = PassCfg{cols_for(logr), 4, 0, 0};
-  const char* env = getenv("PBF_NTT_CFG");  // "W,LQ,DB" e.g. "16,4,0" (benchmarking override)
-  if (env && *env) {
-    int v[4] = {def.w, def.lq, def.db, 0}, i = 0;
-    for (const char* c = env; *c && i < 4;) {
-      v[i++] = atoi(c);
-      while (*c && *c != ',') ++c;
-      if (*c == ',') ++c;
-    }
-    return PassCfg{v[0], v[1], v[2], v[3]};
-  }
-  return def;
-}
+static PassCfg pass_cfg(int logr) { return PassCfg{cols_for(logr), 4}; }
 
-#define PBF_PASS(F, LR, W, LQ, E)                                                              \
-  if (logr == LR && c.w == W && c.lq == LQ && !c.db && !c.nt) return ntt_pass_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
-#define PBF_PASS_DB(F, LR, W, LQ, E)                                                           \
-  if (logr == LR && c.w == W && c.lq == LQ && c.db == 1) return ntt_pass_db_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
-#define PBF_PASS_NT(F, LR, W, LQ, NTH, E)                                                      \
-  if (logr == LR && c.w == W && c.lq == LQ && !c.db && c.nt == NTH) return ntt_pass_kernel<F, LR, W, NTH, LQ, E>;
-#define PBF_PASS_RP(F, LR, W, LQ, E)                                                           \
-  if (logr == LR && c.w == W && c.lq == LQ && c.db == 2) return ntt_pass_rp_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
+#define PBF_PASS(F, LR, W, LQ, E) \
+  if (logr == LR && c.w == W && c.lq == LQ) return ntt_pass_kernel<F, LR, W, ((W << LR) >> LQ), LQ, E>;
 
 template <class F, int E>
 static PassFn pass_fn_e(int logr, PassCfg c) {
-  PBF_PASS_DB(F, 10, 8, 4, E)  // A/B only (PBF_NTT_CFG=8,4,1): measured slower, DESIGN.md "NTT"
-  PBF_PASS_RP(F, 10, 8, 4, E)  // A/B only (PBF_NTT_CFG=8,4,2)
   PBF_PASS(F, 10, 8, 4, E)
   PBF_PASS(F, 11, 8, 4, E)
   PBF_PASS(F, 12, 4, 4, E)
@@ -496,122 +356,36 @@ int launch_shard_combine(FieldKind k, const FieldArgs& fa, const TwoLevel& tl, u
   return combine_typed<Mod32>(fa, tl, G, rank, in, out, nl, batch, inverse, s);
 }
 
-// Persistent grid: every resident workgroup slot once (blocks per CU from the
-// occupancy query x CUs), never more than there are tiles.
-// The answer depends only on the kernel, the block size and the device, never on a context's
-// state, so one process-wide table under a lock serves every context (pbf.h: contexts share
-// no mutable state a caller could observe).
-uint32_t persistent_grid(const void* fn, int nt, uint64_t tiles) {
-  static std::mutex mu;
-  static std::map<std::tuple<const void*, int, int>, uint32_t> cache;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const auto key = std::make_tuple(fn, nt, dev);
-  uint32_t slots;
-  {
-    std::lock_guard<std::mutex> g(mu);
-    auto it = cache.find(key);
-    if (it != cache.end()) {
-      slots = it->second;
-    } else {
-      int cus = 256, per_cu = 1;
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nt, 0) != hipSuccess || per_cu < 1)
-        per_cu = 1;
-      slots = (uint32_t)(cus * per_cu);
-      cache[key] = slots;
-    }
-  }
-  const char* env = getenv("PBF_NTT_GRID_MULT");  // A/B: oversubscribe the persistent grid
-  if (env) slots *= (uint32_t)atoi(env);
-  return (uint32_t)(tiles < slots ? tiles : slots);
-}
-
 typedef void (*GlPassFn)(GlPassArgs);
 
-#define PBF_GL_K(LR, FIRST, T) (persist ? ntt_gl_pass_pkernel<LR, E, FIRST, T> : ntt_gl_pass_kernel<LR, E, FIRST, T>)
-
-template <int E, int T>
-static GlPassFn gl_fn_t(int logr, bool first, bool persist) {
-  switch (logr) {
-    case 6: return first ? PBF_GL_K(6, true, T) : PBF_GL_K(6, false, T);
-    case 7: return first ? PBF_GL_K(7, true, T) : PBF_GL_K(7, false, T);
-    case 8: return first ? PBF_GL_K(8, true, T) : PBF_GL_K(8, false, T);
-    case 9: return first ? PBF_GL_K(9, true, T) : PBF_GL_K(9, false, T);
-    default: return nullptr;
-  }
-}
-
-// Tile of R x W elements per workgroup: 4096 (four workgroups per CU) or 8192 (two);
-// radix 2^10 always 8192 (W >= 8: 64-B runs in HBM).
-static int gl_tile(int logr) {
-  const char* env = getenv("PBF_NTT_TILE");  // A/B override
-  const int e = env ? atoi(env) : 0;
-  if (logr >= 10) return e == 16384 ? 16384 : 8192;
-  return e == 8192 ? 8192 : 4096;
-}
+// Tile of R x W elements per workgroup: radix 2^10 8192 (W = 8: 64-B runs in HBM, two
+// workgroups per CU), smaller radices 4096 (W >= 16; four or five workgroups per CU). Wider
+// tiles (W = 16 at 2^10: one workgroup per CU) measured slower in round 4.
+static int gl_tile(int logr) { return logr >= 10 ? 8192 : 4096; }
 
 template <int E>
-static GlPassFn gl_fn_e(int logr, bool first, int tile, bool persist) {
-  if (logr == 10 && tile == 16384) return first ? PBF_GL_K(10, true, 16384) : PBF_GL_K(10, false, 16384);
-  if (logr == 10) return first ? PBF_GL_K(10, true, 8192) : PBF_GL_K(10, false, 8192);
-  return tile == 8192 ? gl_fn_t<E, 8192>(logr, first, persist) : gl_fn_t<E, 4096>(logr, first, persist);
-}
-#undef PBF_GL_K
-
-// blocked-intermediate variants (two-pass plans), the default tile of each radix
-template <int E>
-static GlPassFn gl_fn_blk(int logr, bool first) {
-#define PBF_GL_B(LR, T) (first ? ntt_gl_pass_kernel<LR, E, true, T, true> : ntt_gl_pass_kernel<LR, E, false, T, true>)
+static GlPassFn gl_fn_e(int logr, bool first) {
   switch (logr) {
-    case 6: return PBF_GL_B(6, 4096);
-    case 7: return PBF_GL_B(7, 4096);
-    case 8: return PBF_GL_B(8, 4096);
-    case 9: return PBF_GL_B(9, 4096);
-    case 10: return PBF_GL_B(10, 8192);
+    case 6: return first ? ntt_gl_pass_kernel<6, E, true, 4096> : ntt_gl_pass_kernel<6, E, false, 4096>;
+    case 7: return first ? ntt_gl_pass_kernel<7, E, true, 4096> : ntt_gl_pass_kernel<7, E, false, 4096>;
+    case 8: return first ? ntt_gl_pass_kernel<8, E, true, 4096> : ntt_gl_pass_kernel<8, E, false, 4096>;
+    case 9: return first ? ntt_gl_pass_kernel<9, E, true, 4096> : ntt_gl_pass_kernel<9, E, false, 4096>;
+    case 10: return first ? ntt_gl_pass_kernel<10, E, true, 8192> : ntt_gl_pass_kernel<10, E, false, 8192>;
     default: return nullptr;
   }
-#undef PBF_GL_B
 }
 
 // the regrouped 2^24 plan's three pass kernels
 template <int E>
 static GlPassFn gl_fn_rg(int pass) {
-  if (pass == 0) return ntt_gl_pass_kernel<8, E, true, 4096, false, 1>;
-  if (pass == 1) return getenv("PBF_NTT_T2GEO") ? ntt_gl_rg2_kernel<E, true> : ntt_gl_rg2_kernel<E, false>;
-  return ntt_gl_pass_kernel<8, E, false, 4096, false, 3>;
+  if (pass == 0) return ntt_gl_pass_kernel<8, E, true, 4096, 1>;
+  if (pass == 1) return ntt_gl_rg2_kernel<E>;
+  return ntt_gl_pass_kernel<8, E, false, 4096, 3>;
 }
-
-// one pass launch of a group, recorded instead of launched (the dual-group schedule below)
-struct GlLaunch {
-  GlPassFn fn;
-  uint32_t grid, block;
-  size_t lds;
-  GlPassArgs a;
-};
 
 // Passes of a standard-root Goldilocks plan through ntt_gl_pass_kernel (ntt_gl.hpp).
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0,
-                        std::vector<GlLaunch>* rec = nullptr);
-
-// Padded intermediates (PBF_NTT_PAD = elements per row, A/B): the scratch between passes i and
-// i+1 keeps each of its rows (n / R_(i+1) elements: what pass i+1 reads as one row r) `pad`
-// elements apart, breaking the power-of-two strides of the strided reads. Not with the
-// persistent or blocked variants.
-static uint64_t gl_pad(const NttPlan& p) {
-  const char* e = getenv("PBF_NTT_PAD");
-  if (!e || !p.gl || p.logr.size() < 2 || getenv("PBF_NTT_PERSIST") || getenv("PBF_NTT_BLK")) return 0;
-  const long long v = atoll(e);
-  return v > 0 && v <= 4096 ? (uint64_t)v : 0;
-}
-// elements per polynomial in the scratch buffers
-static uint64_t gl_pitch(const NttPlan& p) {
-  const uint64_t pad = gl_pad(p);
-  uint64_t rows = 0;
-  for (size_t i = 1; i < p.logr.size(); ++i) rows = std::max<uint64_t>(rows, 1ull << p.logr[i]);
-  return p.n + rows * pad;
-}
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff = 0);
 
 int ForkSet::ensure(int streams) {
   if (streams > GL_MAX_STREAMS) streams = GL_MAX_STREAMS;
@@ -620,35 +394,11 @@ int ForkSet::ensure(int streams) {
     if (!aux[i]) PBF_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     if (!join[i]) PBF_HIP(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
   }
-  if (!flags) {
-    PBF_HIP(hipMalloc((void**)&flags, GL_MAX_STREAMS * sizeof(uint64_t)));
-    PBF_HIP(hipMemset(flags, 0, GL_MAX_STREAMS * sizeof(uint64_t)));
-    PBF_HIP(hipDeviceSynchronize());
-  }
-  return 0;
-}
-
-int ForkSet::ensure_q(size_t n) {
-  if (n <= qctr_n) return 0;
-  if (qctr) {
-    PBF_HIP(hipDeviceSynchronize());  // a launch still using the old counters
-    PBF_HIP(hipFree(qctr));
-    qctr = nullptr;
-    qctr_n = 0;
-  }
-  PBF_HIP(hipMalloc((void**)&qctr, n * sizeof(uint32_t)));
-  PBF_HIP(hipMemset(qctr, 0, n * sizeof(uint32_t)));
-  PBF_HIP(hipDeviceSynchronize());
-  qctr_n = n;
   return 0;
 }
 
 ForkSet::~ForkSet() {
   (void)hipSetDevice(device);
-  if (qctr) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(qctr);
-  }
   for (int i = 1; i < GL_MAX_STREAMS; ++i) {
     if (aux[i]) {
       (void)hipStreamSynchronize(aux[i]);
@@ -657,191 +407,51 @@ ForkSet::~ForkSet() {
     if (join[i]) (void)hipEventDestroy(join[i]);
   }
   if (fork) (void)hipEventDestroy(fork);
-  if (flags) (void)hipFree(flags);
-}
-
-// Dual-group schedule of a two-pass plan (round 5, opt-in PBF_NTT_DUAL=1): ONE stream, launches
-// {pass 1 of group 0}, {pass 2 of group g-1 + pass 1 of group g} (one launch, the two roles
-// interleaved in runs of 8 workgroups so both run at once on every XCD: ntt_gl_dual_kernel),
-// ..., {pass 2 of the last group}. Two groups' passes overlap as with the two-stream schedule,
-// without its per-call fork and join (cross-queue event waits, ~20 us of idle GPU per call at
-// 2^20 x 32: profiles/r04/ntt_2p20_timeline.txt). Measured slower (2^20 x 32: 0.411 against
-// 0.357 ms, profiles/r05/dual_ab.log): each launch ends in a tail of its last workgroups that the
-// two-stream schedule fills with the other stream's kernel. Returns -1 when the plan has no
-// dual-group kernel (the caller falls back to the stream schedule).
-typedef void (*GlDualFn)(GlPassArgs, GlPassArgs);
-template <int E>
-static GlDualFn gl_fn_dual(int logr, int tile) {
-  if (logr == 10 && tile == 8192) return ntt_gl_dual_kernel<10, E, 8192>;
-  if (logr == 9 && tile == 4096) return ntt_gl_dual_kernel<9, E, 4096>;
-  if (logr == 8 && tile == 4096) return ntt_gl_dual_kernel<8, E, 4096>;
-  return nullptr;
-}
-
-static int run_gl_dual(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, size_t G, DevBuf& s0,
-                       DevBuf& s1, hipStream_t stream) {
-  if (p.logr.size() != 2 || p.logr[0] != p.logr[1] || batch <= G || p.r4k || gl_pad(p) || getenv("PBF_NTT_BLK") ||
-      getenv("PBF_NTT_PERSIST"))
-    return -1;
-  const int tile = gl_tile(p.logr[0]);
-  const GlDualFn dual = p.e64 == 39 ? gl_fn_dual<39>(p.logr[0], tile) : gl_fn_dual<153>(p.logr[0], tile);
-  if (!dual) return -1;
-  const size_t groups = (batch + G - 1) / G;  // the last one may be smaller
-  std::vector<std::vector<GlLaunch>> L(groups);
-  for (size_t g = 0; g < groups; ++g) {
-    const size_t b = std::min(G, batch - g * G);
-    const int rc = run_gl_group(p, d_in + g * G * p.n, d_out + g * G * p.n, b, s0, s1, stream, 0, g * G * gl_pitch(p),
-                                &L[g]);
-    if (rc) return rc;
-    if (L[g].size() != 2 || L[g][0].block != L[g][1].block) return -1;
-  }
-  auto launch = [&](const GlLaunch& l) -> int {
-    hipLaunchKernelGGL(l.fn, dim3(l.grid), dim3(l.block), l.lds, stream, l.a);
-    PBF_HIP(hipGetLastError());
-    return 0;
-  };
-  int rc = launch(L[0][0]);
-  for (size_t g = 1; g < groups && !rc; ++g) {
-    const GlLaunch &sec = L[g - 1][1], &fst = L[g][0];
-    if (sec.grid == fst.grid && sec.grid % 8 == 0 && !sec.lds && !fst.lds) {
-      hipLaunchKernelGGL(dual, dim3(2 * fst.grid), dim3(fst.block), 0, stream, sec.a, fst.a);
-      PBF_HIP(hipGetLastError());
-    } else {  // unequal groups (the remainder): the two passes one after the other
-      if (!(rc = launch(sec))) rc = launch(fst);
-    }
-  }
-  if (!rc) rc = launch(L[groups - 1][1]);
-  return rc;
-}
-
-// Work-queue schedule (ntt_gl.hpp ntt_gl_queue_kernel): both passes of an equal-radix two-pass
-// plan for the whole batch in one launch on the caller's stream. Returns -1 when the plan or
-// batch has no queue form (the caller falls back to the stream schedule).
-typedef void (*GlQueueFn)(GlQueueArgs);
-template <int E>
-static GlQueueFn gl_fn_queue(int logr, int tile, int pub) {
-#define PBF_GL_Q(LR, T)                                                                                      \
-  if (logr == LR && tile == T)                                                                               \
-    return pub == 0 ? ntt_gl_queue_kernel<LR, E, T, 0> : pub == 1 ? ntt_gl_queue_kernel<LR, E, T, 1>        \
-                                                                   : ntt_gl_queue_kernel<LR, E, T, 2>;
-  PBF_GL_Q(10, 8192)
-  PBF_GL_Q(9, 4096)
-  PBF_GL_Q(8, 4096)
-#undef PBF_GL_Q
-  return nullptr;
-}
-
-static int run_gl_queue(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, ForkSet* fork) {
-  if (!fork || p.logr.size() != 2 || p.logr[0] != p.logr[1] || p.r4k || gl_pad(p) || getenv("PBF_NTT_BLK") ||
-      getenv("PBF_NTT_PERSIST") || getenv("PBF_NTT_NO_PRETW"))
-    return -1;
-  const int tile = gl_tile(p.logr[0]);
-  const char* pe = getenv("PBF_NTT_QPUB");
-  const int pub = pe ? atoi(pe) : 1;
-  const GlQueueFn fn = p.e64 == 39 ? gl_fn_queue<39>(p.logr[0], tile, pub) : gl_fn_queue<153>(p.logr[0], tile, pub);
-  if (!fn) return -1;
-  size_t G = batch % 4 == 0 ? 4 : (batch % 2 == 0 ? 2 : 1);
-  if (const char* g = getenv("PBF_NTT_QG")) {
-    const size_t v = (size_t)atoll(g);
-    if (v >= 1 && batch % v == 0) G = v;
-  }
-  const uint64_t T = p.n / (uint64_t)tile;  // tiles per polynomial and pass
-  if ((G * T) % 8 || batch * T * 2 > 0x7fffffffull) return -1;
-  std::vector<GlLaunch> L;
-  int rc = run_gl_group(p, d_in, d_out, G, s0, s1, stream, 0, 0, &L);
-  if (rc) return rc;
-  if (L.size() != 2 || L[0].lds || L[1].lds || L[0].block != L[1].block || !L[0].a.post_tw || !L[1].a.skip_pass_tw)
-    return -1;
-  const size_t groups = batch / G;
-  if ((rc = fork->ensure_q(9 + groups))) return rc;
-  GlQueueArgs q;
-  q.p1 = L[0].a;
-  q.p2 = L[1].a;
-  q.p1.xcd_kmajor = q.p2.xcd_kmajor = 1;
-  q.ctr = fork->qctr;
-  q.in_gs = q.out_gs = G * p.n;
-  q.scr_gs = G * gl_pitch(p);
-  q.per_class = (uint32_t)(G * T / 8);
-  q.groups = (uint32_t)groups;
-  const char* le = getenv("PBF_NTT_QLAG");
-  q.lag = le ? (uint32_t)atoi(le) : 1;
-  if (q.lag < 1) q.lag = 1;
-  q.total = (uint32_t)(2 * batch * T);
-  hipLaunchKernelGGL(fn, dim3(q.total), dim3(L[0].block), 0, stream, q);
-  PBF_HIP(hipGetLastError());
-  return 0;
 }
 
 static int run_gl_passes(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
-  // round 6 default: the work-queue schedule (one launch, no second stream) for batches of >= 2
-  if (split_log == 0 && batch >= 2 && !env_default_off("PBF_NTT_NO_QUEUE") && !getenv("PBF_NTT_DUAL")) {
-    const int rc = run_gl_queue(p, d_in, d_out, batch, s0, s1, stream, fork);
-    if (rc != -1) return rc;
-  }
-  // default schedule (measured best at 2^20 x 32): groups of 4
-  // polynomials alternating over two streams once the batch has at least 8
-  size_t G = batch >= 8 ? 4 : batch;
-  if (const char* g = getenv("PBF_NTT_GROUP")) G = (size_t)atoll(g);
+  // default schedule (measured best at 2^20 x 32): groups of 4 polynomials
+  // alternating over the caller's stream and a second one once the batch has at least 8, so the
+  // passes of two groups run concurrently and their load / compute / store phases interleave
+  // (options ntt.group = polynomials per group, ntt.streams = streams; 0 or >= batch: one group)
+  const long long go = p.opts.num("ntt.group", -1);
+  const size_t G = go >= 0 ? (size_t)go : (batch >= 8 ? 4 : batch);
   if (split_log != 0 || G == 0 || G >= batch) return run_gl_group(p, d_in, d_out, batch, s0, s1, stream, split_log);
-  if (getenv("PBF_NTT_DUAL") && !getenv("PBF_NTT_STREAMS")) {
-    const int rc = run_gl_dual(p, d_in, d_out, batch, G, s0, s1, stream);
-    if (rc != -1) return rc;  // -1: this plan has no dual-group form
-  }
-  // PBF_NTT_STREAMS=k: groups round-robin over the caller's stream and k-1 more (disjoint
-  // scratch), so the passes of k groups run concurrently and their phases interleave
-  // (the extra streams are the context's own ForkSet; without one everything stays on `stream`)
-  int ns = getenv("PBF_NTT_STREAMS") ? atoi(getenv("PBF_NTT_STREAMS")) : 2;
+  int ns = (int)p.opts.num("ntt.streams", 2);
   ns = ns < 1 ? 1 : (ns > GL_MAX_STREAMS ? GL_MAX_STREAMS : ns);
   if (!fork) ns = 1;
   hipStream_t sts[GL_MAX_STREAMS];
   sts[0] = stream;
-  // fork / join by stream memory operations (round 5 default; PBF_NTT_EVENTS=1 restores hipEvent
-  // waits): a flag written by one stream and waited on by the other resolves faster than an
-  // event wait across hardware queues: 2^20 x 32 0.349-0.352 against 0.357-0.360 ms, three
-  // alternations on one box (profiles/r05/memop_ab.log)
-  // Under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION, which serialises dispatches
-  // across queues) a stream waiting on a flag that another queue writes never resumes: events
-  // there (profiles/r05/memop_prof.log).
-  const bool memop = getenv("PBF_NTT_EVENTS") == nullptr && getenv("ROCPROF_COUNTER_COLLECTION") == nullptr;
-  uint64_t seq = 0;
+  // Fork and join by events: a stream waiting on an event waits in the command processor
+  // (a barrier packet), so it cannot hold the GPU against the work it waits for. Round 5's
+  // stream memory-operation joins (hipStreamWaitValue64: a spinning wait kernel) measured 1-4 %
+  // faster but never resumed when the queues were serialised (rocprofv3 counter collection,
+  // profiles/r05/memop_prof.log); removed in round 6.
   if (ns > 1) {
     int rc = fork->ensure(ns);
     if (rc) return rc;
     for (int i = 1; i < ns; ++i) sts[i] = fork->aux[i];
-    if (memop) {
-      seq = ++fork->seq;
-      PBF_HIP(hipStreamWriteValue64(stream, fork->flags, seq, 0));
-      for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitValue64(sts[i], fork->flags, seq, hipStreamWaitValueGte, ~0ull));
-    } else {
-      PBF_HIP(hipEventRecord(fork->fork, stream));
-      for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], fork->fork, 0));
-    }
+    PBF_HIP(hipEventRecord(fork->fork, stream));
+    for (int i = 1; i < ns; ++i) PBF_HIP(hipStreamWaitEvent(sts[i], fork->fork, 0));
   }
   int gi = 0;
   for (size_t g0 = 0; g0 < batch; g0 += G, ++gi) {
     const size_t b = batch - g0 < G ? batch - g0 : G;
     const int rc = run_gl_group(p, d_in + g0 * p.n, d_out + g0 * p.n, b, s0, s1, sts[gi % ns], 0,
-                                ns > 1 ? g0 * gl_pitch(p) : 0);
+                                ns > 1 ? g0 * p.n : 0);
     if (rc) return rc;
   }
-  if (ns > 1) {
-    for (int i = 1; i < ns; ++i) {
-      if (memop) {
-        PBF_HIP(hipStreamWriteValue64(sts[i], fork->flags + i, seq, 0));
-        PBF_HIP(hipStreamWaitValue64(stream, fork->flags + i, seq, hipStreamWaitValueGte, ~0ull));
-      } else {
-        PBF_HIP(hipEventRecord(fork->join[i], sts[i]));
-        PBF_HIP(hipStreamWaitEvent(stream, fork->join[i], 0));
-      }
-    }
+  for (int i = 1; i < ns; ++i) {
+    PBF_HIP(hipEventRecord(fork->join[i], sts[i]));
+    PBF_HIP(hipStreamWaitEvent(stream, fork->join[i], 0));
   }
   return 0;
 }
 
 // The regrouped plan's twiddle tables, built on the first run that takes the regrouped path:
-// tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18), t3[f][a0][j] (2^24, n^-1 folded in for the inverse)
+// tc1[a2l][r2][k1] (4096), t2[a1][K] (2^18), and the last pass's C[r2][X] = w^(r2 X) (n^-1
+// folded in for the inverse), D[X] = w^(4 X) (X < 2^18: 10 MiB)
 static int ensure_rg_tables(const NttPlan& p) {
   if (p.rg_built) return 0;
   const uint64_t m = p.m, n = p.n;
@@ -861,17 +471,9 @@ static int ensure_rg_tables(const NttPlan& p) {
     uint64_t y = 1;
     for (uint64_t K = 0; K < 4096; ++K) { t2[(a1 << 12) + K] = y; y = hmul(y, st, m); }
   }
-  std::vector<uint64_t> t3(1ull << 24);
+  // the last pass's twiddle w^(a0 X) (a0 = r2 + 4 s2, X = 65536 f + j) as C[r2][X] D[X]^s2 (round
+  // 5: from 10 MiB instead of a 2^24-entry, 128 MiB table T3[f][a0][j], profiles/r05/t3geo_ab.log)
   const uint64_t scale = inverse ? p.n_inv : 1;
-  for (uint64_t fq = 0; fq < 4; ++fq)
-    for (uint64_t a0 = 0; a0 < 64; ++a0) {
-      const uint64_t st = hpow(w, a0, m);
-      uint64_t y = hmul(hpow(w, (65536 * a0 * fq) % n, m), scale, m);
-      uint64_t* row = t3.data() + ((fq * 64 + a0) << 16);
-      for (uint64_t j = 0; j < 65536; ++j) { row[j] = y; y = hmul(y, st, m); }
-    }
-  // the last pass's twiddle w^(a0 X) (a0 = r2 + 4 s2, X = 65536 f + j) as C[r2][X] D[X]^s2 with
-  // C = w^(r2 X) (n^-1 folded in for the inverse), D = w^(4 X): 10 MiB instead of 128
   std::vector<uint64_t> tgc(4ull << 18), tgb(1ull << 18);
   {
     const uint64_t w4 = hpow(w, 4, m);
@@ -887,92 +489,17 @@ static int ensure_rg_tables(const NttPlan& p) {
       x4 = hmul(x4, w4, m);
     }
   }
-  std::vector<uint64_t> t2d(64);
-  for (uint64_t a1 = 0; a1 < 64; ++a1) t2d[a1] = hpow(w, (16384 * a1) % n, m);
-  if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_t3, t3)) ||
-      (rc = upload(p.rg_tgc, tgc)) || (rc = upload(p.rg_tgb, tgb)) || (rc = upload(p.rg_t2d, t2d)))
+  if ((rc = upload(p.rg_tc1, tc1)) || (rc = upload(p.rg_t2, t2)) || (rc = upload(p.rg_tgc, tgc)) ||
+      (rc = upload(p.rg_tgb, tgb)))
     return rc;
   p.rg_built = true;
   return 0;
 }
 
-// The two-pass plan's tables (ntt_r4k.hpp): tst[b][c] = w_4096^(b c) for pass 1, the same times
-// n^-1 for an inverse's pass 2, post[j][k] = w^(j k) (2^24 entries) for pass 1's stores
-static int ensure_r4k_tables(const NttPlan& p) {
-  if (p.r4k_built) return 0;
-  const uint64_t m = p.m;
-  uint64_t w = p.omega;
-  if (p.inverse && !hinv(p.omega, m, &w)) return fail(1, "omega not invertible");
-  const uint64_t w4096 = hpow(w, 4096, m);
-  std::vector<uint64_t> t1(4096), t2(4096);
-  for (uint64_t b = 0; b < 64; ++b)
-    for (uint64_t c = 0; c < 64; ++c) {
-      t1[b * 64 + c] = hpow(w4096, b * c, m);
-      t2[b * 64 + c] = p.inverse ? hmul(t1[b * 64 + c], p.n_inv, m) : t1[b * 64 + c];
-    }
-  std::vector<uint64_t> post(1ull << 24);
-  for (uint64_t j = 0; j < 4096; ++j) {
-    const uint64_t st = hpow(w, j, m);
-    uint64_t y = 1;
-    uint64_t* row = post.data() + (j << 12);
-    for (uint64_t k = 0; k < 4096; ++k) { row[k] = y; y = hmul(y, st, m); }
-  }
-  int rc;
-  if ((rc = upload(p.r4k_tst1, t1)) || (rc = upload(p.r4k_tst2, t2)) || (rc = upload(p.r4k_post, post))) return rc;
-  p.r4k_built = true;
-  return 0;
-}
-
-// ntt_r4k.hip
-int launch_r4k_pass(const R4kArgs& a, bool first, int e64, uint32_t tiles, bool persist, hipStream_t stream);
-
-static int run_r4k(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                   hipStream_t stream, size_t soff) {
-  int rc = ensure_r4k_tables(p);
-  if (rc) return rc;
-  if (batch * 512 > 0x7fffffffull) return fail(1, "batch too large");
-  R4kArgs a;
-  a.batch = (uint32_t)batch;
-  a.kmajor = batch > 1 && !getenv("PBF_NTT_NO_KMAJOR") ? 1 : 0;
-  const uint32_t grid = (uint32_t)(512 * batch);
-  // pass 1: in -> s0 (inter-pass twiddle applied at the stores)
-  a.in = d_in;
-  a.out = (uint64_t*)s0.p + soff;
-  a.tst = (const uint64_t*)p.r4k_tst1.p;
-  a.post = (const uint64_t*)p.r4k_post.p;
-  a.scaled = 0;
-  const char* mode = getenv("PBF_NTT_R4K");
-  const bool persist = mode && mode[0] == '2';
-  if ((rc = launch_r4k_pass(a, true, p.e64, grid, persist, stream))) return rc;
-  // pass 2: s0 -> out (n^-1 in the stage table of an inverse)
-  a.in = (const uint64_t*)s0.p + soff;
-  a.out = d_out;
-  a.tst = (const uint64_t*)p.r4k_tst2.p;
-  a.post = nullptr;
-  a.scaled = p.inverse ? 1 : 0;
-  if ((rc = launch_r4k_pass(a, false, p.e64, grid, persist, stream))) return rc;
-  return 0;
-}
-
 static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
-                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff, std::vector<GlLaunch>* rec) {
-  if (p.r4k && split_log == 0 && gl_pad(p) == 0) return run_r4k(p, d_in, d_out, batch, s0, stream, soff);
+                        DevBuf& s1, hipStream_t stream, uint32_t split_log, size_t soff) {
   const size_t P = p.logr.size();
-  // two-pass plans with equal tile widths may keep the intermediate blocked (ntt_gl.hpp BLK)
-  bool blk = false;
-  uint32_t blk_log = 0;
-  // opt-in (PBF_NTT_BLK): measured level with the natural layout
-  if (P == 2 && getenv("PBF_NTT_BLK") && !getenv("PBF_NTT_PERSIST")) {
-    const int t0 = gl_tile(p.logr[0]), t1 = gl_tile(p.logr[1]);
-    const uint64_t w0 = (uint64_t)t0 >> p.logr[0], w1 = (uint64_t)t1 >> p.logr[1];
-    const bool dflt = (t0 == (p.logr[0] >= 10 ? 8192 : 4096)) && (t1 == (p.logr[1] >= 10 ? 8192 : 4096));
-    if (w0 == w1 && dflt && (p.n >> p.logr[0]) % w0 == 0 && (p.n >> p.logr[1]) % w1 == 0) {
-      blk = true;
-      while ((1ull << blk_log) < w1) ++blk_log;
-    }
-  }
-  const bool rg = p.rg && P == 3 && split_log == 0 && !blk && gl_pad(p) == 0 && !getenv("PBF_NTT_PERSIST") &&
-                  gl_tile(8) == 4096;
+  const bool rg = p.rg && P == 3 && split_log == 0;
   if (rg) {
     const int rc = ensure_rg_tables(p);
     if (rc) return rc;
@@ -981,10 +508,7 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
     const int tile = gl_tile(lr);
-    const bool persist = getenv("PBF_NTT_PERSIST") != nullptr;  // A/B: pipelined persistent kernel
-    GlPassFn fn =
-        p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0, tile, persist) : gl_fn_e<153>(lr, log_ns == 0, tile, persist);
-    if (blk) fn = p.e64 == 39 ? gl_fn_blk<39>(lr, log_ns == 0) : gl_fn_blk<153>(lr, log_ns == 0);
+    GlPassFn fn = p.e64 == 39 ? gl_fn_e<39>(lr, log_ns == 0) : gl_fn_e<153>(lr, log_ns == 0);
     if (rg) fn = p.e64 == 39 ? gl_fn_rg<39>((int)i) : gl_fn_rg<153>((int)i);
     if (!fn) return fail(1, "no Goldilocks pass kernel for this radix");
     const uint64_t W = (uint64_t)tile >> lr;
@@ -992,17 +516,12 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     GlPassArgs a;
     a.in = (i == 0) ? d_in : (const uint64_t*)(((i - 1) & 1) ? s1.p : s0.p) + soff;
     a.out = (i == P - 1) ? d_out : (uint64_t*)((i & 1) ? s1.p : s0.p) + soff;
-    const uint64_t pad = blk ? 0 : gl_pad(p), pitch = gl_pitch(p);
-    a.in_pitch = (i == 0) ? p.n : pitch;
-    a.out_pitch = (i == P - 1) ? p.n : pitch;
-    a.in_pad = (i == 0) ? 0 : (uint32_t)pad;
-    a.out_pad = (i == P - 1) ? 0 : (uint32_t)pad;
-    a.out_rows_log = (i == P - 1) ? 0 : p.log_n - (uint32_t)p.logr[i + 1];
+    a.in_pitch = a.out_pitch = p.n;
     a.twpass = (const uint64_t*)p.twpass[i]->p;
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;
     a.tc = (const uint64_t*)p.tc[i]->p;
-    const bool tws = !a.twpass && i == P - 1 && p.tws_a && (uint64_t)p.tws_w == W && !blk;
+    const bool tws = !a.twpass && i == P - 1 && p.tws_a && (uint64_t)p.tws_w == W;
     a.tws_a = tws ? (const uint64_t*)p.tws_a->p : nullptr;
     a.tws_b = tws ? (const uint64_t*)p.tws_b->p : nullptr;
     a.n = p.n;
@@ -1015,67 +534,35 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
     a.out_split_log = (i == P - 1) ? split_log : 0;
     const uint64_t tiles = (uint64_t)a.blocks_per_poly * batch;
     if (tiles > 0x7fffffffull) return fail(1, "batch too large");
-    a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
-    a.blk_log = blk_log;
+    // tile order (gl_tile_coords): later passes XCD k-major (the pass-twiddle table's slices
+    // fetched into each XCD's L2 once per pass, not once per polynomial)
+    a.xcd_kmajor = (log_ns > 0 && batch > 1 && tiles % 8 == 0) ? 1 : 0;
     // two-pass plans apply the second pass's twiddle w^(j k) at the first pass's stores (the
     // first pass hides the product under its memory phase: 2^20 x 32 0.400 -> 0.386 ms,
-    // DESIGN.md §3.1); PBF_NTT_NO_PRETW=1 restores it at the second pass's loads
+    // DESIGN.md §3.1), reading that table by column in XCD k-major order too (round 4: 2^20 x 32
+    // 0.354-0.357 ms against 0.368-0.371 linear, profiles/r04/ntt_orders_sweep.log)
     a.post_tw = nullptr;
     a.skip_pass_tw = 0;
-    if (P == 2 && !blk && pad == 0 && split_log == 0 && !persist && !getenv("PBF_NTT_NO_PRETW") && p.twpass[1]->p) {
+    if (P == 2 && split_log == 0 && p.twpass[1]->p) {
       if (i == 0) a.post_tw = (const uint64_t*)p.twpass[1]->p;
       else a.skip_pass_tw = 1;
     }
-    // the first pass of a 2-pass plan reads the second pass's twiddle table by column too
-    // (post_tw): k-major keeps its rows in the XCD's L2 across the polynomials of a block
-    // (round 4: 2^20 x 32 0.354-0.357 ms against 0.368-0.371 linear, profiles/r04/ntt_orders_sweep.log)
-    if (a.post_tw && batch > 1 && tiles % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) a.xcd_kmajor = 1;
-    if (rg && i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
-    if (rg && i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
-    if (rg && i == 1 && getenv("PBF_NTT_T2GEO")) a.tws_b = (const uint64_t*)p.rg_t2d.p;  // A/B (ntt_gl_rg2_kernel)
-    if (rg && i == 2) a.twpass = (const uint64_t*)p.rg_t3.p;
-    // round 5: the last pass forms its twiddles as C[r2][X] D[X]^s2 from 10 MiB of tables instead
-    // of reading the 128 MiB T3 (one more product per element): 2 x 2^24 0.390-0.392 against
-    // 0.411-0.412 ms, three alternations (profiles/r05/t3geo_ab.log); PBF_NTT_T3GEO=0 reads T3
-    const char* geo_env = getenv("PBF_NTT_T3GEO");
-    if (rg && i == 2 && !(geo_env && geo_env[0] == '0')) {
-      a.twpass = nullptr;
-      a.tws_a = (const uint64_t*)p.rg_tgc.p;
-      a.tws_b = (const uint64_t*)p.rg_tgb.p;
-    }
-    // the regrouped 2^24 plan takes the XCD-blocked order in every pass (round 4: 2 x 2^24
-    // 0.433-0.437 ms against 0.447-0.453 k-major, 0.462-0.466 linear, five alternations on one
-    // box, profiles/r04/ntt_order24_ab.log); the 2-pass plans keep k-major (2^20 x 32: 0.352-0.355
-    // k-major against 0.362-0.364, profiles/r04/ntt_order_ab.log)
-    if (rg && tiles % 8 == 0) a.xcd_kmajor = 2;
-    // round 5: the last pass takes XCD k-major instead (both polynomials of a column block on one
-    // XCD, so each slice of its 128 MiB T3 table is read into one L2 once, not once per XCD of
-    // each polynomial): calibrated traffic 1.886 -> 1.753 GB per 2 x 2^24 step, time level
-    // (0.4375-0.4433 against 0.4362-0.4379 ms, profiles/r05/order24.log)
-    // With the geometric last pass (below) there is no T3 to share: XCD-blocked again (orders 222
-    // 0.3867-0.3868 against 221 0.3918-0.3930 ms, profiles/r05/order_geo.log)
-    const char* geo_off = getenv("PBF_NTT_T3GEO");
-    if (rg && i == 2 && batch > 1 && tiles % 8 == 0 && geo_off && geo_off[0] == '0') a.xcd_kmajor = 1;
-    if (const char* o = getenv("PBF_NTT_ORDER")) {  // A/B: 0 linear, 1 k-major per XCD, 2 XCD-blocked
-      const uint32_t ord = (uint32_t)atoi(o);
-      a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
-    }
-    if (const char* o = getenv("PBF_NTT_ORDERS")) {  // A/B: one digit per pass, e.g. "021"
-      if (strlen(o) > i && o[i] >= '0' && o[i] <= '2') {
-        const uint32_t ord = (uint32_t)(o[i] - '0');
-        a.xcd_kmajor = (tiles % 8 == 0 && (ord != 1 || batch > 1)) ? ord : 0;
+    if (a.post_tw && batch > 1 && tiles % 8 == 0) a.xcd_kmajor = 1;
+    if (rg) {
+      if (i == 0) a.tc = (const uint64_t*)p.rg_tc1.p;
+      if (i == 1) a.twpass = (const uint64_t*)p.rg_t2.p;
+      if (i == 2) {
+        a.twpass = nullptr;
+        a.tws_a = (const uint64_t*)p.rg_tgc.p;
+        a.tws_b = (const uint64_t*)p.rg_tgb.p;
       }
+      // XCD-blocked order in every pass of the regrouped plan (round 4: 2 x 2^24 0.433-0.437 ms
+      // against 0.447-0.453 k-major, 0.462-0.466 linear, profiles/r04/ntt_order24_ab.log; round
+      // 5 with the geometric last pass 0.3867-0.3868 against 0.3918-0.3930, order_geo.log)
+      if (tiles % 8 == 0) a.xcd_kmajor = 2;
     }
-    const uint32_t grid = persist ? persistent_grid((const void*)fn, tile / 16, tiles) : (uint32_t)tiles;
-    // A/B diagnostic: extra dynamic LDS per workgroup (PBF_NTT_LDSPAD bytes) lowers the
-    // workgroups resident per CU without changing the code
-    const size_t ldspad = getenv("PBF_NTT_LDSPAD") ? (size_t)atoll(getenv("PBF_NTT_LDSPAD")) : 0;
-    if (rec) {
-      rec->push_back(GlLaunch{fn, grid, (uint32_t)(tile / 16), ldspad, a});
-    } else {
-      hipLaunchKernelGGL(fn, dim3(grid), dim3(tile / 16), ldspad, stream, a);
-      PBF_HIP(hipGetLastError());
-    }
+    hipLaunchKernelGGL(fn, dim3((uint32_t)tiles), dim3(tile / 16), 0, stream, a);
+    PBF_HIP(hipGetLastError());
     log_ns += lr;
   }
   return 0;
@@ -1084,7 +571,6 @@ static int run_gl_group(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out,
 static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out, size_t batch, DevBuf& s0,
                          DevBuf& s1, hipStream_t stream, uint32_t split_log, ForkSet* fork) {
   if (batch == 0) return 0;
-  if (p.ip && split_log == 0 && p.n > 1) return run_ip(p, d_in, d_out, batch, s0, stream);
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * 8, hipMemcpyDeviceToDevice, stream));
     return 0;  // size-1 DFT is the identity; n^-1 = 1
@@ -1100,9 +586,9 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     return 0;
   }
   const size_t P = p.logr.size();
-  const size_t bytes = batch * (p.gl ? gl_pitch(p) : p.n) * 8;
+  const size_t bytes = batch * p.n * 8;
   int rc = s0.ensure(bytes);
-  if (!rc && P > 2 && !(p.r4k && split_log == 0 && gl_pad(p) == 0)) rc = s1.ensure(bytes);
+  if (!rc && P > 2) rc = s1.ensure(bytes);
   if (rc) return rc;
   uint32_t log_ns = 0;
   if (p.gl) return run_gl_passes(p, d_in, d_out, batch, s0, s1, stream, split_log, fork);
@@ -1112,7 +598,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     PassFn fn = pass_fn(p.kind, p.e64, lr, cfg);
     for (int w : {16, 8, 4}) {  // robust fallback: any instantiated single-tile shape
       if (fn) break;
-      cfg = PassCfg{w, 4, 0};
+      cfg = PassCfg{w, 4};
       fn = pass_fn(p.kind, p.e64, lr, cfg);
     }
     if (!fn) return fail(1, "no kernel for this radix");
@@ -1123,7 +609,7 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     a.tw0 = (const uint64_t*)p.tw0.p;
     a.tw1 = (const uint64_t*)p.tw1.p;
     a.rtab = (const uint64_t*)p.rtab[i]->p;
-    a.twfull = (const uint64_t*)p.twfull.p;
+    a.twfull = nullptr;
     a.twpass = (const uint64_t*)p.twpass[i]->p;
     a.n = p.n;
     a.n_inv = p.n_inv;
@@ -1133,14 +619,14 @@ static int run_plan_impl(const NttPlan& p, const uint64_t* d_in, uint64_t* d_out
     a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
     a.scale = (p.inverse && i == P - 1) ? 1 : 0;
     a.out_split_log = (i == P - 1) ? split_log : 0;
-    a.dbg = getenv("PBF_NTT_DBG") ? (uint32_t)atoi(getenv("PBF_NTT_DBG")) : 0;
+    a.dbg = 0;
     a.batch = (uint32_t)batch;
     a.f = p.fa;
-    const int nt = cfg.nt ? cfg.nt : (W << lr) >> cfg.lq;
+    const int nt = (W << lr) >> cfg.lq;
     const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
     if (blocks > 0x7fffffffull) return fail(1, "batch too large");
-    const uint32_t grid = cfg.db ? persistent_grid((const void*)fn, nt, blocks) : (uint32_t)blocks;  // modes 1, 2: persistent
-    a.xcd_kmajor = (!cfg.db && log_ns > 0 && batch > 1 && grid % 8 == 0 && !getenv("PBF_NTT_NO_KMAJOR")) ? 1 : 0;
+    const uint32_t grid = (uint32_t)blocks;
+    a.xcd_kmajor = (log_ns > 0 && batch > 1 && grid % 8 == 0) ? 1 : 0;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(nt), 0, stream, a);
     PBF_HIP(hipGetLastError());
     log_ns += lr;

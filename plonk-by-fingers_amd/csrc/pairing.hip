@@ -1491,14 +1491,15 @@ static int pairing_values(pbf_ctx* ctx, const uint64_t* d_g1, const uint64_t* d_
   int rc = ensure_inv2k(ctx->device);
   if (rc) return rc;
   const PairingConsts k = make_consts();
-  const char* lane_env = getenv("PBF_PAIR_LANE");  // A/B: 1 forces the lane engine, 0 the workgroup one
-  const bool lane = lane_env ? lane_env[0] == '1' : (n >= PAIR_LANE_MIN && !getenv("PBF_PAIR_WG"));
+  // option pair.engine = "lane" / "wg" forces an engine (the tests' cross-check)
+  const char* eng = ctx->options.get("pair.engine");
+  const bool lane = eng ? strcmp(eng, "lane") == 0 : n >= PAIR_LANE_MIN;
   if (lane) {
     const uint32_t waves = (uint32_t)((n + 63) / 64);
     int dev_cus = 0;
     PBF_HIP(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     bool two = waves >= (uint32_t)(8 * dev_cus);  // at least two waves per SIMD (four SIMDs per CU)
-    if (const char* w = getenv("PBF_PAIR_LANE_WPE")) two = w[0] == '2';  // A/B and tests: force a build
+    if (const char* w = ctx->options.get("pair.lane_wpe")) two = w[0] == '2';  // option (tests): force a build
     if (two)
       hipLaunchKernelGGL(pairing_lane_kernel<2>, dim3(waves), dim3(64), 0, s, d_g1, d_g2, n, d_out, k);
     else

@@ -1312,7 +1312,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
     }
   }
   {
-    const char* qc = getenv("PBF_QUOT_CHUNK");
+    const char* qc = ab_env("PBF_QUOT_CHUNK");
     const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
     hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, Wq, qch);
     PBF_HIP(hipGetLastError());
@@ -1484,7 +1484,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   Prover P;
   P.ctx = ctx;
   P.s = (hipStream_t)stream;
-  P.timing = getenv("PBF_PROVER_TIMING") != nullptr;
+  P.timing = ctx->options.num("prover.timing", 0) != 0;
   P.mark("start");
   P.n = n;
   P.N = 4 * n;
@@ -1537,9 +1537,9 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // slots) are kept in the context and reused while the circuit is the same -- what a
   // PLONK proving key holds -- validated on every call by comparing d_q and d_copies with the
   // context's device copies of the gates and copies the key was built from (exact content).
-  // PBF_PROVER_NO_PK=1 recomputes them per proof, as the reference does (plonk.rs:233-243,
+  // Option prover.pk = 0 recomputes them per proof, as the reference does (plonk.rs:233-243,
   // 339-370).
-  const bool pk_on = !getenv("PBF_PROVER_NO_PK");  // sharded too: this rank's coset blocks
+  const bool pk_on = ctx->options.num("prover.pk", 1) != 0;  // sharded too: this rank's coset blocks
   bool pk_hit = false;
   uint64_t* pkcoef = nullptr;
   uint64_t* pkcoset = nullptr;
@@ -1770,7 +1770,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   }
   uint64_t* tq = (uint64_t*)B.t.p;
   {
-    const char* qc = getenv("PBF_QUOT_CHUNK");
+    const char* qc = ab_env("PBF_QUOT_CHUNK");
     const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
     hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, W0, qch);
   }
@@ -2032,7 +2032,7 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   const U256 k1 = hm(k1k2), k2 = hm(k1k2 + 4);
   uint64_t pre[8][8];
   std::vector<uint64_t> vk_key;
-  const bool vk_on = !getenv("PBF_VERIFIER_NO_VK");
+  const bool vk_on = ctx->options.num("verifier.vk", 1) != 0;
   if (vk_on) {
     const SnapItem items[3] = {{"q", d_q, 20 * (uint64_t)n},
                                {"copies", d_copies, 6 * (uint64_t)n},

@@ -42,6 +42,7 @@ SIGNATURES = [
     ("pbf_ctx_destroy", None, [_vp]),
     ("pbf_last_error", ctypes.c_char_p, []),
     ("pbf_ctx_set_stream", ctypes.c_int, [_vp, _vp]),
+    ("pbf_ctx_set_option", ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_char_p]),
     ("pbf_device_sync", ctypes.c_int, [_vp]),
     ("pbf_ctx_release_caches", ctypes.c_int, [_vp]),
     ("pbf_ntt_u64", ctypes.c_int, [_vp, _u64, _u64, _p64, _p64, _sz, ctypes.c_int]),
@@ -152,13 +153,15 @@ def _ptr(a: np.ndarray):
 class Context:
     """pbf_ctx: one device, one stream, cached twiddle tables and scratch."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, options: dict | None = None):
         lib = load_library()
         h = _vp()
         _check(lib.pbf_ctx_create(device, ctypes.byref(h)))
         self.h = h
         self.lib = lib
         self.device = device
+        for k, v in (options or {}).items():
+            self.set_option(k, v)
 
     def close(self) -> None:
         if self.h:
@@ -178,6 +181,11 @@ class Context:
 
     def set_stream(self, stream_ptr: int) -> None:
         _check(self.lib.pbf_ctx_set_stream(self.h, _vp(stream_ptr)))
+
+    def set_option(self, name: str, value) -> None:
+        """pbf_ctx_set_option (include/pbf.h): a context option such as "ntt.passes" = "12,12";
+        None removes it. Cached plans are rebuilt under the new value."""
+        _check(self.lib.pbf_ctx_set_option(self.h, name.encode(), None if value is None else str(value).encode()))
 
     def sync(self) -> None:
         _check(self.lib.pbf_device_sync(self.h))

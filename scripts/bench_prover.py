@@ -20,13 +20,13 @@ G2 = ((1085704699902305713594457076223282948137075635957851808699051999328565585
        4082367875863433681332203403145435568316851327593401208105741076214120093531))
 
 
-def breakdown(fn) -> dict:
-    """Per-round wall times of one proof: PBF_PROVER_TIMING=1 makes the prover synchronise its
+def breakdown(ctx, fn) -> dict:
+    """Per-round wall times of one proof: context option prover.timing = 1 makes the prover synchronise its
     stream at each round mark and print it on stderr (csrc/prover.hip Prover::mark); fd 2 is
     captured around the call. The marks serialise the proof, so their sum exceeds prove_ms."""
     import tempfile
 
-    os.environ["PBF_PROVER_TIMING"] = "1"
+    ctx.set_option("prover.timing", 1)
     sys.stderr.flush()
     saved = os.dup(2)
     with tempfile.TemporaryFile(mode="w+b") as tf:
@@ -37,7 +37,7 @@ def breakdown(fn) -> dict:
         finally:
             os.dup2(saved, 2)
             os.close(saved)
-            del os.environ["PBF_PROVER_TIMING"]
+            ctx.set_option("prover.timing", None)
         tf.seek(0)
         text = tf.read().decode(errors="replace")
     out = {}
@@ -88,7 +88,7 @@ def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True, no_k
     if no_key:
         # the same proof with the circuit's preprocessing (8 INTTs + 9 coset NTTs of the
         # selector / permutation / l1 polynomials) recomputed per proof, as the reference does
-        os.environ["PBF_PROVER_NO_PK"] = "1"
+        ctx.set_option("prover.pk", 0)
         tc = []
         try:
             for _ in range(max(3, reps // 2)):
@@ -98,18 +98,18 @@ def run(ctx, log_n: int, reps: int = 2, mode: int = 1, verify: bool = True, no_k
                 torch.cuda.synchronize()
                 tc.append(time.perf_counter() - t0)
         finally:
-            del os.environ["PBF_PROVER_NO_PK"]
+            ctx.set_option("prover.pk", None)
         tc.sort()
         t_cold = tc[len(tc) // 2]
         out.update({"prove_ms_no_key": t_cold * 1e3, "proofs_per_s_no_key": 1 / t_cold, "reps_no_key": len(tc),
                     "same_proof_with_and_without_key": bool(np.array_equal(np.asarray(pts_c), np.asarray(pts))
                                                             and np.array_equal(np.asarray(fs_c), np.asarray(fs)))})
     if rounds:
-        out["rounds_ms"] = breakdown(lambda: ctx.plonk_prove_bn254_dev(
+        out["rounds_ms"] = breakdown(ctx, lambda: ctx.plonk_prove_bn254_dev(
             n, dq.data_ptr(), dc.data_ptr(), dabc.data_ptr(), chal, rnd, dsrs.data_ptr(), srs_m, mode=mode,
             stream=sp))
         out["rounds_note"] = ("one proof with a stream synchronisation at every round mark "
-                              "(PBF_PROVER_TIMING): where the time goes, not the overlapped total")
+                              "(option prover.timing): where the time goes, not the overlapped total")
     if verify:
         import ctypes
 

@@ -22,6 +22,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -52,6 +54,7 @@ struct Clique;
 struct Comm {
   Clique* cq;
   int rank;
+  int sends = 0;  // ncclSend calls on this communicator (failure injection below)
 };
 
 struct Slot {  // what rank s posted for peer d
@@ -217,9 +220,19 @@ int ncclGroupEnd() {
   return issue(ops);
 }
 
+// Failure injection (tests only): FAKE_RCCL_FAIL_SEND="r,k" makes the k-th ncclSend call on
+// rank r's communicator fail (ncclSystemError, nothing posted) -- a rank failing inside its half
+// of a collective after every rank has passed the library's pre-post barrier.
 int ncclSend(const void* buf, size_t count, int dtype, int peer, void* comm, hipStream_t stream) {
   const size_t b = dtype_bytes(dtype);
-  if (!b) return ncclInvalidArgument;
+  if (!b || !comm) return ncclInvalidArgument;
+  Comm* c = (Comm*)comm;
+  if (const char* f = getenv("FAKE_RCCL_FAIL_SEND")) {  // counted from when the variable is set
+    int fr = -1, fk = -1;
+    if (sscanf(f, "%d,%d", &fr, &fk) == 2 && c->rank == fr && ++c->sends == fk) return ncclSystemError;
+  } else {
+    c->sends = 0;
+  }
   return post(Op{true, const_cast<void*>(buf), count * b, peer, (Comm*)comm, stream});
 }
 

@@ -79,3 +79,33 @@ def test_single_hip_runtime_in_process():
     maps = open("/proc/self/maps").read()
     paths = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert len(paths) == 1, paths
+
+
+def test_product_library_reads_no_tuning_environment():
+    """the product build never takes a schedule or a code path from the
+    environment -- tuning goes through pbf_ctx_set_option (include/pbf.h) and the A/B switches
+    of measured-negative variants are compiled in only with -DPBF_AB (make ab). The only
+    variable names left in libpbf.so are the RCCL library path and the single-device test hook
+    of the RCCL branch (csrc/group.hip)."""
+    import pbf
+
+    data = open(pbf.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"PBF_[A-Z0-9_]{3,}", data))
+    assert names <= {b"PBF_RCCL_LIB", b"PBF_GROUP_FORCE_RCCL"}, sorted(names)
+    src = os.path.join(ROOT, "plonk-by-fingers_amd", "csrc")
+    calls = []
+    for fn in os.listdir(src):
+        if fn.endswith((".hip", ".hpp")):
+            calls += [(fn, m) for m in re.findall(r"getenv\((\"?[A-Za-z_]+\"?)\)", open(os.path.join(src, fn)).read())]
+    # group.hip's two names and internal.hpp's ab_env (PBF_AB builds only)
+    assert sorted(calls) == [("group.hip", '"PBF_GROUP_FORCE_RCCL"'), ("group.hip", '"PBF_RCCL_LIB"'),
+                             ("internal.hpp", "name")], calls
+
+
+def test_set_option_is_declared_with_its_names():
+    src = open(HEADER).read()
+    assert "pbf_ctx_set_option" in src
+    capi = open(os.path.join(ROOT, "plonk-by-fingers_amd", "csrc", "capi.hip")).read()
+    known = re.search(r"known\[\] = \{(.*?)\};", capi, flags=re.S).group(1)
+    for name in re.findall(r"\"([a-z0-9_.]+)\"", known):
+        assert name in src, name  # every accepted option is documented in pbf.h

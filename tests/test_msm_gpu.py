@@ -129,9 +129,10 @@ def test_msm_bucket_chunking_and_signed_digits(ctx, kind):
     assert _dlog_msm(ctx, t, sc)
 
 
-def test_fixed_base_comb_matches_double_and_add(ctx, monkeypatch):
+def test_fixed_base_comb_matches_double_and_add(ctx):
     """The byte-window comb of pbf_g1_bn254_mul_base_dev (SRS::create) against the plain
-    double-and-add kernel, including zero bytes, 0xff bytes, 0 and r - 1."""
+    double-and-add kernel (context option g1.mul_base = daa), including zero bytes, 0xff bytes,
+    0 and r - 1."""
     import torch
 
     n = 4096
@@ -145,9 +146,12 @@ def test_fixed_base_comb_matches_double_and_add(ctx, monkeypatch):
     a = torch.empty(n * 8, dtype=torch.int64, device="cuda")
     b = torch.empty_like(a)
     ctx.g1_mul_base_dev(dt.data_ptr(), a.data_ptr(), n, stream=st)
-    monkeypatch.setenv("PBF_G1_DOUBLE_AND_ADD", "1")
-    ctx.g1_mul_base_dev(dt.data_ptr(), b.data_ptr(), n, stream=st)
-    torch.cuda.synchronize()
+    ctx.set_option("g1.mul_base", "daa")
+    try:
+        ctx.g1_mul_base_dev(dt.data_ptr(), b.data_ptr(), n, stream=st)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option("g1.mul_base", None)
     assert torch.equal(a, b)
     assert a[:8].tolist() == [0] * 8  # 0 * G = identity
     # parity anchor: the edge scalars and a sample re-derived by the oracle's double-and-add
@@ -207,12 +211,11 @@ def test_fixed_base_msm_edges_and_cache(ctx):
 
 
 @pytest.mark.parametrize("n_points,n", [(300, 255), (300, 256), (300, 300), (70001, 70001), (70001, 69000)])
-def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n):
+def test_fixed_base_digit_sort_matches_windowed(ctx, n_points, n):
     """The MSM sorts' first pass from 16-bit digit codes (msm_sort.hpp RsDigits; fixed-base and
-    windowed forms; the default) gives the same result as the (key, value) pair sort (=0),
-    including tiles that straddle two windows (n not a multiple of the 8192-entry tile).
-    n = 255 is just below the digit-code path's minimum (rs_dig_ok: n >= 256), so both settings
-    take the pair sort there; n = 256 is the smallest digit-code case."""
+    windowed forms) against the naive fold, including tiles that straddle two windows (n not a
+    multiple of the 8192-entry tile). n = 255 is just below the digit-code path's minimum
+    (rs_dig_ok: n >= 256: the pair sort there); n = 256 is the smallest digit-code case."""
     rnd = random.Random(n_points + n)
     base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(32)]
     pts = (base * (n_points // len(base) + 1))[:n_points]
@@ -220,31 +223,23 @@ def test_fixed_base_fused_digit_sort_matches_pairs(ctx, monkeypatch, n_points, n
     sc[::97] = [0] * len(sc[::97])  # zero scalars: every window's code is "no entry"
     dp, ds = _dev_points(pts), _dev_scalars(sc)
     ptr = ds.data_ptr()
-    res = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
-        res[fused] = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ptr, n)
-        res["w" + fused] = ctx.msm_g1_dev(dp.data_ptr(), ptr, n)  # the windowed form's 3-pass sort
-    assert res["1"] == res["0"] == res["w1"] == res["w0"]
+    got = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ptr, n)
+    assert got == ctx.msm_g1_dev(dp.data_ptr(), ptr, n)  # the windowed form's 3-pass sort
     if n <= 300:
-        assert res["1"] == enc(bn254.msm_naive(pts[:n], sc))
+        assert got == enc(bn254.msm_naive(pts[:n], sc))
 
 
 @pytest.mark.parametrize("n_points,first,n", [(1000, 300, 256), (1000, 1, 999), (70001, 8193, 40000), (600, 599, 1)])
-def test_fixed_base_range_first_nonzero(ctx, monkeypatch, n_points, first, n):
+def test_fixed_base_range_first_nonzero(ctx, n_points, first, n):
     """pbf_msm_g1_bn254_fixed_range_dev: scalars against points [first, first + n) of the fixed
     base set -- the value encoding w * n_table + first + i of the digit-code sort with first > 0
-    (a sharded commitment's point range) -- equals the pair sort's result and the naive sum."""
+    (a sharded commitment's point range) -- equals the windowed MSM and the naive sum."""
     rnd = random.Random(n_points * 7 + first)
     base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(37)]
     pts = (base * (n_points // len(base) + 1))[:n_points]
     sc = [rnd.randrange(R) for _ in range(n)]
     dp, ds = _dev_points(pts), _dev_scalars(sc)
-    res = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
-        res[fused] = ctx.msm_g1_fixed_range_dev(dp.data_ptr(), n_points, first, ds.data_ptr(), n)
-    assert res["1"] == res["0"]
+    res = {"1": ctx.msm_g1_fixed_range_dev(dp.data_ptr(), n_points, first, ds.data_ptr(), n)}
     # the same range as a plain MSM over the sliced points (windowed path, no table)
     dsl = _dev_points(pts[first:first + n])
     assert res["1"] == ctx.msm_g1_dev(dsl.data_ptr(), ds.data_ptr(), n)
@@ -274,14 +269,14 @@ def test_fixed_base_msm_2p20_discrete_log(ctx):
 
 
 @pytest.mark.parametrize("c", [16, 18, 20, 22])
-def test_fixed_base_window_widths(ctx, monkeypatch, c):
-    """The fixed-base table's window width (PBF_MSM_FX_C, round 4: ceil(255 / c) windows of
+def test_fixed_base_window_widths(ctx, c):
+    """The fixed-base table's window width (option msm.fx_c, round 4: ceil(255 / c) windows of
     2^(c-1) signed-digit buckets, 32-bit digit codes above c = 16, sorts of c key bits in passes
     of balanced digit widths, the generalised quad reduction tail) gives the windowed MSM's
     result: random scalars, digits at the c-bit recoding boundaries with carry chains, zero
-    scalars, tiles straddling windows, both sorts' first passes, and a point range."""
+    scalars, tiles straddling windows, and a point range."""
     rnd = random.Random(c)
-    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    ctx.set_option("msm.fx_c", c)
     h = 1 << (c - 1)
     edges = [h - 1, h, h + 1, (1 << c) - 1, 1, 0]
     base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(41)]
@@ -297,12 +292,9 @@ def test_fixed_base_window_widths(ctx, monkeypatch, c):
             sc = [rnd.randrange(R)] * n
         dp, ds = _dev_points(pts), _dev_scalars(sc)
         want = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n)
-        for fused in ("1", "0"):
-            monkeypatch.setenv("PBF_MSM_FUSED_SORT", fused)
-            assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n) == want, (c, kind, fused)
+        assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n) == want, (c, kind)
         if n == 300:
             assert want == enc(bn254.msm_naive(pts, sc))
-    monkeypatch.setenv("PBF_MSM_FUSED_SORT", "1")
     first, n = 8193, 40000
     pts = (base * (70001 // len(base) + 1))[:70001]
     sc = [rnd.randrange(R) for _ in range(n)]
@@ -310,14 +302,15 @@ def test_fixed_base_window_widths(ctx, monkeypatch, c):
     got = ctx.msm_g1_fixed_range_dev(dp.data_ptr(), len(pts), first, ds.data_ptr(), n)
     assert got == ctx.msm_g1_dev(_dev_points(pts[first:first + n]).data_ptr(), ds.data_ptr(), n)
     ctx.release_caches()
+    ctx.set_option("msm.fx_c", None)
 
 
 @pytest.mark.parametrize("c", [20, 22])
-def test_fixed_base_wide_windows_2p20_discrete_log(ctx, monkeypatch, c):
+def test_fixed_base_wide_windows_2p20_discrete_log(ctx, c):
     """Config 4's size with the wide-window table: P_i = t_i G, result (sum s_i t_i) G."""
     import torch
 
-    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    ctx.set_option("msm.fx_c", c)
     m = 1 << 20
     t = bn254.random_limbs(m, 45 + c)
     s = bn254.random_limbs(m, 46 + c)
@@ -330,32 +323,18 @@ def test_fixed_base_wide_windows_2p20_discrete_log(ctx, monkeypatch, c):
     k = sum(a * b for a, b in zip(tv, sv)) % R
     assert got == enc(bn254.g1_mul(bn254.G1_GEN, k))
     ctx.release_caches()
-
-
-def test_sort_digit_widths_knob(ctx, monkeypatch):
-    """The windowed MSM's 20-bit sort in balanced 7/7/6-bit passes (default) and in 8/8/4
-    (PBF_MSM_SORT_W8=1) give the same result."""
-    rnd = random.Random(77)
-    n = 70001
-    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(29)]
-    pts = (base * (n // len(base) + 1))[:n]
-    sc = [rnd.randrange(R) for _ in range(n)]
-    dp, ds = _dev_points(pts), _dev_scalars(sc)
-    a = ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n)
-    monkeypatch.setenv("PBF_MSM_SORT_W8", "1")
-    assert ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n) == a
-    assert ctx.msm_g1_fixed_dev(dp.data_ptr(), n, ds.data_ptr(), n) == a
+    ctx.set_option("msm.fx_c", None)
 
 
 @pytest.mark.parametrize("c", [16, 22])
-def test_fixed_base_heavy_buckets(ctx, monkeypatch, c):
+def test_fixed_base_heavy_buckets(ctx, c):
     """Skewed digit distributions through the fixed-base joins: 2^18 equal scalars (every
     window's n entries in ONE bucket: spans of ~6100 chunks, past the per-chunk steps' 4096, so
     msm_join_rest_g finishes them) and 2^18 small scalars (< 2^40: two or three nonzero windows,
     a few thousand heavy buckets). Compared with the windowed MSM; P_i = t_i G random."""
     import torch
 
-    monkeypatch.setenv("PBF_MSM_FX_C", str(c))
+    ctx.set_option("msm.fx_c", c)
     m = 1 << 18
     t = bn254.random_limbs(m, 700 + c)
     dt = torch.from_numpy(t.view(np.int64)).cuda()
@@ -370,32 +349,6 @@ def test_fixed_base_heavy_buckets(ctx, monkeypatch, c):
         want = ctx.msm_g1_dev(pts.data_ptr(), ds.data_ptr(), m)
         assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want, c
     ctx.release_caches()
+    ctx.set_option("msm.fx_c", None)
 
 
-@pytest.mark.parametrize("knob", ["PBF_MSM_CD_RESOLVE=0", "PBF_MSM_HEAVY_JOIN=0", "PBF_MSM_DEFER_CONV=0",
-                                  "PBF_MSM_CD_SEQ32=1", "PBF_MSM_CHUNK_JOIN=0"])
-def test_wide_tail_forms_agree(ctx, monkeypatch, knob):
-    """The round-5 wide-window tail (buckets resolved once, heavy buckets joined by lane groups,
-    partials converted as read) against its A/B forms: c = 22, random scalars (light buckets,
-    the narrow top window's heavy ones) and small scalars (a few thousand heavy buckets), each
-    form equal to the windowed MSM."""
-    import torch
-
-    monkeypatch.setenv("PBF_MSM_FX_C", "22")
-    m = 1 << 17
-    t = bn254.random_limbs(m, 900)
-    dt = torch.from_numpy(t.view(np.int64)).cuda()
-    pts = torch.empty(m * 8, dtype=torch.int64, device="cuda")
-    ctx.g1_mul_base_dev(dt.data_ptr(), pts.data_ptr(), m)
-    rng = np.random.default_rng(901)
-    small = np.zeros((m, 4), dtype=np.uint64)
-    small[:, 0] = rng.integers(0, 1 << 40, size=m, dtype=np.uint64)
-    for sc in (bn254.random_limbs(m, 902), small):
-        ds = torch.from_numpy(np.ascontiguousarray(sc).reshape(-1).view(np.int64)).cuda()
-        want = ctx.msm_g1_dev(pts.data_ptr(), ds.data_ptr(), m)
-        assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want
-        name, val = knob.split("=")
-        monkeypatch.setenv(name, val)
-        assert ctx.msm_g1_fixed_dev(pts.data_ptr(), m, ds.data_ptr(), m) == want, knob
-        monkeypatch.delenv(name)
-    ctx.release_caches()

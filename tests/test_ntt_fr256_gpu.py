@@ -29,19 +29,19 @@ def test_small_vs_recursion_faithful(ctx, logn):
     assert ctx.ntt_fr(w, got, inverse=True) == a
 
 
-@pytest.mark.parametrize("conv", [False, True])
+@pytest.mark.parametrize("maxr", [None, "5"])
 @pytest.mark.parametrize("logn", [12, 13, 14, 15, 16, 17])
-def test_multi_pass_vs_oracle(ctx, monkeypatch, logn, conv):
-    """Multi-pass Fr NTT both ways vs the oracle; conv: with the (optional) Montgomery
-    conversions of the first and last pass (PBF_NTT256_CONV), which the default skips."""
-    if conv:
-        monkeypatch.setenv("PBF_NTT256_CONV", "1")
+def test_multi_pass_vs_oracle(logn, maxr):
+    """Multi-pass Fr NTT both ways vs the oracle; maxr: with passes of at most 2^5 points (context
+    option ntt256.maxr: more, lighter passes, the planner's other radix families)."""
+    ctx = pbf.Context(0, options={"ntt256.maxr": maxr} if maxr else None)
     n = 1 << logn
     w = bn254.root_of_unity(n)
     a = bn254.limbs_to_ints(bn254.random_limbs(n, 20 + logn))
     got = ctx.ntt_fr(w, a)
     assert got == bn254.ntt(a, w)
     assert ctx.ntt_fr(w, got, inverse=True) == a
+    ctx.close()
 
 
 def test_kat_structure_small_field_values(ctx):
@@ -107,13 +107,11 @@ def test_mul_ntt_config3_size_evaluation_identity(ctx):
 
 
 @pytest.mark.parametrize("logn", [21, 22])
-def test_twiddle_table_forms_agree(monkeypatch, logn):
-    """The last pass's twiddles three ways: a per-pass table filled on the device (default, past
-    2^20 entries), the two-level tables (PBF_NTT256_TWLOG=20), and with the inverse's n^-1 as a
-    separate product (PBF_NTT256_SCALE_PASS=1) instead of folded into those twiddles: identical
-    forward and inverse outputs, and the round trip restores the input. mul_ntt likewise: its
-    product fused into the second operand's last pass (default), the one-product pointwise kernel
-    (PBF_MUL_NTT_NO_FUSE) and the two-product form (PBF_MUL_NTT_TWO_PRODUCTS)."""
+def test_twiddle_table_forms_agree(logn):
+    """The last pass's twiddles two ways: a per-pass table filled on the device (default, past
+    2^20 entries) and the two-level tables (context option ntt256.twlog = 20, the path of passes
+    past 2^26 entries): identical forward and inverse outputs and mul_ntt products, and the round
+    trip restores the input."""
     import torch
 
     n = 1 << logn
@@ -123,13 +121,8 @@ def test_twiddle_table_forms_agree(monkeypatch, logn):
     half = torch.zeros_like(x)
     half[: n * 2] = x[: n * 2]  # n/2 coefficients, zero-padded: a mul_ntt operand
     outs = []
-    for env in ({}, {"PBF_NTT256_TWLOG": "20"}, {"PBF_NTT256_SCALE_PASS": "1"},
-                {"PBF_MUL_NTT_TWO_PRODUCTS": "1"}, {"PBF_MUL_NTT_NO_FUSE": "1"}):
-        for k in ("PBF_NTT256_TWLOG", "PBF_NTT256_SCALE_PASS", "PBF_MUL_NTT_TWO_PRODUCTS", "PBF_MUL_NTT_NO_FUSE"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        c = pbf.Context(0)  # plans are cached per context: a fresh one per setting
+    for opts in ({}, {"ntt256.twlog": "20"}):
+        c = pbf.Context(0, options=opts)
         try:
             f = torch.empty_like(x)
             c.ntt_fr_batch_dev(w, x.data_ptr(), f.data_ptr(), n, 1)

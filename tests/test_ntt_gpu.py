@@ -127,10 +127,10 @@ def test_linearity_2p24(ctx):
 
 
 @pytest.mark.parametrize("passes", ["12,12", "8,8,8", "6,6,6,6"])
-def test_alternative_pass_plans_2p24(passes, monkeypatch, vectors):
-    # every radix family the planner can pick gives the same (golden) answer
-    monkeypatch.setenv("PBF_NTT_PASSES", passes)
-    c2 = pbf.Context(0)  # fresh plan cache picks up the env override
+def test_alternative_pass_plans_2p24(passes, vectors):
+    # every radix family the planner can pick gives the same (golden) answer (context option
+    # ntt.passes, include/pbf.h)
+    c2 = pbf.Context(0, options={"ntt.passes": passes})
     c = vectors["large"][2]
     a = oracle.splitmix_field(c["modulus"], c["seed"], c["n"])
     assert sha(c2.ntt(c["modulus"], c["omega"], a)) == c["sha256_fwd"]
@@ -138,13 +138,11 @@ def test_alternative_pass_plans_2p24(passes, monkeypatch, vectors):
 
 
 @pytest.mark.parametrize("inverse", [False, True])
-@pytest.mark.parametrize("other", [{"PBF_NTT_NO_RG": "1"}, {"PBF_NTT_T3GEO": "0"}])
-def test_regrouped_2p24_matches_stockham(monkeypatch, inverse, other):
+def test_regrouped_2p24_matches_stockham(inverse):
     """The regrouped 2^24 plan (ntt_gl.hpp ntt_gl_rg2_kernel: general twiddles only between
     64-point blocks, the default for 8,8,8; its last pass forming w^(a0 X) as C[r2][X] D[X]^s2)
-    against the round-2 passes (PBF_NTT_NO_RG=1) and against its last pass reading the full
-    2^24-entry table (PBF_NTT_T3GEO=0), batch of 2 (XCD k-major tiles), forward and inverse,
-    bit-exact, and polynomial 0 against the oracle's iterative transform."""
+    against the round-2 passes (option ntt.no_rg=1), batch of 2 (XCD-blocked tiles), forward
+    and inverse, bit-exact, and polynomial 0 against the oracle's iterative transform."""
     import torch
 
     n, batch = 1 << 24, 2
@@ -152,55 +150,16 @@ def test_regrouped_2p24_matches_stockham(monkeypatch, inverse, other):
     host = np.stack([oracle.splitmix_field(GOLD, 900 + i, n) for i in range(batch)])
     stream = torch.cuda.current_stream().cuda_stream
     outs = []
-    for env in ({}, other):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        c = pbf.Context(0)
+    for opts in ({}, {"ntt.no_rg": "1"}):
+        c = pbf.Context(0, options=opts)
         d_in = torch.from_numpy(host.view(np.int64)).cuda()
         d_out = torch.empty_like(d_in)
         c.ntt_batch_dev(GOLD, w, d_in.data_ptr(), d_out.data_ptr(), n, batch, inverse=inverse, stream=stream)
         torch.cuda.synchronize()
         outs.append(d_out.cpu().numpy().view(np.uint64).copy())
         c.close()
-        for k in env:
-            monkeypatch.delenv(k)
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0][0], oracle.ntt_gl_par(w, host[0], inverse=inverse))
-
-
-@pytest.mark.parametrize("inverse", [False, True])
-@pytest.mark.parametrize("batch", [1, 2])
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_two_pass_r4k_2p24_matches_default(monkeypatch, vectors, inverse, batch, mode):
-    """The two-pass 4096 x 4096 plan (ntt_r4k.hpp, PBF_NTT_R4K=1: 64 x 64 register DFTs in
-    512-thread workgroups, LDS exchange in two rounds; =2: its persistent form with the next
-    tile's even rows LDS-DMA'd during stage II) against the default three-pass plan, forward and
-    inverse, batch 1 (linear tile order) and 2 (XCD k-major), bit-exact; forward against the
-    2^24 golden digest."""
-    import torch
-
-    n = 1 << 24
-    w = root(GOLD, n)
-    host = np.stack([oracle.splitmix_field(GOLD, 950 + i, n) for i in range(batch)])
-    stream = torch.cuda.current_stream().cuda_stream
-    outs = []
-    for env in ({}, {"PBF_NTT_R4K": mode}):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        c = pbf.Context(0)
-        d_in = torch.from_numpy(host.view(np.int64)).cuda()
-        d_out = torch.empty_like(d_in)
-        c.ntt_batch_dev(GOLD, w, d_in.data_ptr(), d_out.data_ptr(), n, batch, inverse=inverse, stream=stream)
-        torch.cuda.synchronize()
-        outs.append(d_out.cpu().numpy().view(np.uint64).copy())
-        if env and not inverse and batch == 1:
-            cg = vectors["large"][2]
-            a = oracle.splitmix_field(cg["modulus"], cg["seed"], cg["n"])
-            assert sha(c.ntt(cg["modulus"], cg["omega"], a)) == cg["sha256_fwd"]
-        c.close()
-        for k in env:
-            monkeypatch.delenv(k)
-    assert np.array_equal(outs[0], outs[1])
 
 
 def test_batch_dev_matches_single(ctx):
@@ -223,21 +182,17 @@ def test_batch_dev_matches_single(ctx):
     assert np.array_equal(d_in.cpu().numpy().view(np.uint64), got)
 
 
-@pytest.mark.parametrize("env", [{"PBF_NTT_BLK": "1"}, {"PBF_NTT_PERSIST": "1"}, {"PBF_NTT_GROUP": "2"},
-                                 {"PBF_NTT_GROUP": "1", "PBF_NTT_STREAMS": "3"}, {"PBF_NTT_STREAMS": "1"},
-                                 {"PBF_NTT_GROUP": "0"}, {"PBF_NTT_ORDER": "0"}, {"PBF_NTT_ORDER": "2"},
-                                 {"PBF_NTT_NO_KMAJOR": "1"}, {"PBF_NTT_PAD": "16"}, {"PBF_NTT_PAD": "8", "PBF_NTT_STREAMS": "1"},
-                                 {"PBF_NTT_NO_PRETW": "1"}, {"PBF_NTT_EVENTS": "1"}])
+@pytest.mark.parametrize("opts", [{}, {"ntt.group": "2"}, {"ntt.group": "1", "ntt.streams": "3"},
+                                  {"ntt.streams": "1"}, {"ntt.group": "0"}, {"ntt.group": "3", "ntt.streams": "4"}])
 @pytest.mark.parametrize("logn", [16, 20])
-def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
-    """Every opt-in schedule of the Goldilocks pass kernel (blocked intermediate, persistent
-    pipelined kernel, polynomial groups, tile orders; ntt_launch.hip) gives the oracle's
-    answer, forward and inverse, on a batch."""
+def test_schedule_options_same_result(opts, logn):
+    """Every group / stream schedule of the batched Goldilocks NTT (ntt_launch.hip
+    run_gl_passes: context options ntt.group, ntt.streams) gives the oracle's answer, forward
+    and inverse, on a batch (9: the default 4-polynomial groups on 2 streams, a last group of 1)."""
     import torch
 
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    n, batch = 1 << logn, (9 if logn == 16 else 3)  # 9: the default 4-polynomial groups, 2 streams
+    ctx = pbf.Context(0, options=opts)
+    n, batch = 1 << logn, (9 if logn == 16 else 3)
     w = root(GOLD, n)
     host = np.stack([oracle.splitmix_field(GOLD, 700 + i, n) for i in range(batch)])
     d_in = torch.from_numpy(host.view(np.int64)).cuda()
@@ -251,49 +206,18 @@ def test_schedule_knobs_same_result(ctx, monkeypatch, env, logn):
     ctx.ntt_batch_dev(GOLD, w, d_out.data_ptr(), d_out.data_ptr(), n, batch, inverse=True, stream=stream)
     torch.cuda.synchronize()
     assert np.array_equal(d_out.cpu().numpy().view(np.uint64), host)
+    ctx.close()
 
 
-@pytest.mark.parametrize("logn,batch", [(16, 12), (16, 9), (16, 5), (20, 8), (14, 32)])
-def test_dual_group_schedule(ctx, monkeypatch, logn, batch):
-    """The dual-group schedule of batched two-pass transforms (PBF_NTT_DUAL=1, ntt_launch.hip
-    run_gl_dual: one stream, pass 2 of group g-1 and pass 1 of group g in one launch, a smaller
-    last group launched on its own) against the default two-stream schedule and the oracle,
-    forward and inverse, in place."""
-    import torch
-
-    n = 1 << logn
-    w = root(GOLD, n)
-    host = np.stack([oracle.splitmix_field(GOLD, 4100 + i, n) for i in range(batch)])
-    stream = torch.cuda.current_stream().cuda_stream
-    outs = []
-    for env in ({"PBF_NTT_DUAL": "1"}, {}):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        d = torch.from_numpy(host.view(np.int64)).cuda()
-        ctx.ntt_batch_dev(GOLD, w, d.data_ptr(), d.data_ptr(), n, batch, stream=stream)
-        torch.cuda.synchronize()
-        outs.append(d.cpu().numpy().view(np.uint64).copy())
-        ctx.ntt_batch_dev(GOLD, w, d.data_ptr(), d.data_ptr(), n, batch, inverse=True, stream=stream)
-        torch.cuda.synchronize()
-        assert np.array_equal(d.cpu().numpy().view(np.uint64), host)
-        for k in env:
-            monkeypatch.delenv(k)
-    assert np.array_equal(outs[0], outs[1])
-    for i in (0, batch - 1):
-        assert np.array_equal(outs[0][i], oracle.ntt_iter(GOLD, w, host[i]))
-
-
-@pytest.mark.parametrize("env", [{"PBF_NTT_TWMAX_LOG": "18"}, {"PBF_NTT_TWSPLIT": "1"},
-                                 {"PBF_NTT_TWMAX_LOG": "18", "PBF_NTT_NO_TWSPLIT": "1"}, {"PBF_NTT_PAD": "16"}])
-def test_twiddle_table_paths(monkeypatch, vectors, env):
+@pytest.mark.parametrize("opts", [{"ntt.twmax_log": "18"}, {"ntt.twsplit": "1"},
+                                  {"ntt.twmax_log": "18", "ntt.twsplit": "0"}])
+def test_twiddle_table_paths(vectors, opts):
     """The three sources of the pass twiddle w^(r k): the per-pass [r][k] table (default up to
-    2^PBF_NTT_TWMAX_LOG = 2^24 entries), the last pass's split table B[kb][r] * A[r][w]
-    (default beyond; forced by PBF_NTT_TWSPLIT) and the two-level table (PBF_NTT_NO_TWSPLIT).
-    A fresh context (plans read the knobs when they are built) must reproduce the 2^16, 2^20
-    and 2^24 golden digests and round-trip."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    c2 = pbf.Context(0)
+    2^ntt.twmax_log = 2^24 entries), the last pass's split table B[kb][r] * A[r][w]
+    (default beyond; forced by ntt.twsplit=1) and the two-level table (ntt.twsplit=0): the
+    paths of transforms above 2^24 points, exercised at test sizes. Must reproduce the 2^16,
+    2^20 and 2^24 golden digests and round-trip."""
+    c2 = pbf.Context(0, options=opts)
     try:
         for c in vectors["large"]:
             a = oracle.splitmix_field(c["modulus"], c["seed"], c["n"])
@@ -382,3 +306,28 @@ def test_error_codes(ctx):
     # F_5 with n = 4: ok; the ENOINV branch needs n = 0 mod M, i.e. M = 2 (even, unsupported) — so
     # only check that a valid small-field inverse works (reference test field F17, omega 4).
     assert ctx.ntt(17, 4, [1, 2, 3, 4], inverse=True).tolist() == oracle.ntt_ct(17, 4, [1, 2, 3, 4], True).tolist()
+
+
+def test_context_options_errors_and_environment(monkeypatch, vectors):
+    """pbf_ctx_set_option rejects unknown names (PBF_EINVAL) and null removes an option; the
+    retired environment knobs of earlier rounds change nothing: with them set, a fresh context
+    still reproduces the golden digests (they are not read at all, test_capi_exports.py)."""
+    c = pbf.Context(0)
+    try:
+        with pytest.raises(pbf.PbfError) as e:
+            c.set_option("ntt.no_such_option", "1")
+        assert e.value.code == pbf.PBF_EINVAL
+        c.set_option("ntt.passes", "12,12")
+        c.set_option("ntt.passes", None)
+    finally:
+        c.close()
+    for k, v in {"PBF_NTT_PASSES": "6,6,6,6", "PBF_NTT_GROUP": "1", "PBF_NTT_TILE": "16384", "PBF_NTT_R4K": "1",
+                 "PBF_NTT_PAD": "16", "PBF_NTT_EVENTS": "1", "PBF_NTT_IP": "1"}.items():
+        monkeypatch.setenv(k, v)
+    c = pbf.Context(0)
+    try:
+        for cv in vectors["large"]:
+            a = oracle.splitmix_field(cv["modulus"], cv["seed"], cv["n"])
+            assert sha(c.ntt(cv["modulus"], cv["omega"], a)) == cv["sha256_fwd"], cv["n"]
+    finally:
+        c.close()

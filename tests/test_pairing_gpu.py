@@ -52,10 +52,22 @@ def test_bilinearity_on_device(ctx):
     assert e1 == B.f12_flat(B.f12_pow(B.f12_from_flat(e2), a * b))
 
 
-def test_lane_engine_matches_oracle(ctx, monkeypatch):
-    """The lane-per-pairing engine (pairing_lane_kernel, PBF_PAIR_LANE=1 forces it below its
-    batch threshold) against the oracle: generators, random points, identities, bilinearity."""
-    monkeypatch.setenv("PBF_PAIR_LANE", "1")
+@pytest.fixture
+def lane_ctx():
+    """A context with the lane engine forced (option pair.engine = lane, below its batch
+    threshold)."""
+    import pbf
+
+    c = pbf.Context(0, options={"pair.engine": "lane"})
+    yield c
+    c.close()
+
+
+def test_lane_engine_matches_oracle(lane_ctx):
+    """The lane-per-pairing engine (pairing_lane_kernel, option pair.engine = lane forces it
+    below its batch threshold) against the oracle: generators, random points, identities,
+    bilinearity."""
+    ctx = lane_ctx
     rng = random.Random(41)
     ps = [B.G1_GEN, None, B.G1_GEN] + [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(2)]
     qs = [B.G2_GEN, B.G2_GEN, None] + [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(2)]
@@ -69,7 +81,7 @@ def test_lane_engine_matches_oracle(ctx, monkeypatch):
     assert e1 == B.f12_flat(B.f12_pow(B.f12_from_flat(e2), a * b))
 
 
-def test_lane_engine_matches_workgroup_engine(ctx, monkeypatch):
+def test_lane_engine_matches_workgroup_engine(ctx):
     """A batch of 131 pairs (two full waves and a ragged one; identities mixed in) through both
     engines, bit for bit (the default for this size is the lane engine)."""
     rng = random.Random(43)
@@ -80,27 +92,30 @@ def test_lane_engine_matches_workgroup_engine(ctx, monkeypatch):
     qs = ctx.g2_bn254_mul([B.G2_GEN] * n, ls)
     ps[5] = None
     qs[77] = None
-    monkeypatch.setenv("PBF_PAIR_LANE", "0")
-    wg = ctx.pairing_bn254(ps, qs)
-    monkeypatch.setenv("PBF_PAIR_LANE", "1")
-    lane = ctx.pairing_bn254(ps, qs)
+    try:
+        ctx.set_option("pair.engine", "wg")
+        wg = ctx.pairing_bn254(ps, qs)
+        ctx.set_option("pair.engine", "lane")
+        lane = ctx.pairing_bn254(ps, qs)
+    finally:
+        ctx.set_option("pair.engine", None)
     assert lane == wg
 
 
-def test_lane_engine_two_wave_build_matches(ctx, monkeypatch):
+def test_lane_engine_two_wave_build_matches(lane_ctx):
     """The lane kernel built for two waves per SIMD (taken from 2 x 4 x CUs waves, i.e. batches of
     >= 131072 on MI355X) against the unconstrained build, bit for bit, on a ragged batch with
-    identities (PBF_PAIR_LANE_WPE forces either build)."""
+    identities (option pair.lane_wpe forces either build)."""
+    ctx = lane_ctx
     rng = random.Random(47)
     n = 150
     ps = [B.g1_mul(B.G1_GEN, rng.randrange(1, B.R)) for _ in range(n)]
     qs = ctx.g2_bn254_mul([B.G2_GEN] * n, [rng.randrange(1, B.R) for _ in range(n)])
     ps[3] = None
     qs[100] = None
-    monkeypatch.setenv("PBF_PAIR_LANE", "1")
-    monkeypatch.setenv("PBF_PAIR_LANE_WPE", "1")
+    ctx.set_option("pair.lane_wpe", 1)
     one = ctx.pairing_bn254(ps, qs)
-    monkeypatch.setenv("PBF_PAIR_LANE_WPE", "2")
+    ctx.set_option("pair.lane_wpe", 2)
     two = ctx.pairing_bn254(ps, qs)
     assert one == two
     assert one[7] == B.f12_flat(B.pairing(ps[7], qs[7]))

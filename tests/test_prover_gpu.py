@@ -114,11 +114,11 @@ def test_challenge_on_the_evaluation_coset(ctx):
         assert [list(p) if p else None for p in pts] == [list(p) if p else None for p in want_pts]
 
 
-def test_proving_key_cache_matches_cold_proofs(monkeypatch):
+def test_proving_key_cache_matches_cold_proofs():
     """The context keeps the preprocessed polynomials (q_*, s_sigma_*, l1: coefficients and
     coset evaluations) per circuit, checked by fingerprints of the gates and copies on every
     call. Proofs over interleaved circuits and sizes (A A B A C A) on one context equal the
-    proofs of the same inputs with every preprocessing step recomputed (PBF_PROVER_NO_PK)."""
+    proofs of the same inputs with every preprocessing step recomputed (option prover.pk = 0)."""
     import pbf
 
     rng = random.Random(4242)
@@ -135,8 +135,7 @@ def test_proving_key_cache_matches_cold_proofs(monkeypatch):
             got.append(warm.plonk_prove_bn254(*P.mul_gates_circuit(n, seed), chal, rnd, srs, mode=1))
     finally:
         warm.close()
-    monkeypatch.setenv("PBF_PROVER_NO_PK", "1")
-    cold = pbf.Context(0)
+    cold = pbf.Context(0, options={"prover.pk": 0})
     try:
         srs = cold.srs_create(77, 2 * 128 + 2)
         ref = {name: cold.plonk_prove_bn254(*P.mul_gates_circuit(*circ[name]), chal, rnd, srs, mode=1) for name in circ}
@@ -146,11 +145,11 @@ def test_proving_key_cache_matches_cold_proofs(monkeypatch):
     assert ref["A"] != ref["B"]
 
 
-def test_verification_key_cache(ctx, monkeypatch):
+def test_verification_key_cache(ctx):
     """The verifier keeps the 8 preprocessed commitments per (circuit, SRS), fingerprint-
     checked on every call: accept / reject over interleaved inputs (the proof against a
     circuit with one selector changed, with two copy labels swapped, against another SRS)
-    equals the answers with the commitments recomputed per call (PBF_VERIFIER_NO_VK)."""
+    equals the answers with the commitments recomputed per call (option verifier.vk = 0)."""
     rng = random.Random(777)
     n = 64
     chal = [rng.randrange(P.R) for _ in range(5)]
@@ -173,8 +172,11 @@ def test_verification_key_cache(ctx, monkeypatch):
                 for qq, cc, srs, s, pr in runs]
 
     warm = answers()
-    monkeypatch.setenv("PBF_VERIFIER_NO_VK", "1")
-    cold = answers()
+    ctx.set_option("verifier.vk", 0)
+    try:
+        cold = answers()
+    finally:
+        ctx.set_option("verifier.vk", None)
     assert warm == cold, (warm, cold)
     assert warm == [True, False, False, True, True, False, True], warm
 
@@ -223,20 +225,3 @@ def test_shared_snapshots_across_caches(ctx):
     assert ctx.plonk_prove_bn254(*Bc, chal, rnd, srs2, mode=1) == pb2
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-def test_msm_prep_stream_same_proof(ctx, monkeypatch, mode):
-    """The opt-in MSM prep stream (PBF_MSM_PREP=1: each round's commitments sort on a second
-    stream while the previous one accumulates, csrc/msm.hip msm_scalars_ready) gives the same
-    proof as the one-stream schedule, over two proofs (the prep buffers and their events are
-    reused by the second)."""
-    n = 1 << 12
-    rng = random.Random(4242 + mode)
-    q, cp, abc = P.mul_gates_circuit(n, 0x5EED0042)
-    chal = [rng.randrange(P.R) for _ in range(5)]
-    rnd = [rng.randrange(P.R) for _ in range(9)]
-    srs = ctx.srs_create(rng.randrange(1, P.R), 2 * n + 2)
-    monkeypatch.setenv("PBF_MSM_PREP", "0")
-    ref = ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=mode)
-    monkeypatch.setenv("PBF_MSM_PREP", "1")
-    for _ in range(2):
-        assert ctx.plonk_prove_bn254(q, cp, abc, chal, rnd, srs, mode=mode) == ref

@@ -184,3 +184,26 @@ def test_release_caches_frees_exchange_buffers(ranks):
     assert np.array_equal(pbf.ntt_multi(ranks[:2], GOLD, w, a), ref)
     ranks[1].release_caches()
     assert np.array_equal(pbf.ntt_multi(ranks[:2], GOLD, w, a), ref)
+
+
+def test_rank_failure_inside_a_later_collective_aborts_safely(ranks, monkeypatch):
+    """a rank that fails inside its half of a LATER collective (after every rank
+    passed the pre-post barrier; injected in the stand-in: rank 1's 5th ncclSend, i.e. the first
+    send of its second all-to-all at G = 4) while the other ranks are inside their own RCCL calls.
+    abort_all takes each rank's post lock before aborting its communicator, so no communicator
+    is aborted under a thread still using it; the call returns an error naming a rank, and the
+    next call on the same contexts builds a new group and is bit-exact."""
+    import oracle
+    import pbf
+
+    G = 4
+    n = 1 << 12
+    w = pow(7, (GOLD - 1) // n, GOLD)
+    x = oracle.splitmix_field(GOLD, 9400, n // 2)
+    y = oracle.splitmix_field(GOLD, 9401, n // 2)
+    ref = ranks[0].mul_ntt(GOLD, w, x, y)
+    monkeypatch.setenv("FAKE_RCCL_FAIL_SEND", f"1,{G + 1}")
+    with pytest.raises(pbf.PbfError, match="rank"):
+        pbf.mul_ntt_multi(ranks[:G], GOLD, w, x, y)
+    monkeypatch.delenv("FAKE_RCCL_FAIL_SEND")
+    assert np.array_equal(pbf.mul_ntt_multi(ranks[:G], GOLD, w, x, y), ref)
