@@ -18,7 +18,8 @@ log_n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 300
 idle = float(sys.argv[4]) if len(sys.argv) > 4 else 2.0
-ctx = pbf.Context(0)
+opts = dict(kv.split("=") for kv in os.environ.get("RAMP_OPTS", "").split(",") if kv)
+ctx = pbf.Context(0, options=opts)
 sp = torch.cuda.current_stream().cuda_stream
 step, _ = bench._single_gpu(ctx, 1 << log_n, B, sp)
 torch.cuda.synchronize()
@@ -33,7 +34,7 @@ torch.cuda.synchronize()
 ts = [ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]
 def mean(a):
     return sum(a) / len(a)
-print(json.dumps({"log_n": log_n, "batch": B, "env_events": os.environ.get("PBF_NTT_EVENTS"),
+print(json.dumps({"log_n": log_n, "batch": B, "opts": opts,
                   "first5": [round(x, 4) for x in ts[:5]], "mean_5_25": round(mean(ts[5:25]), 4),
                   "mean_25_50": round(mean(ts[25:50]), 4), "mean_50_100": round(mean(ts[50:100]), 4),
                   "mean_200_300": round(mean(ts[200:300]), 4) if steps >= 300 else None,
