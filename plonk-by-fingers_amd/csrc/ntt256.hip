@@ -373,7 +373,7 @@ static int make_plan256(const pbf::Options& o, const uint64_t* omega, uint64_t n
   // per-pass tables up to 2^tw_log entries (32 B each); larger passes fall back to the two-level
   // tables (one extra Fr product per element). Tables past 2^20 entries are filled on the device.
   int tw_log = 26;  // option ntt256.twlog: the two-level path of larger passes at test sizes
-  if (const char* e = o.get("ntt256.twlog")) tw_log = atoi(e);
+  if (const char* e = o.get("ntt256.twlog")) tw_log = atoi(e) < 0 ? 0 : (atoi(e) > 30 ? 30 : atoi(e));
   uint64_t ns = 1;
   uint32_t log_ns = 0;
   for (size_t pi = 0; pi < p->logr.size(); ++pi) {

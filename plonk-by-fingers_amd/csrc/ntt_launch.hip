@@ -133,7 +133,8 @@ int make_plan(uint64_t m, uint64_t omega, uint64_t n, int inverse, NttPlan* p) {
   // use the two-level table
   {
     uint64_t ns = 1;
-    const int twmax = (int)p->opts.num("ntt.twmax_log", 24);
+    long long tm = p->opts.num("ntt.twmax_log", 24);
+    const int twmax = (int)(tm < 0 ? 0 : (tm > 30 ? 30 : tm));
     for (size_t i = 0; i < p->logr.size(); ++i) {
       const uint64_t R = 1ull << p->logr[i];
       auto b = std::make_shared<DevBuf>();
