@@ -13,7 +13,8 @@
 // the flushed bucket sums change domain (products by 2^266, 2^271, 2^256, 2^251 mod p).
 // Values stay lazily reduced: products of normalised inputs below 17.3p are below 3.3p (R is
 // 128x p), differences are taken as a + M - b with M = 8p or 16p in redundant limbs (every
-// limb but the top >= 2^31 - 4: no borrows), and the accumulator is bounded by 11.3p, all
+// limb but the top >= 2^31 - 4: no borrows), and the accumulator is bounded by 11.3p (X; Y below
+// 3.8p since round 6's mulsub), all
 // derived in DESIGN.md §3.5. Results are exact group elements: bit-identical after the
 // canonical conversion at the flush.
 #pragma once
@@ -83,6 +84,41 @@ __device__ __forceinline__ L29 mul(const L29& a, const L29& b) {
     acc >>= 29;
   }
   r.l[8] = (uint32_t)acc;
+  return r;
+}
+// (a b - c d) 2^-261 + p (mod p) by ONE product scan (round 6): the c d terms enter the same
+// columns through -c (v_mad_i64_i32), the accumulator is signed with arithmetic carries, and
+// p 2^261 is added at columns 9..17 so that the total is positive; one Montgomery reduction
+// instead of two products' and the lazy difference's (~150 fewer VALU per mixed addition).
+// Column bound: the a b and m p terms are below 18 x 2^58, the c d terms above -9 x 2^58, so
+// every column fits a signed 64-bit word. For madd-2008-s's Y3 (a b = R (Q - X3) below
+// (17.3 p)^2, c d = Y PPP below 11.3 p x 3.3 p < p 2^261) the output is normalised and in
+// (0.78 p, 3.8 p) (tests/test_l29_constants.py::test_mulsub_matches_montgomery restates it).
+__device__ __forceinline__ L29 mulsub(const L29& a, const L29& b, const L29& c, const L29& d) {
+  uint32_t m[9], nc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) nc[i] = 0u - c.l[i];
+  L29 r;
+  uint64_t acc = 0;  // a signed value in two's complement
+#pragma unroll
+  for (int k = 0; k < 17; ++k) {
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; ++i) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = lo; i <= hi; ++i) acc += (uint64_t)((int64_t)(int32_t)nc[i] * (int64_t)d.l[k - i]);
+#pragma unroll
+    for (int i = lo; i < (k < 9 ? k : 9); ++i) acc += (uint64_t)m[i] * P29[k - i];
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * NP29) & MASK;
+      acc += (uint64_t)m[k] * P29[0];
+    } else {
+      acc += P29[k - 9];
+      r.l[k - 9] = (uint32_t)acc & MASK;
+    }
+    acc = (uint64_t)((int64_t)acc >> 29);
+  }
+  r.l[8] = (uint32_t)acc + P29[8];
   return r;
 }
 // mul(a, a) with the square's symmetric column terms taken once, doubled (a_i (2 a_j), i < j:
@@ -289,7 +325,6 @@ __device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
     return false;
   }
   const L29 PPP = mul(P, PP);
-  const L29 YP = mul(a.Y, PPP);
   a.ZZZ = mul(a.ZZZ, PPP);
   const L29 Q = mul(a.X, PP);
   const L29 RR = sqr(R);
@@ -297,7 +332,8 @@ __device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) X3.l[i] = RR.l[i] + M8P[i] - PPP.l[i] - 2 * Q.l[i];
   X3 = norm(X3);
-  a.Y = sub(mul(R, sub(Q, X3, M16P)), YP, M8P);
+  // Y3 = R (Q - X3) - Y PPP under one reduction (round 6; round 5: two products and a + 8p - b)
+  a.Y = mulsub(R, sub(Q, X3, M16P), a.Y, PPP);
   a.X = X3;
   a.ZZ = ZZ3;
   return false;

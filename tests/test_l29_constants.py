@@ -184,3 +184,87 @@ def test_lazy_madd_chain_bounds():
             X, Y, ZZ = X3, Y3, ZZ3
             for v, bound in ((X, 11.3), (Y, 11.3), (ZZ, 1.03), (ZZZ, 1.03), (Pv, 17.02), (R, 17.02)):
                 assert value(v) < bound * P
+
+
+def mulsub29(a, b, c, d):
+    """csrc/msm_l29.hpp l29::mulsub, step for step (round 6): a b - c d under ONE Montgomery
+    reduction, p 2^261 added at columns 9..17 so the total stays positive; a signed 64-bit
+    accumulator with arithmetic carries."""
+    p29, np29 = C["P29"], C["NP29"][0]
+    m = [0] * 9
+    r = [0] * 9
+    acc = 0
+    for k in range(17):
+        lo, hi = (0, k) if k < 9 else (k - 8, 8)
+        for i in range(lo, hi + 1):
+            acc += a[i] * b[k - i]
+        for i in range(lo, hi + 1):
+            acc -= c[i] * d[k - i]
+        for i in range(lo, k if k < 9 else 9):
+            acc += m[i] * p29[k - i]
+        assert -(1 << 63) <= acc < 1 << 63, "signed column overflow"
+        if k < 9:
+            m[k] = ((acc & 0xFFFFFFFF) * np29) & MASK
+            acc += m[k] * p29[0]
+            assert acc & MASK == 0
+        else:
+            acc += p29[k - 9]
+            r[k - 9] = acc & MASK
+        acc >>= 29  # arithmetic, as the kernel's v_ashrrev_i64
+    r[8] = acc + p29[8]
+    assert r[8] >= 0
+    return r
+
+
+def test_mulsub_matches_montgomery():
+    """(a b - c d) 2^-261 + p (mod p), normalised limbs, for the operand ranges madd-2008-s's Y3
+    feeds it (R, Q - X3 below 17.3p; Y below 11.3p, PPP below 3.3p) and their extremes."""
+    rinv = pow(2, -261, P)
+    rng = random.Random(2026)
+    cases = [(0, 0, 0, 0), (P - 1, P - 1, 0, 0), (0, 0, int(11.3 * P), int(3.3 * P)),
+             (int(17.3 * P), int(17.3 * P), int(11.3 * P), int(3.3 * P))]
+    cases += [(rng.randrange(int(17.3 * P)), rng.randrange(int(17.3 * P)), rng.randrange(int(11.3 * P)),
+               rng.randrange(int(3.3 * P))) for _ in range(500)]
+    for x, y, u, v in cases:
+        r = mulsub29(limbs(x), limbs(y), limbs(u), limbs(v))
+        assert value(r) % P == (x * y - u * v) * rinv % P
+        assert all(0 <= t <= MASK for t in r[:8])
+        assert 0 < value(r) < (x * y) // (1 << 261) + 2 * P + 1
+
+
+def test_lazy_madd_chain_round6_matches_round5():
+    """The round-6 madd (Y3 = R (Q - X3) - Y PPP under one reduction, plus p) against the round-5
+    form (two products and a lazy difference), step for step over random chains in the kernel's
+    domains: equal modulo p at every step, and every intermediate within its bound (Y now below
+    4p instead of 11.3p; every product input still below 17.3p)."""
+    rng = random.Random(66)
+    one = limbs(pow(2, 266, P))
+    for _ in range(20):
+        X = Y = ZZ = ZZZ = None
+        for step in range(40):
+            x, y = rng.randrange(P), rng.randrange(P)
+            x256, y256 = limbs(x * 2 ** 256 % P), limbs(y * 2 ** 256 % P)
+            if X is None:
+                X, Y = times32(x256), times32(y256)
+                ZZ = ZZZ = one
+                continue
+            Pv = sub(mul29(x256, ZZ), X, C["M16P"])
+            R = sub(mul29(y256, ZZZ), Y, C["M16P"])
+            PP = sqr29(Pv)
+            ZZ3 = mul29(ZZ, PP)
+            PPP = mul29(Pv, PP)
+            ZZZ3 = mul29(ZZZ, PPP)
+            Q = mul29(X, PP)
+            RR = sqr29(R)
+            X3 = [RR[i] + C["M8P"][i] - PPP[i] - 2 * Q[i] for i in range(9)]
+            assert all(0 <= v < 1 << 32 for v in X3)
+            X3 = norm(X3)
+            QX = sub(Q, X3, C["M16P"])
+            Y3_old = sub(mul29(R, QX), mul29(Y, PPP), C["M8P"])
+            Y3 = mulsub29(R, QX, Y, PPP)
+            assert value(Y3) % P == value(Y3_old) % P
+            for v, bound in ((Pv, 17.3), (R, 17.3), (QX, 17.3), (PP, 3.3), (PPP, 3.3), (Q, 3.3)):
+                assert value(v) < bound * P
+            X, Y, ZZ, ZZZ = X3, Y3, ZZ3, ZZZ3
+            for v, bound in ((X, 11.3), (Y, 4.0), (ZZ, 1.03), (ZZZ, 1.03)):
+                assert value(v) < bound * P
