@@ -32,6 +32,8 @@ constexpr uint32_t C266[9] = {0x13349ca1u, 0x1a5d84a8u, 0x0a3e5cacu, 0x100249e0u
 constexpr uint32_t C271[9] = {0x1d1c9c4bu, 0x08a372eeu, 0x1273abadu, 0x17c9d397u, 0x1698b0a7u, 0x09c89e50u, 0x177e12abu, 0x185f3518u, 0x001ed378u};
 constexpr uint32_t C256[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u, 0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};
 constexpr uint32_t C251[9] = {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00080000u};
+constexpr uint32_t P12[9] = {0x05dbdf54u, 0x0c348891u, 0x155fa7b4u, 0x01fda1cau, 0x024631a1u, 0x02470908u, 0x07d28f0du, 0x0c51ca70u, 0x0244b3adu};
+constexpr uint32_t P4[9] = {0x01f3f51cu, 0x041182dbu, 0x11ca8d3cu, 0x0b548b43u, 0x161765e0u, 0x0b6d0302u, 0x029b8504u, 0x197098d0u, 0x00c19139u};
 
 constexpr uint32_t MASK = (1u << 29) - 1;
 
@@ -119,6 +121,36 @@ __device__ __forceinline__ L29 mulsub(const L29& a, const L29& b, const L29& c, 
     acc = (uint64_t)((int64_t)acc >> 29);
   }
   r.l[8] = (uint32_t)acc + P29[8];
+  return r;
+}
+// a b 2^-261 + E - f (mod p) by one product scan (round 6): E (a constant multiple of p) and f
+// (a normalised value) enter at 2^261, i.e. their limbs at columns 9..17, into a signed
+// accumulator; the difference madd-2008-s takes after its first two products (P = U2 - X,
+// R = S2 - Y) then needs no separate a + M - b and carry normalisation. With E = 12p for
+// f = X < 11.3p and E = 4p for f = Y < 3.8p the output is normalised and below 13.1p / 5.1p
+// (tests/test_l29_constants.py::test_mul_shift_sub_matches_montgomery).
+__device__ __forceinline__ L29 mul_shift_sub(const L29& a, const L29& b, const uint32_t* E, const L29& f) {
+  uint32_t m[9];
+  L29 r;
+  uint64_t acc = 0;  // signed from column 9 on
+#pragma unroll
+  for (int k = 0; k < 17; ++k) {
+    const int lo = k < 9 ? 0 : k - 8, hi = k < 9 ? k : 8;
+#pragma unroll
+    for (int i = lo; i <= hi; ++i) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = lo; i < (k < 9 ? k : 9); ++i) acc += (uint64_t)m[i] * P29[k - i];
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * NP29) & MASK;
+      acc += (uint64_t)m[k] * P29[0];
+      acc >>= 29;  // nonnegative so far
+    } else {
+      acc += (uint64_t)(int64_t)((int32_t)E[k - 9] - (int32_t)f.l[k - 9]);
+      r.l[k - 9] = (uint32_t)acc & MASK;
+      acc = (uint64_t)((int64_t)acc >> 29);
+    }
+  }
+  r.l[8] = (uint32_t)acc + E[8] - f.l[8];
   return r;
 }
 // mul(a, a) with the square's symmetric column terms taken once, doubled (a_i (2 a_j), i < j:
@@ -313,8 +345,9 @@ __device__ __forceinline__ bool madd(Acc& a, const L29& x, const L29& y) {
     start_run(a, x, y);
     return false;
   }
-  const L29 P = sub(mul(x, a.ZZ), a.X, M16P);
-  const L29 R = sub(mul(y, a.ZZZ), a.Y, M16P);
+  // P = U2 - X, R = S2 - Y with the differences inside the products' reductions (round 6)
+  const L29 P = mul_shift_sub(x, a.ZZ, P12, a.X);
+  const L29 R = mul_shift_sub(y, a.ZZZ, P4, a.Y);
   const L29 PP = sqr(P);
   const L29 ZZ3 = mul(a.ZZ, PP);
   if (zero_mod_p(ZZ3)) {  // P == 0: doubling (R == 0) or the identity

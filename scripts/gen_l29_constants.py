@@ -2,7 +2,8 @@
 """Constants of the 29-bit-limb Montgomery arithmetic of csrc/msm_l29.hpp (BN254 Fq,
 R = 2^261): p's limbs, -p^-1 mod 2^29, 8p and 16p in redundant limbs (every limb >= 2^31 - 4
 below the top, so a + M - b never borrows for normalised b), and the domain constants
-2^266, 2^271, 2^256, 2^251 mod p. Prints the C++ block; tests/test_l29_constants.py checks
+2^266, 2^271, 2^256, 2^251 mod p, and 12p, 4p in normalised limbs (round 6: the values added
+at 2^261 by l29::mul_shift_sub). Prints the C++ block; tests/test_l29_constants.py checks
 the header against this script."""
 P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 MASK = (1 << 29) - 1
@@ -35,6 +36,8 @@ def constants():
         "C271": limbs(pow(2, 271, P)),
         "C256": limbs(pow(2, 256, P)),
         "C251": limbs(pow(2, 251, P)),
+        "P12": limbs(12 * P),
+        "P4": limbs(4 * P),
     }
 
 

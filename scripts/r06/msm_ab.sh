@@ -12,4 +12,4 @@ for i in 1 2; do
   for L in libpbf_base.so libpbf.so; do
     PBF_LIB=$PWD/plonk-by-fingers_amd/$L timeout -k 10 300 python scripts/r06/msm_ab.py || exit 1
   done
-done | tee gpurun_out/r06/msm_mulsub_ab.log
+done | tee gpurun_out/r06/msm_ab_${TAG:-x}.log

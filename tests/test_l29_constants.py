@@ -268,3 +268,85 @@ def test_lazy_madd_chain_round6_matches_round5():
             X, Y, ZZ, ZZZ = X3, Y3, ZZ3, ZZZ3
             for v, bound in ((X, 11.3), (Y, 4.0), (ZZ, 1.03), (ZZZ, 1.03)):
                 assert value(v) < bound * P
+
+
+def mul_shift_sub29(a, b, E, f):
+    """csrc/msm_l29.hpp l29::mul_shift_sub, step for step (round 6): a b 2^-261 + E - f with E and
+    f entering at columns 9..17 of one product scan, signed carries from column 9 on."""
+    p29, np29 = C["P29"], C["NP29"][0]
+    m = [0] * 9
+    r = [0] * 9
+    acc = 0
+    for k in range(17):
+        lo, hi = (0, k) if k < 9 else (k - 8, 8)
+        for i in range(lo, hi + 1):
+            acc += a[i] * b[k - i]
+        for i in range(lo, k if k < 9 else 9):
+            acc += m[i] * p29[k - i]
+        assert -(1 << 63) <= acc < 1 << 63
+        if k < 9:
+            m[k] = ((acc & 0xFFFFFFFF) * np29) & MASK
+            acc += m[k] * p29[0]
+            assert acc & MASK == 0 and acc >= 0
+        else:
+            acc += E[k - 9] - f[k - 9]
+            assert -(1 << 63) <= acc < 1 << 63
+            r[k - 9] = acc & MASK
+        acc >>= 29
+    r[8] = acc + E[8] - f[8]
+    assert 0 <= r[8] < 1 << 32
+    return r
+
+
+def test_mul_shift_sub_matches_montgomery():
+    """P = x ZZ - X + 12p and R = y ZZZ - Y + 4p in one reduction each, over the operand ranges of
+    madd-2008-s (x, y canonical points, ZZ, ZZZ below 1.03p, X below 11.3p, Y below 3.8p)."""
+    rinv = pow(2, -261, P)
+    rng = random.Random(1206)
+    for E, fmax, out in ((C["P12"], 11.3, 13.1), (C["P4"], 3.8, 5.1)):
+        e = value(E)
+        cases = [(0, 0, int(fmax * P) - 1), (P - 1, int(1.03 * P), 0)]
+        cases += [(rng.randrange(P), rng.randrange(int(1.03 * P)), rng.randrange(int(fmax * P))) for _ in range(500)]
+        for x, zz, f in cases:
+            r = mul_shift_sub29(limbs(x), limbs(zz), E, limbs(f))
+            assert value(r) % P == (x * zz * rinv + e - f) % P
+            assert all(0 <= t <= MASK for t in r[:8])
+            assert 0 <= value(r) < out * P
+
+
+def test_lazy_madd_chain_round6_full():
+    """The round-6 madd as the kernel runs it (P, R by mul_shift_sub; Y3 by mulsub) against plain
+    modular arithmetic of madd-2008-s over random chains, with every product input below 17.3p."""
+    rng = random.Random(67)
+    one = limbs(pow(2, 266, P))
+    rinv = pow(2, -261, P)
+    for _ in range(20):
+        X = Y = ZZ = ZZZ = None
+        for step in range(40):
+            x, y = rng.randrange(P), rng.randrange(P)
+            x256, y256 = limbs(x * 2 ** 256 % P), limbs(y * 2 ** 256 % P)
+            if X is None:
+                X, Y = times32(x256), times32(y256)
+                ZZ = ZZZ = one
+                continue
+            Pv = mul_shift_sub29(x256, ZZ, C["P12"], X)
+            R = mul_shift_sub29(y256, ZZZ, C["P4"], Y)
+            assert value(Pv) % P == (value(x256) * value(ZZ) * rinv - value(X)) % P
+            assert value(R) % P == (value(y256) * value(ZZZ) * rinv - value(Y)) % P
+            PP = sqr29(Pv)
+            ZZ3 = mul29(ZZ, PP)
+            PPP = mul29(Pv, PP)
+            ZZZ3 = mul29(ZZZ, PPP)
+            Q = mul29(X, PP)
+            RR = sqr29(R)
+            X3 = [RR[i] + C["M8P"][i] - PPP[i] - 2 * Q[i] for i in range(9)]
+            assert all(0 <= v < 1 << 32 for v in X3)
+            X3 = norm(X3)
+            QX = sub(Q, X3, C["M16P"])
+            Y3 = mulsub29(R, QX, Y, PPP)
+            assert value(Y3) % P == (value(R) * value(QX) - value(Y) * value(PPP)) * rinv % P
+            for v, bound in ((Pv, 13.1), (R, 5.1), (QX, 17.3), (PP, 3.3), (PPP, 3.3), (Q, 3.3)):
+                assert value(v) < bound * P
+            X, Y, ZZ, ZZZ = X3, Y3, ZZ3, ZZZ3
+            for v, bound in ((X, 11.3), (Y, 3.8), (ZZ, 1.03), (ZZZ, 1.03)):
+                assert value(v) < bound * P
