@@ -132,7 +132,7 @@ int pbf_ctx_set_option(pbf_ctx* ctx, const char* name, const char* value) {
   static const char* const known[] = {"ntt.passes",  "ntt.group",       "ntt.streams",   "ntt.twmax_log",
                                       "ntt.twsplit", "ntt.no_rg",       "ntt256.maxr",   "ntt256.twlog",
                                       "msm.fx_c",    "g1.mul_base",     "pair.engine",   "pair.lane_wpe",
-                                      "prover.pk",   "prover.timing",   "verifier.vk"};
+                                      "prover.pk",   "prover.timing",   "verifier.vk",   "ntt256.l29"};
   bool ok = false;
   for (const char* k : known) ok = ok || strcmp(k, name) == 0;
   if (!ok) return fail(PBF_EINVAL, std::string("unknown option ") + name);

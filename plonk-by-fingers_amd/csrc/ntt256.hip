@@ -6,9 +6,11 @@
 // pass's store). Replaces fft.rs:66-78 and fft.rs:109-132 for the 256-bit field.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 #include "../../include/pbf.h"
 #include "fp256.hpp"
+#include "fr29.hpp"
 #include "internal.hpp"
 
 // Product form of the pass kernel's butterflies and twiddles: the single-chain Montgomery
@@ -20,6 +22,7 @@
 #define PBF_FRMUL(a, b) Fr::mul_tp(a, b)
 #endif
 namespace pbf {
+using l29::L29;
 
 struct Pass256 {
   const U256* in;
@@ -213,6 +216,175 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PBF_NTT
   }
 }
 
+// ---- The same passes on nine 29-bit limbs (round 6, fr29.hpp): ntt256l_pass_kernel. Same
+// Stockham shape, tile, tables and element order as ntt256_pass_kernel; the elements stay in
+// lazily reduced 29-bit limbs from the pass's loads to its stores (36 B in LDS), every table
+// holds w 2^261 mod r in limbs (Pass256L), and the stores are canonical again, so both kernels
+// write the same integers. Bounds of every step: fr29.hpp, tests/test_fr29_bounds.py.
+struct Pass256L {
+  const U256* in;
+  U256* out;
+  const L29* rtab;    // w_R^m 2^261
+  const L29* twpass;  // [r][k] pass twiddles 2^261 (n^-1 folded into the inverse's last pass) or null
+  const L29* tw0;     // two-level tables 2^261 (tw1: tw1s for the inverse's last pass)
+  const L29* tw1;
+  const U256* mul_by;  // last pass only, or null: outputs become mul_by[i] y 2^-256 (mul_ntt)
+  uint64_t n;
+  uint32_t log_n, log_ns, tw_bits, blocks_per_poly, batch;
+};
+
+// radix-4 DIF in registers (natural in, bit-reversed out; dif256_row's order): inputs normalised
+// below 2.05 r, outputs below 12.1 r with limbs below 2^32 (fr29.hpp)
+__device__ __forceinline__ void dft4_29(L29* v, const L29& w4) {
+  const L29 n0 = fr29::add(v[0], v[2]);
+  const L29 n2 = fr29::sub(v[0], v[2], fr29::B4R);
+  const L29 n1 = fr29::add(v[1], v[3]);
+  const L29 n3 = fr29::mul(fr29::sub(v[1], v[3], fr29::B4R), w4);
+  v[0] = fr29::add(n0, n1);
+  v[1] = fr29::sub(n0, n1, fr29::B8R);
+  v[2] = fr29::add(n2, n3);
+  v[3] = fr29::sub(n2, n3, fr29::B2R);
+}
+__device__ __forceinline__ void dft2_29(L29* v) {
+  const L29 a = fr29::add(v[0], v[1]);
+  v[1] = fr29::sub(v[0], v[1], fr29::B4R);
+  v[0] = a;
+}
+
+template <int E, int N, typename F>
+__device__ __forceinline__ void unroll_each(F&& f) {
+  if constexpr (E < N) {
+    f(std::integral_constant<int, E>{});
+    unroll_each<E + 1, N>(f);
+  }
+}
+
+template <int LOGR, int W, int NT, int LQ, int S>
+__device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const Pass256L& a, const U256* in,
+                                        U256* out, uint64_t j0, int t) {
+  constexpr int R = 1 << LOGR;
+  constexpr int PER = (R * W) / NT;
+  constexpr int NST = st_count(LOGR, LQ);
+  constexpr int LOGQ = st_logq(LOGR, S, LQ);
+  constexpr int Q = 1 << LOGQ;
+  constexpr int L = 1 << st_logl(LOGR, S, LQ);
+  constexpr int NSUB = PER / Q;
+  constexpr bool LAST = (S == NST - 1);
+  static_assert(LQ == 2 && (Q == 2 || Q == 4), "radix-4 register sub-DFTs");
+  if constexpr (S == 0) {
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
+#pragma unroll
+      for (int c = 0; c < Q; ++c)
+        v[u * Q + c] = l29::from_u256(in[(j0 + w) + (uint64_t)(i + c * (R / Q)) * (a.n >> LOGR)]);
+    }
+    // the pass twiddle, one element at a time (a table of 4 limb twiddles would not fit beside v)
+    // (compile-time element indices: the loop vectoriser had turned a plain loop here into one
+    // over v in scratch memory)
+    if (a.log_ns > 0 && a.twpass) {
+      unroll_each<0, PER>([&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+        const int sub = t + NT * (e / Q);
+        const uint64_t k = (j0 + sub % W) & ((1ull << a.log_ns) - 1);
+        const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
+        v[e] = fr29::mul(v[e], a.twpass[(r << a.log_ns) + k]);
+      });
+    } else if (a.log_ns > 0) {
+      unroll_each<0, PER>([&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+        const int sub = t + NT * (e / Q);
+        const uint64_t k = (j0 + sub % W) & ((1ull << a.log_ns) - 1);
+        const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
+        const uint64_t x = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
+        v[e] = fr29::mul(v[e], fr29::mul(a.tw0[x & ((1ull << a.tw_bits) - 1)], a.tw1[x >> a.tw_bits]));
+      });
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) {
+      const int sub = t + NT * u;
+      const int w = sub % W, i = sub / W;
+      const int k = i % L;
+#pragma unroll
+      for (int c = 0; c < Q; ++c) {
+        const int r = i + c * (R / Q);
+        L29 x = lds[r * W + w];
+        if (c != 0 && k != 0) x = fr29::mul(x, a.rtab[(R / (L * Q)) * c * k]);
+        v[u * Q + c] = x;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NSUB; ++u) {
+    if constexpr (Q == 4) dft4_29(v + u * Q, w4);
+    else dft2_29(v + u * Q);
+  }
+  if constexpr (S > 0) __syncthreads();
+#pragma unroll
+  for (int u = 0; u < NSUB; ++u) {
+    const int sub = t + NT * u;
+    const int w = sub % W, i = sub / W;
+    const int k = i % L;
+#pragma unroll
+    for (int d = 0; d < Q; ++d) {
+      const L29 y = fr29::reduce(v[u * Q + brev_c(d, LOGQ)]);
+      const int r = (i / L) * L * Q + k + d * L;
+      if constexpr (!LAST) {
+        lds[r * W + w] = y;
+      } else if (a.log_ns == 0) {
+        reinterpret_cast<U256*>(lds)[w * (R + 1) + r] = fr29::canon(y);
+      } else {
+        const uint64_t j = j0 + w;
+        const uint64_t msk = (1ull << a.log_ns) - 1;
+        const uint64_t o = ((j >> a.log_ns) << (a.log_ns + LOGR)) + (j & msk) + ((uint64_t)r << a.log_ns);
+        // mul_ntt's product as in ntt256_pass_kernel (mul_by y 2^-256: the extra-R inverse plans
+        // serve both kernels); the same element is read, then written
+        const U256 c = fr29::canon(y);
+        out[o] = a.mul_by ? Fr::mul_tp(a.mul_by[(out - a.out) + o], c) : c;
+      }
+    }
+  }
+  if constexpr (!LAST) {
+    __syncthreads();
+    stage29<LOGR, W, NT, LQ, S + 1>(v, lds, w4, a, in, out, j0, t);
+  }
+}
+
+template <int LOGR, int W, int NT, int LQ>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PBF_NTT256_WPE))) ntt256l_pass_kernel(Pass256L a) {
+  constexpr int R = 1 << LOGR;
+  constexpr int E = R * W;
+  constexpr int PER = E / NT;
+  static_assert(PER % 4 == 0 && LOGR >= LQ && E * 36 >= (E + W) * 32, "bad shape");
+  __shared__ L29 lds[E + W];
+  const uint32_t poly = blockIdx.x / a.blocks_per_poly;
+  const uint64_t j0 = (uint64_t)(blockIdx.x % a.blocks_per_poly) * W;
+  const U256* in = a.in + (uint64_t)poly * a.n;
+  U256* out = a.out + (uint64_t)poly * a.n;
+  const int t = threadIdx.x;
+  const L29 w4 = a.rtab[R / 4];
+  L29 v[PER];
+  stage29<LOGR, W, NT, LQ, 0>(v, lds, w4, a, in, out, j0, t);
+  if (a.log_ns == 0) {
+    __syncthreads();
+    U256* o = out + j0 * R;
+    const U256* l = reinterpret_cast<const U256*>(lds);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int m = t + NT * u;
+      o[m] = l[(m / R) * (R + 1) + (m % R)];
+    }
+  }
+}
+
+// table conversion: out[i] = in[i] 2^5 (in: w 2^256 mod r, canonical) in 29-bit limbs = w 2^261
+__global__ void tw256_to29_kernel(const U256* in, L29* out, uint64_t count, U256 c32m) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = l29::from_u256(Fr::mul(in[i], c32m));
+}
+
 // Whole transform for n <= 2048 in one workgroup (bit-reversed load, radix-2 DIT).
 __global__ void __launch_bounds__(256) ntt256_small_kernel(const U256* in, U256* out, const U256* tw, uint32_t logn,
                                                            U256 n_inv, uint32_t scale) {
@@ -308,7 +480,27 @@ struct Plan256 {
   bool fold_scale = false;  // inverse: n^-1 folded into the last pass's twiddles (tw1s / its table)
   DevBuf small_tw, tw0, tw1, tw1s;
   std::vector<std::shared_ptr<DevBuf>> rtab, twpass;
+  // the 29-bit-limb passes (option ntt256.l29, default on; multi-pass plans with the scale folded):
+  // the same tables as w 2^261 in limbs
+  bool l29 = false;
+  DevBuf tw0_29, tw1_29, tw1s_29;
+  std::vector<std::shared_ptr<DevBuf>> rtab29, twpass29;
 };
+
+// in (count U256 Montgomery values w 2^256) -> out (count L29 values w 2^261)
+static int to29(const DevBuf& in, DevBuf& out, uint64_t count) {
+  if (!count) return 0;
+  int rc = out.ensure(count * sizeof(L29));
+  if (rc) return rc;
+  U256 c32 = Fr::one_plain();
+  c32.w[0] = 32;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(tw256_to29_kernel, dim3((uint32_t)blocks), dim3(256), 0, 0, (const U256*)in.p, (L29*)out.p, count,
+                     Fr::to_mont(c32));
+  PBF_HIP(hipGetLastError());
+  return 0;
+}
 
 static int up256(DevBuf& b, const std::vector<U256>& v) {
   int rc = b.ensure(v.size() * sizeof(U256));
@@ -404,6 +596,30 @@ static int make_plan256(const pbf::Options& o, const uint64_t* omega, uint64_t n
     ns *= R;
     log_ns += lr;
   }
+  // the 29-bit-limb passes' tables (ntt256l_pass_kernel; PBF_NTT256_SCALE_PASS / CONV, A/B
+  // builds only, keep the 32-bit kernel). A converted per-pass table replaces its 32-bit form.
+  p->l29 = o.num("ntt256.l29", 1) != 0 && p->fold_scale == (inverse != 0) && !ab_env("PBF_NTT256_CONV");
+  if (p->l29) {
+    const uint64_t nlo = 1ull << p->tw_bits, nhi = n >> p->tw_bits;
+    if ((rc = to29(p->tw0, p->tw0_29, nlo)) || (rc = to29(p->tw1, p->tw1_29, nhi)) ||
+        (p->fold_scale && (rc = to29(p->tw1s, p->tw1s_29, nhi))))
+      return rc;
+    ns = 1;
+    for (size_t pi = 0; pi < p->logr.size(); ++pi) {
+      const uint64_t R = 1ull << p->logr[pi];
+      auto rb = std::make_shared<DevBuf>(), tb = std::make_shared<DevBuf>();
+      if ((rc = to29(*p->rtab[pi], *rb, R))) return rc;
+      if (p->twpass[pi]->p) {
+        if ((rc = to29(*p->twpass[pi], *tb, R * ns))) return rc;
+        PBF_HIP(hipStreamSynchronize(0));
+        p->twpass[pi]->release();
+      }
+      p->rtab29.push_back(rb);
+      p->twpass29.push_back(tb);
+      ns *= R;
+    }
+    PBF_HIP(hipStreamSynchronize(0));
+  }
   return 0;
 }
 
@@ -421,6 +637,18 @@ static Pass256Fn pass256_fn(int logr) {
   }
 }
 static int threads256(int logr) { return ((cols256(logr) << logr) / 4); }
+typedef void (*Pass256LFn)(Pass256L);
+static Pass256LFn pass256l_fn(int logr) {
+  switch (logr) {  // the shapes of pass256_fn
+    case 4: return ntt256l_pass_kernel<4, 64, 256, 2>;
+    case 5: return ntt256l_pass_kernel<5, 64, 512, 2>;
+    case 6: return ntt256l_pass_kernel<6, 32, 512, 2>;
+    case 7: return ntt256l_pass_kernel<7, 16, 512, 2>;
+    case 8: return ntt256l_pass_kernel<8, 8, 512, 2>;
+    case 9: return ntt256l_pass_kernel<9, 4, 512, 2>;
+    default: return nullptr;
+  }
+}
 
 // mul_by (not for n <= 2048): the last pass multiplies its outputs by mul_by's elements (one
 // Montgomery product: mont(m, y) = m y / R) -- mul_ntt's pointwise product fused into the second
@@ -445,6 +673,34 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
   if (!rc && P > 2) rc = s1.ensure(bytes);
   if (rc) return rc;
   uint32_t log_ns = 0;
+  if (p.l29) {
+    for (size_t i = 0; i < P; ++i) {
+      const int lr = p.logr[i];
+      const int W = cols256(lr);
+      Pass256L a;
+      a.in = (i == 0) ? d_in : (const U256*)(((i - 1) & 1) ? s1.p : s0.p);
+      a.out = (i == P - 1) ? d_out : (U256*)((i & 1) ? s1.p : s0.p);
+      a.rtab = (const L29*)p.rtab29[i]->p;
+      a.twpass = (const L29*)p.twpass29[i]->p;
+      a.tw0 = (const L29*)p.tw0_29.p;
+      a.tw1 = (const L29*)((p.fold_scale && i == P - 1) ? p.tw1s_29.p : p.tw1_29.p);
+      a.mul_by = (i == P - 1) ? mul_by : nullptr;
+      a.n = p.n;
+      a.log_n = p.log_n;
+      a.log_ns = log_ns;
+      a.tw_bits = p.tw_bits;
+      a.blocks_per_poly = (uint32_t)((p.n >> lr) / W);
+      a.batch = (uint32_t)batch;
+      Pass256LFn fn = pass256l_fn(lr);
+      if (!fn) return fail(PBF_EINVAL, "no 256-bit kernel for this radix");
+      const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
+      if (blocks > 0x7fffffffull) return fail(PBF_EINVAL, "batch too large");
+      hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(threads256(lr)), 0, st, a);
+      PBF_HIP(hipGetLastError());
+      log_ns += lr;
+    }
+    return 0;
+  }
   for (size_t i = 0; i < P; ++i) {
     const int lr = p.logr[i];
     const int W = cols256(lr);

@@ -6,6 +6,7 @@ below the top, so a + M - b never borrows for normalised b), and the domain cons
 at 2^261 by l29::mul_shift_sub). Prints the C++ block; tests/test_l29_constants.py checks
 the header against this script."""
 P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
+R = 21888242871839275222246405745257275088548364400416034343698204186575808495617  # BN254 Fr
 MASK = (1 << 29) - 1
 
 
@@ -26,6 +27,28 @@ def redundant(mult):
     return m
 
 
+def redundant_r(mult, a):
+    """mult r with 2^a added to limbs 0..7 and 2^(a-29) taken from the next limb: every limb but
+    the top at least 2^a - 2^(a-29), so x + B - y never borrows for y's limbs below that"""
+    n = limbs(mult * R)
+    m = [n[0] + (1 << a)] + [n[i] + (1 << a) - (1 << (a - 29)) for i in range(1, 8)] + [n[8] - (1 << (a - 29))]
+    assert sum(x << (29 * i) for i, x in enumerate(m)) == mult * R
+    assert all(0 <= x < (1 << 32) for x in m)
+    return m
+
+
+def fr_constants():
+    """csrc/fr29.hpp (round 6: the Fr NTT passes on 29-bit limbs, R' = 2^261)"""
+    return {
+        "R29": limbs(R),
+        "NR29": [(-pow(R, -1, 1 << 29)) % (1 << 29)],
+        "QC": [(1 << 264) // R],
+        "B4R": redundant_r(4, 29),
+        "B8R": redundant_r(8, 30),
+        "B2R": redundant_r(2, 29),
+    }
+
+
 def constants():
     return {
         "P29": limbs(P),
@@ -42,7 +65,7 @@ def constants():
 
 
 def main():
-    for name, v in constants().items():
+    for name, v in list(constants().items()) + list(fr_constants().items()):
         vals = ", ".join(f"0x{x:08x}u" for x in v)
         if len(v) == 1:
             print(f"constexpr uint32_t {name} = {vals};")

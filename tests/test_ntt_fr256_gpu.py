@@ -148,3 +148,54 @@ def test_fr_errors(ctx):
         ctx.ntt_fr(bn254.root_of_unity(16), [1] * 8)  # omega order 16 != 8
     with pytest.raises(pbf.PbfError):
         ctx.ntt_fr(bn254.root_of_unity(8), [R] * 8)  # non-canonical
+
+
+@pytest.mark.parametrize("logn,maxr", [(12, "4"), (13, "5"), (14, "6"), (15, "7"), (16, "8"), (18, "9"), (21, None),
+                                       (23, None)])
+def test_l29_passes_match_32bit_passes(logn, maxr):
+    """The 29-bit-limb pass kernels (ntt256l_pass_kernel, default; fr29.hpp) against the 32-bit
+    ones (context option ntt256.l29 = 0), bit for bit, through every pass radix (4..9) and the
+    config-3 size: forward, inverse and the fused mul_ntt, on random inputs and on the worst
+    cases of the lazy bounds (every element r - 1; alternating 0 and r - 1)."""
+    import torch
+
+    n = 1 << logn
+    w = bn254.root_of_unity(n)
+    rm1 = np.array([(R - 1) >> (64 * k) & ((1 << 64) - 1) for k in range(4)], dtype=np.uint64)
+    inputs = [bn254.random_limbs(n, 70 + logn), np.tile(rm1, n)]
+    alt = np.tile(rm1, n).reshape(n, 4)
+    alt[::2] = 0
+    inputs.append(alt.reshape(-1))
+    res = []
+    for opts in ({"ntt256.l29": "0"}, {}):
+        if maxr:
+            opts = dict(opts, **{"ntt256.maxr": maxr})
+        c = pbf.Context(0, options=opts)
+        try:
+            outs = []
+            for x_np in inputs:
+                x = torch.from_numpy(np.ascontiguousarray(x_np).view(np.int64)).cuda()
+                f = torch.empty_like(x)
+                c.ntt_fr_batch_dev(w, x.data_ptr(), f.data_ptr(), n, 1)
+                i = torch.empty_like(x)
+                c.ntt_fr_batch_dev(w, x.data_ptr(), i.data_ptr(), n, 1, inverse=True)
+                half = torch.zeros_like(x)
+                half[: n * 2] = x[: n * 2]
+                hb = torch.zeros_like(x)
+                hb[: n * 2] = f[: n * 2]  # canonical values of another shape
+                m = torch.empty_like(x)
+                c.mul_ntt_fr_dev(w, half.data_ptr(), hb.data_ptr(), m.data_ptr(), n, 1,
+                                 stream=torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+                outs.append((f.cpu(), i.cpu(), m.cpu()))
+            res.append(outs)
+        finally:
+            c.close()
+    for a, b in zip(res[0], res[1]):
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+    # every output canonical
+    for f, i, m in res[1]:
+        for t in (f, i, m):
+            top = t.numpy().view(np.uint64).reshape(-1, 4)[:, 3]
+            assert int(top.max()) <= (R >> 192)
