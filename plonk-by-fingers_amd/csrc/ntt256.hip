@@ -251,6 +251,31 @@ __device__ __forceinline__ void dft2_29(L29* v) {
   v[0] = a;
 }
 
+// An element in LDS: limbs 0..7 as one 16-B aligned 32-B word (two 128-bit LDS accesses) and limb 8
+// in an array of its own (36 B per element, as two workgroups per CU need)
+struct alignas(16) L8 {
+  uint32_t l[8];
+};
+struct Lds29 {
+  L8* lo;
+  uint32_t* hi;
+  __device__ __forceinline__ L29 ld(int i) const {
+    const L8 a = lo[i];
+    L29 r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r.l[k] = a.l[k];
+    r.l[8] = hi[i];
+    return r;
+  }
+  __device__ __forceinline__ void st(int i, const L29& x) const {
+    L8 a;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.l[k] = x.l[k];
+    lo[i] = a;
+    hi[i] = x.l[8];
+  }
+};
+
 template <int E, int N, typename F>
 __device__ __forceinline__ void unroll_each(F&& f) {
   if constexpr (E < N) {
@@ -260,8 +285,8 @@ __device__ __forceinline__ void unroll_each(F&& f) {
 }
 
 template <int LOGR, int W, int NT, int LQ, int S>
-__device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const Pass256L& a, const U256* in,
-                                        U256* out, uint64_t j0, int t) {
+__device__ __forceinline__ void stage29(L29* v, const Lds29& lds, const Pass256L& a, const U256* in, U256* out,
+                                        uint64_t j0, int t) {
   constexpr int R = 1 << LOGR;
   constexpr int PER = (R * W) / NT;
   constexpr int NST = st_count(LOGR, LQ);
@@ -290,6 +315,7 @@ __device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const P
         const uint64_t k = (j0 + sub % W) & ((1ull << a.log_ns) - 1);
         const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
         v[e] = fr29::mul(v[e], a.twpass[(r << a.log_ns) + k]);
+        __builtin_amdgcn_sched_barrier(0);  // one twiddle's loads and product at a time (VGPRs)
       });
     } else if (a.log_ns > 0) {
       unroll_each<0, PER>([&](auto ec) {
@@ -299,6 +325,7 @@ __device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const P
         const uint64_t r = (uint64_t)(sub / W + (e % Q) * (R / Q));
         const uint64_t x = ((r * k) << (a.log_n - a.log_ns - LOGR)) & (a.n - 1);
         v[e] = fr29::mul(v[e], fr29::mul(a.tw0[x & ((1ull << a.tw_bits) - 1)], a.tw1[x >> a.tw_bits]));
+        __builtin_amdgcn_sched_barrier(0);
       });
     }
   } else {
@@ -310,16 +337,21 @@ __device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const P
 #pragma unroll
       for (int c = 0; c < Q; ++c) {
         const int r = i + c * (R / Q);
-        L29 x = lds[r * W + w];
-        if (c != 0 && k != 0) x = fr29::mul(x, a.rtab[(R / (L * Q)) * c * k]);
-        v[u * Q + c] = x;
+        // the previous stage stored its outputs unreduced: the inter-stage twiddle's product
+        // (w^0 = 2^261 included, where k = 0) or, for c = 0, reduce() bounds them again
+        const L29 x = lds.ld(r * W + w);
+        v[u * Q + c] = c != 0 ? fr29::mul(x, a.rtab[(R / (L * Q)) * c * k]) : fr29::reduce(x);
+        __builtin_amdgcn_sched_barrier(0);  // one element's load and product at a time (VGPRs)
       }
     }
   }
+  if constexpr (Q == 4) {
+    const L29 w4 = a.rtab[R / 4];  // uniform: read per stage (scalar loads), not held in VGPRs
 #pragma unroll
-  for (int u = 0; u < NSUB; ++u) {
-    if constexpr (Q == 4) dft4_29(v + u * Q, w4);
-    else dft2_29(v + u * Q);
+    for (int u = 0; u < NSUB; ++u) dft4_29(v + u * Q, w4);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) dft2_29(v + u * Q);
   }
   if constexpr (S > 0) __syncthreads();
 #pragma unroll
@@ -329,12 +361,14 @@ __device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const P
     const int k = i % L;
 #pragma unroll
     for (int d = 0; d < Q; ++d) {
-      const L29 y = fr29::reduce(v[u * Q + brev_c(d, LOGQ)]);
       const int r = (i / L) * L * Q + k + d * L;
       if constexpr (!LAST) {
-        lds[r * W + w] = y;
-      } else if (a.log_ns == 0) {
-        reinterpret_cast<U256*>(lds)[w * (R + 1) + r] = fr29::canon(y);
+        lds.st(r * W + w, v[u * Q + brev_c(d, LOGQ)]);
+        continue;
+      }
+      const L29 y = fr29::reduce(v[u * Q + brev_c(d, LOGQ)]);
+      if (a.log_ns == 0) {
+        reinterpret_cast<U256*>(lds.lo)[w * (R + 1) + r] = fr29::canon(y);
       } else {
         const uint64_t j = j0 + w;
         const uint64_t msk = (1ull << a.log_ns) - 1;
@@ -348,29 +382,30 @@ __device__ __forceinline__ void stage29(L29* v, L29* lds, const L29& w4, const P
   }
   if constexpr (!LAST) {
     __syncthreads();
-    stage29<LOGR, W, NT, LQ, S + 1>(v, lds, w4, a, in, out, j0, t);
+    stage29<LOGR, W, NT, LQ, S + 1>(v, lds, a, in, out, j0, t);
   }
 }
 
 template <int LOGR, int W, int NT, int LQ>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PBF_NTT256_WPE))) ntt256l_pass_kernel(Pass256L a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT * 2 >= 1024 ? 4 : 3))) ntt256l_pass_kernel(Pass256L a) {
   constexpr int R = 1 << LOGR;
   constexpr int E = R * W;
   constexpr int PER = E / NT;
-  static_assert(PER % 4 == 0 && LOGR >= LQ && E * 36 >= (E + W) * 32, "bad shape");
-  __shared__ L29 lds[E + W];
+  static_assert(PER % 4 == 0 && LOGR >= LQ, "bad shape");
+  __shared__ L8 lds_lo[E + W];  // also the last stage's U256 transpose tile (E + W elements)
+  __shared__ uint32_t lds_hi[E + W];
+  const Lds29 lds{lds_lo, lds_hi};
   const uint32_t poly = blockIdx.x / a.blocks_per_poly;
   const uint64_t j0 = (uint64_t)(blockIdx.x % a.blocks_per_poly) * W;
   const U256* in = a.in + (uint64_t)poly * a.n;
   U256* out = a.out + (uint64_t)poly * a.n;
   const int t = threadIdx.x;
-  const L29 w4 = a.rtab[R / 4];
   L29 v[PER];
-  stage29<LOGR, W, NT, LQ, 0>(v, lds, w4, a, in, out, j0, t);
+  stage29<LOGR, W, NT, LQ, 0>(v, lds, a, in, out, j0, t);
   if (a.log_ns == 0) {
     __syncthreads();
     U256* o = out + j0 * R;
-    const U256* l = reinterpret_cast<const U256*>(lds);
+    const U256* l = reinterpret_cast<const U256*>(lds_lo);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int m = t + NT * u;
@@ -637,14 +672,20 @@ static Pass256Fn pass256_fn(int logr) {
   }
 }
 static int threads256(int logr) { return ((cols256(logr) << logr) / 4); }
+// the 29-bit passes: radix 2^4..2^8 with half the columns per workgroup (half the threads, 4
+// elements each: three workgroups of 4 waves per CU at up to 168 VGPRs), radix 2^9 with the full
+// tile at 4 waves per SIMD (config 3, 8 + 8 + 7: 3.11 -> 3.04 ms; 4 x 2^26, 9 + 9 + 8: 36.5
+// against 37.3 ms with every radix halved; profiles/r06/fr29_ab_c.log)
+static int cols256l(int logr) { return logr == 9 ? cols256(logr) : cols256(logr) / 2; }
+static int threads256l(int logr) { return ((cols256l(logr) << logr) / 4); }
 typedef void (*Pass256LFn)(Pass256L);
 static Pass256LFn pass256l_fn(int logr) {
   switch (logr) {  // the shapes of pass256_fn
-    case 4: return ntt256l_pass_kernel<4, 64, 256, 2>;
-    case 5: return ntt256l_pass_kernel<5, 64, 512, 2>;
-    case 6: return ntt256l_pass_kernel<6, 32, 512, 2>;
-    case 7: return ntt256l_pass_kernel<7, 16, 512, 2>;
-    case 8: return ntt256l_pass_kernel<8, 8, 512, 2>;
+    case 4: return ntt256l_pass_kernel<4, 32, 128, 2>;
+    case 5: return ntt256l_pass_kernel<5, 32, 256, 2>;
+    case 6: return ntt256l_pass_kernel<6, 16, 256, 2>;
+    case 7: return ntt256l_pass_kernel<7, 8, 256, 2>;
+    case 8: return ntt256l_pass_kernel<8, 4, 256, 2>;
     case 9: return ntt256l_pass_kernel<9, 4, 512, 2>;
     default: return nullptr;
   }
@@ -676,7 +717,7 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
   if (p.l29) {
     for (size_t i = 0; i < P; ++i) {
       const int lr = p.logr[i];
-      const int W = cols256(lr);
+      const int W = cols256l(lr);
       Pass256L a;
       a.in = (i == 0) ? d_in : (const U256*)(((i - 1) & 1) ? s1.p : s0.p);
       a.out = (i == P - 1) ? d_out : (U256*)((i & 1) ? s1.p : s0.p);
@@ -695,7 +736,7 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
       if (!fn) return fail(PBF_EINVAL, "no 256-bit kernel for this radix");
       const uint64_t blocks = (uint64_t)a.blocks_per_poly * batch;
       if (blocks > 0x7fffffffull) return fail(PBF_EINVAL, "batch too large");
-      hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(threads256(lr)), 0, st, a);
+      hipLaunchKernelGGL(fn, dim3((uint32_t)blocks), dim3(threads256l(lr)), 0, st, a);
       PBF_HIP(hipGetLastError());
       log_ns += lr;
     }

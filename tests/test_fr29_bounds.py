@@ -175,10 +175,11 @@ def test_stage_bounds_close():
     vin = 2 * R + (1 << 234)  # assumed stage-input bound (normalised)
     for _ in range(3):
         outs = stage_bounds(vin)
-        red = [b_reduce(o) for o in outs]
-        assert max(o[1] for o in red) < vin
-        # the inter-stage twiddle product of a reduced element, and the pass twiddle of a load
-        assert b_mul(red[0], TW)[1] < vin
+        # the next stage loads the unreduced outputs: c != 0 rows through the inter-stage
+        # twiddle's product (its columns must hold for these limbs), c = 0 rows through reduce()
+        assert max(b_reduce(o)[1] for o in outs) < vin
+        assert max(b_mul(o, TW)[1] for o in outs) < vin
+        # the pass twiddle of a canonical load
         assert b_mul(b_norm(R - 1), TW)[1] < vin
     o2 = [b_add(b_norm(vin), b_norm(vin)), b_sub(b_norm(vin), b_norm(vin), B4R)]
     assert max(b_reduce(o)[1] for o in o2) < vin
@@ -211,14 +212,13 @@ def test_stage_on_extreme_and_random_elements():
             a, b, c, d = ref
             n0, n2, n1, n3 = (a + c) % R, (a - c) % R, (b + d) % R, (b - d) * w % R
             ref = [(n0 + n1) % R, (n0 - n1) % R, (n2 + n3) % R, (n2 - n3) % R]
-            v = [reduce(x) for x in v]
             assert [val(x) % R for x in v] == ref
-            # the next stage's inter-stage twiddle on two of the four
-            v[1] = mul(v[1], tw)
-            v[3] = mul(v[3], tw)
+            # the next stage's loads: one row reduced (c = 0), the others through the twiddle
+            # product, one of them by w^0 (k = 0)
             f = pow(5, (R - 1) // 1024, R)
-            ref[1] = ref[1] * f % R
-            ref[3] = ref[3] * f % R
+            one = limbs(RP % R)
+            v = [reduce(v[0]), mul(v[1], tw), mul(v[2], one), mul(v[3], tw)]
+            ref = [ref[0], ref[1] * f % R, ref[2], ref[3] * f % R]
         assert [canon(reduce(x)) for x in v] == ref
 
 
