@@ -1781,10 +1781,11 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   PBF_HIP(hipGetLastError());
   if ((rc = P.check_bad("t(x) = numerator / Z_H is not a polynomial of 3(n+2) coefficients (plonk.rs:370)")))
     return rc;
+  // (round 6: the mark now precedes the t_lo commitment, which rounds 4-5 counted here)
+  P.mark("round 3 quotient + INTT");
   {
     hipEvent_t ready = msm_scalars_ready(ctx, s);
     if ((rc = P.commit(tq, m, 4, ready))) return rc;            // t_lo
-    P.mark("round 3 quotient + INTT");
     if ((rc = P.commit(tq + 4 * m, m, 5, ready))) return rc;    // t_mid
     if ((rc = P.commit(tq + 8 * m, m, 6, ready))) return rc;    // t_hi
   }
