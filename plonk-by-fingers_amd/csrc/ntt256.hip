@@ -230,6 +230,7 @@ struct Pass256L {
   const L29* tw1;
   const U256* mul_by;  // last pass only, or null: outputs become mul_by[i] y 2^-256 (mul_ntt)
   uint64_t n;
+  uint64_t in_len;     // first pass: input elements at index >= in_len read as zero (not loaded)
   uint32_t log_n, log_ns, tw_bits, blocks_per_poly, batch;
 };
 
@@ -302,8 +303,10 @@ __device__ __forceinline__ void stage29(L29* v, const Lds29& lds, const Pass256L
       const int sub = t + NT * u;
       const int w = sub % W, i = sub / W;
 #pragma unroll
-      for (int c = 0; c < Q; ++c)
-        v[u * Q + c] = l29::from_u256(in[(j0 + w) + (uint64_t)(i + c * (R / Q)) * (a.n >> LOGR)]);
+      for (int c = 0; c < Q; ++c) {
+        const uint64_t e = (j0 + w) + (uint64_t)(i + c * (R / Q)) * (a.n >> LOGR);
+        v[u * Q + c] = e < a.in_len ? l29::from_u256(in[e]) : L29{};
+      }
     }
     // the pass twiddle, one element at a time (a table of 4 limb twiddles would not fit beside v)
     // (compile-time element indices: the loop vectoriser had turned a plain loop here into one
@@ -695,7 +698,7 @@ static Pass256LFn pass256l_fn(int logr) {
 // Montgomery product: mont(m, y) = m y / R) -- mul_ntt's pointwise product fused into the second
 // operand's forward transform
 static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch, DevBuf& s0, DevBuf& s1,
-                  hipStream_t st, const U256* mul_by = nullptr) {
+                  hipStream_t st, const U256* mul_by = nullptr, uint64_t in_len = 0) {
   if (batch == 0) return 0;
   if (p.n == 1) {
     if (d_in != d_out) PBF_HIP(hipMemcpyAsync(d_out, d_in, batch * sizeof(U256), hipMemcpyDeviceToDevice, st));
@@ -727,6 +730,7 @@ static int run256(const Plan256& p, const U256* d_in, U256* d_out, size_t batch,
       a.tw1 = (const L29*)((p.fold_scale && i == P - 1) ? p.tw1s_29.p : p.tw1_29.p);
       a.mul_by = (i == P - 1) ? mul_by : nullptr;
       a.n = p.n;
+      a.in_len = (i == 0 && in_len) ? in_len : p.n;
       a.log_n = p.log_n;
       a.log_ns = log_ns;
       a.tw_bits = p.tw_bits;
@@ -956,6 +960,28 @@ int pbf_ntt_fr256_batch_dev(pbf_ctx* ctx, const uint64_t* omega, const uint64_t*
   if (rc) return rc;
   return run256(*p, (const U256*)d_in, (U256*)d_out, batch, ctx->scratch0, ctx->scratch1, (hipStream_t)stream);
 }
+
+}  // extern "C"
+
+// The prover's coset transforms (prover.hip coset_ntt_batch): batch x n elements in d_io, of which
+// only the first in_len of each polynomial were written (the rest is zero padding the caller has
+// not stored): the 29-bit passes read no element past in_len; the 32-bit ones get the padding
+// written first. In place.
+int pbf_internal_ntt_fr256_prefix(pbf_ctx* ctx, const uint64_t* omega, uint64_t* d_io, size_t n, size_t batch,
+                                  size_t in_len, hipStream_t s) {
+  Plan256* p;
+  int rc = get_plan256(ctx, omega, n, 0, &p);
+  if (rc) return rc;
+  if (in_len > n) return fail(PBF_EINVAL, "prefix longer than the transform");
+  if (!p->l29 || p->logr.empty()) {
+    if (in_len < n)
+      PBF_HIP(hipMemset2DAsync(d_io + 4 * in_len, n * 32, 0, (n - in_len) * 32, batch, s));
+    in_len = 0;
+  }
+  return run256(*p, (const U256*)d_io, (U256*)d_io, batch, ctx->scratch0, ctx->scratch1, s, nullptr, in_len);
+}
+
+extern "C" {
 
 // fft.rs:109-132 mul_ntt for BN254 Fr; out has la+lb elements (4 x u64 each)
 int pbf_mul_ntt_fr256(pbf_ctx* ctx, const uint64_t* omega, const uint64_t* a, size_t la, const uint64_t* b,

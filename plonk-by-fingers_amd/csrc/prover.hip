@@ -31,6 +31,10 @@
 #include "../../include/pbf.h"
 #include "msm.hpp"
 
+// ntt256.hip: the coset transforms' batched forward NTT of zero-padded prefixes
+int pbf_internal_ntt_fr256_prefix(pbf_ctx* ctx, const uint64_t* omega, uint64_t* d_io, size_t n, size_t batch,
+                                  size_t in_len, hipStream_t s);
+
 namespace pbf {
 
 typedef uint64_t fr4[4];
@@ -842,10 +846,16 @@ struct Prover {
   int coset_ntt_batch(int k, const uint64_t* const* srcs, const uint64_t* lens, const U256* bases, uint64_t* out,
                       const int* degs = nullptr) {
     if (G == 1) {
+      // only the scaled coefficients are written (the longest length of the batch; round 6): the
+      // transform's first pass reads nothing past them (pbf_internal_ntt_fr256_prefix), so the
+      // 3/4 of every 4n slot that is zero padding is neither stored nor loaded
+      uint64_t mx = 0;
+      for (int i = 0; i < k; ++i) mx = lens[i] > mx ? lens[i] : mx;
+      if (mx > N) mx = N;
       for (int i = 0; i < k; ++i)
-        scale(srcs[i], 0, 1, lens[i], out + 4 * N * i, N, bases[i], 0, 1, degs ? degs[i] : 0);
+        scale(srcs[i], 0, 1, lens[i], out + 4 * N * i, mx, bases[i], 0, 1, degs ? degs[i] : 0);
       PBF_HIP(hipGetLastError());
-      return ntt(wN_plain, out, out, N, k, 0);  // one batched NTT (fuller GPU, one plan lookup)
+      return pbf_internal_ntt_fr256_prefix(ctx, wN_plain, out, N, k, mx, s);  // one batched NTT
     }
     uint64_t* sh = (uint64_t*)shard->p;
     for (int i = 0; i < k; ++i)

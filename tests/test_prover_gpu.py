@@ -225,3 +225,24 @@ def test_shared_snapshots_across_caches(ctx):
     assert ctx.plonk_prove_bn254(*Bc, chal, rnd, srs2, mode=1) == pb2
 
 
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_coset_prefix_transforms_match_32bit_padded(n):
+    """The coset transforms read only the written prefix of each 4n slot (29-bit passes, round 6)
+    or get the zero padding written first (option ntt256.l29 = 0: the 32-bit passes): the same
+    proof either way, with and without the proving-key cache."""
+    import pbf
+
+    rng = random.Random(n)
+    chal = [rng.randrange(P.R) for _ in range(5)]
+    rnd = [rng.randrange(P.R) for _ in range(9)]
+    proofs = []
+    for opts in ({}, {"ntt256.l29": "0"}, {"prover.pk": 0}):
+        c = pbf.Context(0, options=opts)
+        try:
+            srs = c.srs_create(91, n + 3)
+            proofs.append(c.plonk_prove_bn254(*P.mul_gates_circuit(n, 5), chal, rnd, srs, mode=1))
+        finally:
+            c.close()
+    assert proofs[0] == proofs[1] == proofs[2]
