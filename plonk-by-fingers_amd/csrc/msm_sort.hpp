@@ -65,19 +65,40 @@ __global__ void __launch_bounds__(RS_T) rs_hist(const uint32_t* keys, uint32_t m
   __syncthreads();
   const uint32_t base = blockIdx.x * (RS_T * ITEMS);
   uint32_t k[ITEMS];
-  if constexpr (DIG) {
-    // pass 1 (shift 0, kw a multiple of 256): the digit follows from the code alone
+  // four consecutive entries per load (round 6: 16-B key / 8-B code loads; the histogram does
+  // not care which thread counts an entry); the tile's ragged end entry by entry
+  static_assert(ITEMS % 4 == 0, "four entries per load");
 #pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t e = base + u * RS_T + threadIdx.x;
-      const uint32_t c = e < m ? (uint32_t)dg.dig[e] : rs_none<C>();
-      k[u] = e < m ? (c == rs_none<C>() ? dg.zkey : c & (rs_sign<C>() - 1)) : 0xFFFFFFFFu;
-    }
-  } else {
+  for (int u = 0; u < ITEMS / 4; ++u) {
+    const uint32_t e = base + 4 * (u * RS_T + threadIdx.x);
+    uint32_t raw[4];
+    if constexpr (DIG) {
+      if (e + 4 <= m) {
+        if constexpr (sizeof(C) == 4) {
+          const uint4 v = *reinterpret_cast<const uint4*>(dg.dig + e);
+          raw[0] = v.x; raw[1] = v.y; raw[2] = v.z; raw[3] = v.w;
+        } else {
+          const uint2 v = *reinterpret_cast<const uint2*>(dg.dig + e);
+          raw[0] = v.x & 0xFFFFu; raw[1] = v.x >> 16; raw[2] = v.y & 0xFFFFu; raw[3] = v.y >> 16;
+        }
+      } else {
 #pragma unroll
-    for (int u = 0; u < ITEMS; ++u) {
-      const uint32_t e = base + u * RS_T + threadIdx.x;
-      k[u] = e < m ? keys[e] : 0xFFFFFFFFu;
+        for (int q = 0; q < 4; ++q) raw[q] = e + q < m ? (uint32_t)dg.dig[e + q] : 0u;
+      }
+      // pass 1 (shift 0, kw a multiple of 256): the digit follows from the code alone
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        k[4 * u + q] = e + q < m ? (raw[q] == rs_none<C>() ? dg.zkey : raw[q] & (rs_sign<C>() - 1)) : 0xFFFFFFFFu;
+    } else {
+      if (e + 4 <= m) {
+        const uint4 v = *reinterpret_cast<const uint4*>(keys + e);
+        raw[0] = v.x; raw[1] = v.y; raw[2] = v.z; raw[3] = v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) raw[q] = e + q < m ? keys[e + q] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) k[4 * u + q] = raw[q];
     }
   }
 #pragma unroll
@@ -190,12 +211,21 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
     const bool valid = base + wave * RS_WQ + r * 64 + lane < m;
     const uint32_t d =
         DIG ? (key[r] == rs_none<C>() ? dg.zkey : key[r] & (rs_sign<C>() - 1)) & mask : (key[r] >> shift) & mask;
-    uint64_t peers = __ballot(valid);
+    // match-any over the digit's bits (round 6): per bit one ballot, then per 32-bit half
+    // peers &= ~(ballot ^ m) with m = 0 or ~0 the lane's bit: two 3-input logic operations
+    // instead of a 64-bit select (a uniform skip of the bits above the pass's width measured
+    // slower: profiles/r06/sort_match_ab.log)
+    const uint64_t pv = __ballot(valid);
+    uint32_t plo = (uint32_t)pv, phi = (uint32_t)(pv >> 32);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-      const uint64_t bal = __ballot((d >> b) & 1);
-      peers &= ((d >> b) & 1) ? bal : ~bal;
+      // (bits above the width: every lane 0, the ballot 0, peers unchanged)
+      const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int32_t)d, b, 1);  // 0 or ~0
+      const uint64_t bal = __ballot(mk);
+      plo &= ~((uint32_t)bal ^ mk);
+      phi &= ~((uint32_t)(bal >> 32) ^ mk);
     }
+    const uint64_t peers = ((uint64_t)phi << 32) | plo;
     const uint32_t before = __popcll(peers & below);
     rank[r] = wc[wave][d] + before;  // this wave's earlier entries of digit d, then this round's
     if (valid && before == 0) wc[wave][d] += __popcll(peers);
@@ -257,6 +287,7 @@ __global__ void __launch_bounds__(RS_T) __attribute__((amdgpu_waves_per_eu(2))) 
     }
   }
 }
+
 
 // One pass: (kin, vin) (or dg) -> (kout, vout) stably sorted by key bits [shift, shift + dbits),
 // dbits <= 8 (narrower digits: longer runs per digit and tile on the store side).
