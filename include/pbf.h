@@ -75,7 +75,8 @@ int pbf_ctx_set_stream(pbf_ctx* ctx, void* stream);
  *   ntt.no_rg      1          2^24: the round-2 passes instead of the regrouped plan
  *   ntt256.maxr    4..9       largest radix (bits) of the 256-bit NTT passes (default 9)
  *   ntt256.twlog   L          256-bit per-pass twiddle tables up to 2^L entries (default 26)
- *   ntt256.l29     0          256-bit NTT passes on 8 x 32-bit limbs instead of nine 29-bit ones
+ *   ntt256.l29     0          256-bit NTT passes and the prover's quotient kernel on 8 x 32-bit
+ *                             limbs instead of nine 29-bit ones
  *   msm.fx_c       16/20/22   fixed-base MSM window bits (default by size)
  *   g1.mul_base    "daa"      G1 fixed-base products by double-and-add instead of the comb
  *   pair.engine    "lane"/"wg" pairing engine (default: lanes from 4096 pairings)

@@ -30,6 +30,7 @@
 #include <vector>
 #include "../../include/pbf.h"
 #include "msm.hpp"
+#include "fr29.hpp"
 
 // ntt256.hip: the coset transforms' batched forward NTT of zero-padded prefixes
 int pbf_internal_ntt_fr256_prefix(pbf_ctx* ctx, const uint64_t* omega, uint64_t* d_io, size_t n, size_t batch,
@@ -444,6 +445,112 @@ __global__ void __launch_bounds__(256) k_quotient(QuotArgs q, uint64_t* out, uin
     const U256 num = Fr::add(Fr::add(t1, t23), t4);
     u256_to_u64(Fr::mul_tp(num, q.zh_inv[i & 3]), out + o);
   }
+}
+
+// k_quotient on nine 29-bit limbs (round 6, fr29.hpp; option ntt256.l29 = 0 keeps k_quotient).
+// fr29::mul(u, v) = u v / 2^261 = (u v / R) / 32: every product carries one more factor 1/32 than
+// the 32-bit kernel's, on top of the same R-degree bookkeeping. The host scales the constants so
+// that every term of the numerator ends with exactly one such factor -- beta, k1 beta, k2 beta by
+// 32 (their products enter sums with raw data), alpha^4 by 32^3, alpha^2 by 32, zh_inv by 32^2 --
+// and two constant products align the q_m term (x 32) and q_c (x 1/32); so the output is the
+// 32-bit kernel's canonical integer. Lazy sums as in the Fr NTT passes; one operand of every
+// product is normalised (reduce() where both would be sums), so its 64-bit columns hold.
+using l29::L29;
+struct Quot29Args {
+  const uint64_t *a, *b, *c, *z, *ql, *qr, *qo, *qm, *qc, *s1, *s2, *s3, *l1, *zw;
+  uint64_t N, N_all;
+  Blk blk;
+  U256 g, wN;                       // x = g wN^i at degree 1, as k_quotient
+  L29 beta, gamma, k1b, k2b;        // beta 32, gamma (degree 0), k1 beta 32, k2 beta 32 (degree 1 x)
+  L29 alpha4, alpha2, c_qm, c_qc;   // alpha^4 32^3, alpha^2 32, R 32^2, R
+  L29 zh[4];                        // zh_inv 32^2
+};
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_quotient29(Quot29Args q, uint64_t* out, uint32_t ch) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = (t / 64) * 64 * ch + (t % 64);
+  if (i0 >= q.N) return;
+  U256 x = Fr::mul_tp(q.g, fr_pow(q.wN, blk_index(q.blk, i0)));
+  const U256 step = pow64(q.wN);
+  L29 one{};
+  one.l[0] = 1;
+  for (uint64_t p = i0, k = 0; k < ch && p < q.N; ++k, x = blk_next_x(q.blk, p, x, step, q.g, q.wN), p += 64) {
+    const uint64_t o = 4 * p;
+    const uint64_t i = blk_index(q.blk, p);
+    auto ld = [](const uint64_t* p) { return l29::from_u256(u256_from_u64(p)); };
+    const L29 a = ld(q.a + o), b = ld(q.b + o), c = ld(q.c + o), z = ld(q.z + o);
+    const L29 zw = q.zw ? ld(q.zw + o) : ld(q.z + 4 * ((i + 4) % q.N_all));
+    // t1 (one factor 1/32 per term)
+    const L29 ab = fr29::mul(a, b);
+    L29 t1 = fr29::mul(fr29::mul(ab, ld(q.qm + o)), q.c_qm);
+    t1 = fr29::add(t1, fr29::mul(a, ld(q.ql + o)));
+    t1 = fr29::add(t1, fr29::mul(b, ld(q.qr + o)));
+    t1 = fr29::add(t1, fr29::mul(c, ld(q.qo + o)));
+    t1 = fr29::add(t1, fr29::mul(ld(q.qc + o), q.c_qc));
+    // t2 - t3 (three factors 1/32 each side)
+    const L29 xl = l29::from_u256(x);
+    const L29 bx = fr29::mul(q.beta, xl);
+    const L29 A = fr29::add(fr29::add(a, bx), q.gamma);
+    const L29 Bn = fr29::reduce(fr29::add(fr29::add(b, fr29::mul(q.k1b, xl)), q.gamma));
+    const L29 Cs = fr29::add(fr29::add(c, fr29::mul(q.k2b, xl)), q.gamma);
+    const L29 t2 = fr29::mul(fr29::mul(fr29::mul(A, Bn), Cs), z);
+    const L29 D = fr29::add(fr29::add(a, fr29::mul(q.beta, ld(q.s1 + o))), q.gamma);
+    const L29 En = fr29::reduce(fr29::add(fr29::add(b, fr29::mul(q.beta, ld(q.s2 + o))), q.gamma));
+    const L29 Fs = fr29::add(fr29::add(c, fr29::mul(q.beta, ld(q.s3 + o))), q.gamma);
+    const L29 t3 = fr29::mul(fr29::mul(fr29::mul(D, En), Fs), zw);
+    const L29 t23 = fr29::mul(fr29::sub(t2, t3, fr29::B4R), q.alpha4);
+    // t4 = alpha^2 (z - 1) L1
+    const L29 t4 = fr29::mul(fr29::mul(fr29::sub(z, one, fr29::B2R), ld(q.l1 + o)), q.alpha2);
+    const L29 num = fr29::reduce(fr29::add(fr29::add(t1, t23), t4));
+    u256_to_u64(fr29::canon(fr29::mul(num, q.zh[i & 3])), out + o);
+  }
+}
+
+// host: the 29-bit kernel's constants from k_quotient's (QuotArgs)
+static L29 h_relimb(const U256& a) {
+  L29 r;
+  for (int i = 0; i < 9; ++i) {
+    const int bit = 29 * i;
+    uint64_t v = 0;
+    for (int k = 0; k < 29; ++k) {
+      const int bb = bit + k;
+      if (bb < 256 && ((a.w[bb / 32] >> (bb % 32)) & 1)) v |= 1ull << k;
+    }
+    r.l[i] = (uint32_t)v;
+  }
+  return r;
+}
+// a 32^e (mod r) for a canonical integer a (32 in Montgomery form: Fr::mul(a, 32 R) = 32 a)
+static U256 h_times32(U256 a, int e) {
+  U256 c32 = Fr::one_plain();
+  c32.w[0] = 32;
+  const U256 c32m = Fr::to_mont(c32);
+  for (int k = 0; k < e; ++k) a = Fr::mul(a, c32m);
+  return a;
+}
+static void launch_quotient(const QuotArgs& qa, uint64_t* out, bool l29, hipStream_t s) {
+  const char* qc = ab_env("PBF_QUOT_CHUNK");
+  const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
+  const uint32_t blocks = blocks_for((qa.N + qch - 1) / qch);
+  if (!l29) {
+    hipLaunchKernelGGL(k_quotient, dim3(blocks), dim3(256), 0, s, qa, out, qch);
+    return;
+  }
+  Quot29Args q;
+  q.a = qa.a; q.b = qa.b; q.c = qa.c; q.z = qa.z; q.ql = qa.ql; q.qr = qa.qr; q.qo = qa.qo; q.qm = qa.qm;
+  q.qc = qa.qc; q.s1 = qa.s1; q.s2 = qa.s2; q.s3 = qa.s3; q.l1 = qa.l1; q.zw = qa.zw;
+  q.N = qa.N; q.N_all = qa.N_all; q.blk = qa.blk; q.g = qa.g; q.wN = qa.wN;
+  q.beta = h_relimb(h_times32(qa.beta0, 1));
+  q.gamma = h_relimb(qa.gamma0);
+  // k_quotient forms beta x k1 as mont(mont(beta0, x), k1): here beta0 k1 / R once on the host
+  q.k1b = h_relimb(h_times32(Fr::mul(qa.beta0, qa.k1), 1));
+  q.k2b = h_relimb(h_times32(Fr::mul(qa.beta0, qa.k2), 1));
+  q.alpha4 = h_relimb(h_times32(qa.alpha4, 3));
+  q.alpha2 = h_relimb(h_times32(qa.alpha2, 1));
+  const U256 rm = Fr::to_mont(Fr::one_plain());  // R mod r: "1 at degree 1"
+  q.c_qm = h_relimb(h_times32(rm, 2));
+  q.c_qc = h_relimb(rm);
+  for (int j = 0; j < 4; ++j) q.zh[j] = h_relimb(h_times32(qa.zh_inv[j], 2));
+  hipLaunchKernelGGL(k_quotient29, dim3(blocks), dim3(256), 0, s, q, out, qch);
 }
 
 // Synthetic division by (x - z), the quotients of the openings (plonk.rs:430-442):
@@ -1321,12 +1428,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
       x = Fr::mul(x, w4);
     }
   }
-  {
-    const char* qc = ab_env("PBF_QUOT_CHUNK");
-    const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
-    hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, Wq, qch);
-    PBF_HIP(hipGetLastError());
-  }
+  launch_quotient(qa, Wq, ctx->options.num("ntt256.l29", 1) != 0, s);
+  PBF_HIP(hipGetLastError());
   if ((rc = P.coset_intt_ss(Wq, t_ss))) return rc;
   const uint64_t m = n + 2;  // coefficients per t part
   hipLaunchKernelGGL(k_nonzero, dim3(blocks_for(NE)), dim3(256), 0, s, (const uint64_t*)t_ss, P.ss_count(3 * m), NE,
@@ -1779,11 +1882,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     }
   }
   uint64_t* tq = (uint64_t*)B.t.p;
-  {
-    const char* qc = ab_env("PBF_QUOT_CHUNK");
-    const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
-    hipLaunchKernelGGL(k_quotient, dim3(blocks_for((NE + qch - 1) / qch)), dim3(256), 0, s, qa, W0, qch);
-  }
+  launch_quotient(qa, W0, ctx->options.num("ntt256.l29", 1) != 0, s);
   PBF_HIP(hipGetLastError());
   if ((rc = P.coset_intt(W0, tq))) return rc;
   const uint64_t m = n + 2;  // coefficients per t part
