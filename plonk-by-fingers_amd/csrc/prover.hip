@@ -253,35 +253,58 @@ __global__ void __launch_bounds__(256) k_perm_terms(const uint64_t* abc, const u
   u256_to_u64(Fr::mul_tp(Fr::mul_tp(e1, e2), e3), den + 4 * t);
 }
 
-// out[i] = num[i] / den[i] (Montgomery's trick over chunks of 32, one Fermat inverse per
-// chunk); a zero denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297).
-// num and den are read as stored: with both at R-degree e the quotient comes out at
-// degree 1 (the Montgomery inverse of a degree-e value is at degree 2 - e), which the final
-// from_mont turns canonical. num == null: 1 / den (den at degree 1).
-#ifndef PBF_INV_CHUNK
-#define PBF_INV_CHUNK 32
-#endif
-constexpr int INV_CHUNK = PBF_INV_CHUNK;
-__global__ void __launch_bounds__(256) k_div_batch(const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = t * INV_CHUNK;
-  if (i0 >= count) return;
-  const int m = (int)((count - i0) < INV_CHUNK ? (count - i0) : INV_CHUNK);
-  U256 pre[INV_CHUNK];
+// out[i] = num[i] / den[i] by Montgomery's trick (one Fermat inverse per chunk); a zero
+// denominator sets *bad (the reference's `.unwrap()`, plonk.rs:297). num and den are read as
+// stored: with both at R-degree e the quotient comes out at degree 1 (the Montgomery inverse of a
+// degree-e value is at degree 2 - e), which the final from_mont turns canonical. num == null:
+// 1 / den (den at degree 1).
+// The chunk is spread over a wave (round 6): lane l of a wave takes the elements blk + 64 k + l,
+// k < chunk (coalesced), and keeps its running prefix products in `pre` (count elements of
+// scratch) instead of a per-thread array of 32 (which hipcc had placed in scratch memory); the
+// chunk grows with the count (fewer Fermat inversions: 3 + 380 / chunk products per element)
+// while leaving >= 2048 waves.
+__global__ void __launch_bounds__(256) k_div_batch_w(const uint64_t* num, const uint64_t* den, uint64_t* out,
+                                                     uint64_t* pre, uint64_t count, uint32_t chunk, int* bad) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t lane = g & 63, blk = (g >> 6) * 64 * (uint64_t)chunk;
+  if (blk >= count) return;
   U256 acc = fr_one_m();
-  for (int k = 0; k < m; ++k) {
-    const U256 d = u256_from_u64(den + 4 * (i0 + k));
+  for (uint32_t k = 0; k < chunk; ++k) {
+    const uint64_t i = blk + 64 * (uint64_t)k + lane;
+    if (i >= count) break;
+    const U256 d = u256_from_u64(den + 4 * i);
     if (Fr::is_zero(d)) { *bad = 1; return; }
-    pre[k] = acc;
+    u256_to_u64(acc, pre + 4 * i);
     acc = Fr::mul_tp(acc, d);
   }
-  U256 inv = fr_inv(acc);  // 1 / prod
-  for (int k = m - 1; k >= 0; --k) {
-    const U256 d = u256_from_u64(den + 4 * (i0 + k));
-    const U256 dinv = Fr::mul_tp(inv, pre[k]);  // 1 / d_k
+  U256 inv = fr_inv(acc);  // 1 / prod (1 for a lane with no element)
+  for (int k = (int)chunk - 1; k >= 0; --k) {
+    const uint64_t i = blk + 64 * (uint64_t)k + lane;
+    if (i >= count) continue;
+    const U256 d = u256_from_u64(den + 4 * i);
+    const U256 dinv = Fr::mul_tp(inv, u256_from_u64(pre + 4 * i));  // 1 / d_i
     inv = Fr::mul_tp(inv, d);
-    str(out + 4 * (i0 + k), num ? Fr::mul_tp(u256_from_u64(num + 4 * (i0 + k)), dinv) : dinv);
+    str(out + 4 * i, num ? Fr::mul_tp(u256_from_u64(num + 4 * i), dinv) : dinv);
   }
+}
+// chunk of k_div_batch_w: the largest of 32, 64, 128 that leaves >= 2048 waves (2^24 rows: 64)
+static uint32_t div_chunk(uint64_t count) {
+  uint32_t c = 32;
+  while (c < 128 && (uint64_t)c * 2 * 64 * 2048 <= count) c *= 2;
+  return c;
+}
+static int div_batch(pbf_ctx* ctx, const uint64_t* num, const uint64_t* den, uint64_t* out, uint64_t count, int* bad,
+                     hipStream_t s) {
+  if (!count) return 0;
+  DevBuf& pb = ctx->buf("pv.divpre");
+  int rc = pb.ensure(count * 32);
+  if (rc) return rc;
+  const uint32_t ch = div_chunk(count);
+  const uint64_t waves = (count + 64ull * ch - 1) / (64ull * ch);
+  hipLaunchKernelGGL(k_div_batch_w, dim3(blocks_for(waves * 64)), dim3(256), 0, s, num, den, out, (uint64_t*)pb.p,
+                     count, ch, bad);
+  PBF_HIP(hipGetLastError());
+  return 0;
 }
 
 // ---- exclusive prefix product: out[0] = 1, out[i] = prod_{j<i} in[j]  (i < count)
@@ -1338,9 +1361,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(Bn)), dim3(256), 0, s, d_abc, (const uint64_t*)sig,
                      (const uint64_t*)hpow, n, r * Bn, Bn, beta, Fr::from_mont(gamma), k1, k2, num, den);
   const uint64_t terms = r + 1 == G ? Bn - 1 : Bn;  // ratios j < n - 1
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((terms + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)num, (const uint64_t*)den, num, terms, P.d_bad);
-  PBF_HIP(hipGetLastError());
+  if ((rc = div_batch(ctx, (const uint64_t*)num, (const uint64_t*)den, num, terms, P.d_bad, s))) return rc;
   if (terms < Bn) {  // the last row's slot: 1 (canonical), so the local total is defined
     const uint64_t one_c[4] = {1, 0, 0, 0};
     PBF_HIP(hipMemcpyAsync(num + 4 * (Bn - 1), one_c, E, hipMemcpyHostToDevice, s));
@@ -1785,9 +1806,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(n)), dim3(256), 0, s, d_abc, (const uint64_t*)sigma,
                      (const uint64_t*)hpow, (uint64_t)n, (uint64_t)0, (uint64_t)n, beta, Fr::from_mont(gamma), k1, k2, num,
                      den);
-  hipLaunchKernelGGL(k_div_batch, dim3(blocks_for((n - 1 + INV_CHUNK - 1) / INV_CHUNK)), dim3(256), 0, s,
-                     (const uint64_t*)num, (const uint64_t*)den, num, (uint64_t)(n - 1), P.d_bad);
-  PBF_HIP(hipGetLastError());
+  if ((rc = div_batch(ctx, (const uint64_t*)num, (const uint64_t*)den, num, (uint64_t)(n - 1), P.d_bad, s))) return rc;
   if ((rc = P.check_bad("zero permutation denominator (plonk.rs:297 unwrap)"))) return rc;
   {
     const uint64_t nb = (n - 1 + SCAN_BLK - 1) / SCAN_BLK;
