@@ -148,18 +148,42 @@ __global__ void k_interleave(const uint64_t* in, uint64_t* out, uint64_t nl, uin
   for (int q = 0; q < 4; ++q) out[4 * (g + G * m) + q] = in[4 * id + q];
 }
 
-// out[i] = start * base^i
-__global__ void k_powers(uint64_t* out, uint64_t count, U256 base, U256 start) {
+// out[i] = start * base^i. Round 6: a thread's first power comes from the k_scale_pow tables
+// (powers_tab) instead of a square-and-multiply chain per thread (~36 dependent products, about
+// half of the kernel at 2^24 rows)
+__global__ void k_powers(uint64_t* out, uint64_t count, ScalePow sp) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t i0 = chunk_first(t);
   if (i0 >= count) return;
-  U256 x = Fr::mul_tp(start, fr_pow(base, i0));
-  const U256 step = pow64(base);
+  U256 x = Fr::mul_tp(sp.x0, sp.tl[t % 64]);
+  for (uint64_t v = t / 64, k = 0; v; v >>= 1, ++k)
+    if (v & 1) x = Fr::mul_tp(x, sp.tv[k]);
+  const U256 step = sp.step;
   for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
     str(out + 4 * i, x);
     x = Fr::mul_tp(x, step);
   }
 }
+// host Montgomery power a^e (a in Montgomery form)
+static U256 h_pow(U256 a, uint64_t e) {
+  U256 r = fr_one_m();
+  for (; e; e >>= 1, a = Fr::mul(a, a))
+    if (e & 1) r = Fr::mul(r, a);
+  return r;
+}
+// the start-power tables of x0 base^(e_off + e_mult i) (k_scale_pow, k_powers), host products
+static ScalePow scale_pow_tab(const U256& x0, const U256& base, uint64_t e_off, uint64_t e_mult) {
+  ScalePow sp;
+  sp.x0 = Fr::mul(x0, h_pow(base, e_off));
+  sp.step = h_pow(base, 64 * e_mult);
+  const U256 bm = h_pow(base, e_mult);
+  sp.tl[0] = fr_one_m();
+  for (int l = 1; l < 64; ++l) sp.tl[l] = Fr::mul(sp.tl[l - 1], bm);
+  sp.tv[0] = h_pow(sp.step, PV_CHUNK);
+  for (int k = 1; k < SP_WBITS; ++k) sp.tv[k] = Fr::mul(sp.tv[k - 1], sp.tv[k - 1]);
+  return sp;
+}
+static ScalePow powers_tab(const U256& base, const U256& start) { return scale_pow_tab(start, base, 0, 1); }
 
 // copy_constraints_to_roots (plonk.rs:181-189): sigma[col][i] = {w^j, k1 w^j, k2 w^j}[kind]
 // Rows [row0, row0 + rows) of every column; sigma[col][i - row0] (the whole table: 0, n)
@@ -806,43 +830,95 @@ __global__ void k_mul1(const uint64_t* a, const uint64_t* b, uint64_t* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) u256_to_u64(Fr::from_mont(Fr::mul(ldr(a), ldr(b))), out);
 }
 
-// batched Horner: partial[p][chunk] = x^(chunk start) * sum of the chunk's terms
-constexpr int EV_T = 256, EV_PER = 64;
+// batched Horner: partial[p][chunk] = x^(off + chunk start) * sum of the chunk's terms.
+// Round 6: a thread's Horner value h_t enters the block sum as h_t x^(64 t) through the LDS tree
+// (level s adds sh[t + s] x^(64 s)), and the block's x^(off + 16384 ch) is a product over the set
+// bits of ch; the powers are host products in the arguments (one table per distinct (x, off): the
+// prover evaluates at z and z w), not a square-and-multiply chain per thread (~36 dependent
+// products next to the 64 Horner steps)
+constexpr int EV_T = 256, EV_PER = 64, EV_PW = 26, EV_XS = 2;  // chunks < 2^(EV_PW - 8)
 struct EvalArgs {
   const uint64_t* poly[12];
   uint64_t len[12];
   U256 x[12];
   uint64_t off[12];  // global index of poly[p][0] (a rank's coefficient range; 0 on one GPU)
   uint64_t chunks;   // per polynomial
+  // filled by launch_eval: pw[xi[p]][k] = x^(64 2^k), xoff[xi[p]] = x^off (Montgomery form)
+  U256 pw[EV_XS][EV_PW];
+  U256 xoff[EV_XS];
+  uint8_t xi[12];
 };
+static_assert(sizeof(EvalArgs) <= 4096, "kernel argument limit");
 __global__ void __launch_bounds__(EV_T) k_eval_partial(EvalArgs e, uint64_t* partial) {
   __shared__ U256 sh[EV_T];
   const uint64_t p = blockIdx.x / e.chunks, ch = blockIdx.x % e.chunks;
   const int t = threadIdx.x;
   const uint64_t start = (ch * EV_T + t) * EV_PER;
   const U256 x = e.x[p];
+  const int xi = e.xi[p];
   U256 acc = u256_zero();
   if (start < e.len[p]) {
     uint64_t end = start + EV_PER;
     if (end > e.len[p]) end = e.len[p];
     // conversion-free Horner: canonical acc times Montgomery-form x stays canonical
     for (uint64_t j = end; j-- > start;) acc = Fr::add(Fr::mul_tp(acc, x), u256_from_u64(e.poly[p] + 4 * j));
-    acc = Fr::mul_tp(acc, fr_pow(x, e.off[p] + start));
   }
   sh[t] = acc;
   __syncthreads();
-  for (int s = EV_T / 2; s > 0; s >>= 1) {
+  for (int s = EV_T / 2, k = 7; s > 0; s >>= 1, --k) {  // EV_T = 2^8: x^(64 s) = pw[k]
+    if (t < s) sh[t] = Fr::add(sh[t], Fr::mul_tp(sh[t + s], e.pw[xi][k]));
+    __syncthreads();
+  }
+  if (t == 0) {
+    U256 f = e.xoff[xi];
+    for (uint64_t c = ch, k = 8; c; c >>= 1, ++k)  // 16384 ch = 64 2^8 ch
+      if (c & 1) f = Fr::mul_tp(f, e.pw[xi][k]);
+    u256_to_u64(Fr::mul_tp(sh[0], f), partial + 4 * blockIdx.x);
+  }
+}
+// out[p] = sum of the chunks' partials (one block per polynomial; round 6: the serial loop of one
+// thread per polynomial had taken 1.6 ms over the 1024 chunks of a 2^24-row evaluation)
+__global__ void __launch_bounds__(256) k_eval_final(const uint64_t* partial, uint64_t chunks, uint64_t* out) {
+  __shared__ U256 sh[256];
+  const uint64_t p = blockIdx.x;
+  const int t = threadIdx.x;
+  U256 acc = u256_zero();
+  for (uint64_t i = t; i < chunks; i += 256) acc = Fr::add(acc, u256_from_u64(partial + 4 * (p * chunks + i)));
+  sh[t] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
     if (t < s) sh[t] = Fr::add(sh[t], sh[t + s]);
     __syncthreads();
   }
-  if (t == 0) u256_to_u64(sh[0], partial + 4 * blockIdx.x);
+  if (t == 0) u256_to_u64(sh[0], out + 4 * p);
 }
-__global__ void k_eval_final(const uint64_t* partial, uint64_t chunks, uint64_t np, uint64_t* out) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
-  U256 acc = u256_zero();
-  for (uint64_t i = 0; i < chunks; ++i) acc = Fr::add(acc, u256_from_u64(partial + 4 * (p * chunks + i)));
-  u256_to_u64(acc, out + 4 * p);
+
+// the power tables, the partial sums, then the totals of np polynomials into evals
+static int launch_eval(EvalArgs& e, int np, DevBuf& partial, uint64_t* evals, hipStream_t s) {
+  if (e.chunks >= (1ull << (EV_PW - 8))) return fail(PBF_EINVAL, "evaluation longer than its power tables");
+  U256 kx[EV_XS];
+  uint64_t koff[EV_XS];
+  int nx = 0;
+  for (int p = 0; p < np; ++p) {
+    int j = 0;
+    while (j < nx && !(Fr::eq(kx[j], e.x[p]) && koff[j] == e.off[p])) ++j;
+    if (j == nx) {
+      if (nx == EV_XS) return fail(PBF_EINVAL, "more distinct evaluation points than power tables");
+      kx[j] = e.x[p]; koff[j] = e.off[p];
+      e.xoff[j] = h_pow(e.x[p], e.off[p]);
+      e.pw[j][0] = h_pow(e.x[p], EV_PER);
+      for (int k = 1; k < EV_PW; ++k) e.pw[j][k] = Fr::mul(e.pw[j][k - 1], e.pw[j][k - 1]);
+      ++nx;
+    }
+    e.xi[p] = (uint8_t)j;
+  }
+  const uint64_t pn = np * e.chunks;
+  int rc = partial.ensure(pn * 32);
+  if (rc) return rc;
+  uint64_t* part = (uint64_t*)partial.p;
+  hipLaunchKernelGGL(k_eval_partial, dim3((uint32_t)pn), dim3(EV_T), 0, s, e, part);
+  hipLaunchKernelGGL(k_eval_final, dim3(np), dim3(256), 0, s, (const uint64_t*)part, e.chunks, evals);
+  return 0;
 }
 
 // ---------------------------------------------------------------- host helpers
@@ -960,21 +1036,7 @@ struct Prover {
     // outputs at R-degree deg: the constant R^deg in Montgomery form is R^(deg + 1)
     U256 c0 = Fr::one_plain();
     for (int d = 0; d <= deg; ++d) c0 = Fr::to_mont(c0);
-    // the start-power tables (k_scale_pow), Montgomery products on the host
-    auto hpow = [](U256 a, uint64_t e) {
-      U256 r = fr_one_m();
-      for (; e; e >>= 1, a = Fr::mul(a, a))
-        if (e & 1) r = Fr::mul(r, a);
-      return r;
-    };
-    ScalePow sp;
-    sp.x0 = Fr::mul(deg != 0 ? c0 : fr_one_m(), hpow(base, e_off));
-    sp.step = hpow(base, 64 * e_mult);
-    const U256 bm = hpow(base, e_mult);
-    sp.tl[0] = fr_one_m();
-    for (int l = 1; l < 64; ++l) sp.tl[l] = Fr::mul(sp.tl[l - 1], bm);
-    sp.tv[0] = hpow(sp.step, PV_CHUNK);
-    for (int k = 1; k < SP_WBITS; ++k) sp.tv[k] = Fr::mul(sp.tv[k - 1], sp.tv[k - 1]);
+    const ScalePow sp = scale_pow_tab(deg != 0 ? c0 : fr_one_m(), base, e_off, e_mult);
     hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
                        in_stride, len, out, cnt, sp);
   }
@@ -1276,7 +1338,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   if ((rc = P.agree("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
   P.mark("satisfies (rows)");
   // ---- h = w^i (all of H: copy labels point anywhere)
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, P.omega, one);
+  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, powers_tab(P.omega, one));
   PBF_HIP(hipGetLastError());
   const U256 ninv = hinvm(hm64(n));
   // ---- proving key, sharded like the witness (once per circuit; every proof without the key):
@@ -1299,8 +1361,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
     if ((rc = P.a2a(8 * Sn * E))) return rc;
     if ((rc = pbf_ntt_fr256_shard_local_dev(ctx, P.w_plain, (uint32_t)G, recv, Yk, Bn, 8, 1, s))) return rc;
     uint64_t* l1_ss = Xk;  // the blocked evaluations are consumed
-    hipLaunchKernelGGL(k_powers, dim3(blocks_for((Bn + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1_ss, Bn, one,
-                       ninv);
+    hipLaunchKernelGGL(k_powers, dim3(blocks_for((Bn + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1_ss, Bn,
+                       powers_tab(one, ninv));
     PBF_HIP(hipGetLastError());
     const uint64_t lens[5] = {n, n, n, n, n};
     const U256 bases[5] = {P.g, P.g, P.g, P.g, P.g};
@@ -1325,8 +1387,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
     PBF_HIP(hipMemsetAsync(l1, 0, CRS * E, s));
     const uint64_t cnt = P.cr_count(n);
     if (cnt)
-      hipLaunchKernelGGL(k_powers, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, cnt, one,
-                         ninv);
+      hipLaunchKernelGGL(k_powers, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, cnt,
+                         powers_tab(one, ninv));
     PBF_HIP(hipGetLastError());
   }
   P.mark(pk_hit ? "proving key (cached)" : "proving key (built)");
@@ -1490,11 +1552,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
       maxlen = std::max(maxlen, cnt);
     }
     e.chunks = (maxlen + EV_T * EV_PER - 1) / (EV_T * EV_PER);
-    int rc2 = B.partial.ensure(np * e.chunks * 32);
+    int rc2 = launch_eval(e, np, B.partial, (uint64_t*)B.evals.p, s);
     if (rc2) return rc2;
-    hipLaunchKernelGGL(k_eval_partial, dim3((uint32_t)(np * e.chunks)), dim3(EV_T), 0, s, e, (uint64_t*)B.partial.p);
-    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, s, (const uint64_t*)B.partial.p, e.chunks, (uint64_t)np,
-                       (uint64_t*)B.evals.p);
     PBF_HIP(hipGetLastError());
     std::vector<U256> parts;
     if ((rc2 = P.gather((const uint64_t*)B.evals.p, np, parts))) return rc2;
@@ -1766,7 +1825,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
 
   // ---- h = w^i, sigma labels (plonk.rs:124, 181-189, 222-224)
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
-                     P.omega, one);
+                     powers_tab(P.omega, one));
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, (uint64_t)n,
                      (uint64_t)0, (uint64_t)n, k1, k2, sigma, P.d_bad);
   PBF_HIP(hipGetLastError());
@@ -1853,7 +1912,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   {
     uint64_t* l1 = (uint64_t*)B.tmp0.p;
     hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, (uint64_t)n,
-                       one, ninv);
+                       powers_tab(one, ninv));
     PBF_HIP(hipGetLastError());
   }
   {
@@ -1938,11 +1997,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
       if (lens[i] > maxlen) maxlen = lens[i];
     }
     e.chunks = (maxlen + EV_T * EV_PER - 1) / (EV_T * EV_PER);
-    int rc2 = B.partial.ensure(np * e.chunks * 32);
+    int rc2 = launch_eval(e, np, B.partial, (uint64_t*)B.evals.p, s);
     if (rc2) return rc2;
-    hipLaunchKernelGGL(k_eval_partial, dim3((uint32_t)(np * e.chunks)), dim3(EV_T), 0, s, e, (uint64_t*)B.partial.p);
-    hipLaunchKernelGGL(k_eval_final, dim3(1), dim3(64), 0, s, (const uint64_t*)B.partial.p, e.chunks, (uint64_t)np,
-                       (uint64_t*)B.evals.p);
     PBF_HIP(hipGetLastError());
     std::vector<uint64_t> h(4 * np);
     PBF_HIP(hipMemcpyAsync(h.data(), B.evals.p, 4 * np * 8, hipMemcpyDeviceToHost, s));
@@ -2191,7 +2247,7 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   hout(w_plain, omega);
   PBF_HIP(hipMemsetAsync(fl.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
-                     (uint64_t)n, omega, one);
+                     (uint64_t)n, powers_tab(omega, one));
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hp.p, (uint64_t)n,
                      (uint64_t)0, (uint64_t)n, k1, k2, (uint64_t*)sg.p, (int*)fl.p);
   PBF_HIP(hipGetLastError());
@@ -2412,7 +2468,7 @@ extern "C" int pbf_srs_create_bn254_dev(pbf_ctx* ctx, const uint64_t* s, size_t 
   int rc = pw.ensure((n + 1) * 32);
   if (rc) return rc;
   hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + 1 + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, st, (uint64_t*)pw.p,
-                     (uint64_t)(n + 1), hm(s), fr_one_m());
+                     (uint64_t)(n + 1), powers_tab(hm(s), fr_one_m()));
   PBF_HIP(hipGetLastError());
   return pbf_g1_bn254_mul_base_dev(ctx, (const uint64_t*)pw.p, d_out, n + 1, stream);
 }
