@@ -2042,7 +2042,9 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
       L.k = 6;
     }
     L.c0 = u256_zero();
-    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L, rx, N);
+    // only the rlen coefficients r(x) has are written (round 6; the N-long tail of zeros was
+    // never read: the evaluation, the r_3 sum and the W_z numerator stop at rlen)
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(rlen)), dim3(256), 0, s, L, rx, rlen);
     PBF_HIP(hipGetLastError());
     if (mode == 0) {
       // r_3(x) = z(x) s_sigma_3(x) (beta z_w(z)) K3 (plonk.rs:414-416): the product on the coset
@@ -2052,12 +2054,12 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
       if ((rc = P.coset_intt(W2, W0))) return rc;
       LinComb L2;
       L2.k = 2;
-      L2.in[0] = rx; L2.len[0] = N; L2.c[0] = one;
-      L2.in[1] = W0; L2.len[1] = N; L2.c[1] = Fr::mul(Fr::mul(beta, zw_z), K3);
+      L2.in[0] = rx; L2.len[0] = rlen; L2.c[0] = one;  // z s_sigma_3 has rlen = 2n + 2 coefficients
+      L2.in[1] = W0; L2.len[1] = rlen; L2.c[1] = Fr::mul(Fr::mul(beta, zw_z), K3);
       L2.c0 = u256_zero();
-      hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L2, W2, N);
+      hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(rlen)), dim3(256), 0, s, L2, W2, rlen);
       PBF_HIP(hipGetLastError());
-      PBF_HIP(hipMemcpyAsync(rx, W2, N * E, hipMemcpyDeviceToDevice, s));
+      PBF_HIP(hipMemcpyAsync(rx, W2, rlen * E, hipMemcpyDeviceToDevice, s));
     }
   }
   U256 r_z;
@@ -2071,6 +2073,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
 
   // ---- round 5: W_z = [t_lo + z^(n+2) t_mid + z^(2n+4) t_hi - t_z + v (r - r_z) + v^2 (a - a_z)
   //      + v^3 (b - b_z) + v^4 (c - c_z) + v^5 (s1 - s1_z) + v^6 (s2 - s2_z)] / (x - z)   (:430-439)
+  const uint64_t lnum = rlen > m ? rlen : m;  // numerator coefficients (t parts m, r rlen, a/b/c n+2)
   U256 vp[7];
   vp[0] = one;
   for (int i = 1; i < 7; ++i) vp[i] = Fr::mul(vp[i - 1], v);
@@ -2095,13 +2098,12 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
     cst = Fr::add(cst, Fr::mul(vp[5], s1_z));
     cst = Fr::add(cst, Fr::mul(vp[6], s2_z));
     L.c0 = Fr::sub(u256_zero(), cst);
-    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(N)), dim3(256), 0, s, L, W2, N);
+    hipLaunchKernelGGL(k_lincomb, dim3(blocks_for(lnum)), dim3(256), 0, s, L, W2, lnum);  // what the division reads
     PBF_HIP(hipGetLastError());
   }
   // W_z = numerator / (x - z), W_zw = (z(x) - z_w(z)) / (x - z w) (plonk.rs:430-442) by
   // synthetic division on the coefficients (replicated on every rank of a sharded prove)
-  const uint64_t lnum = rlen > m ? rlen : m;  // numerator coefficients (t parts m, r rlen, a/b/c n+2)
-  const uint64_t wlen = lnum - 1;             // = max(rlen - 1, m)
+  const uint64_t wlen = lnum - 1;  // = max(rlen - 1, m)
   if ((rc = P.synth_div(W2, lnum, zc, u256_zero(), W1, "W_z division left a remainder (plonk.rs:438)"))) return rc;
   uint64_t* W3 = W0;  // W1 still feeds the W_z commitment's MSM
   if ((rc = P.synth_div(zx, n + 3, zw, zw_z, W3, "W_zw division left a remainder (plonk.rs:442)"))) return rc;
