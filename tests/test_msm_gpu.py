@@ -210,6 +210,28 @@ def test_fixed_base_msm_edges_and_cache(ctx):
     assert ctx.msm_g1_fixed_dev(dp.data_ptr(), len(pts), dz.data_ptr(), len(pts)) == (0, 0)
 
 
+@pytest.mark.parametrize("n_points,which", [(3001, 3000), (3001, 0), (70001, 35000)])
+def test_fixed_base_cache_sees_one_changed_point(ctx, n_points, which):
+    """The table cache's exact-content check (k_snap_compare) notices one point negated in
+    place, at the first, the middle or the last position of the set; the answer equals the
+    windowed MSM's over the changed points."""
+    import torch
+
+    rnd = random.Random(n_points + which)
+    base = [bn254.g1_mul(bn254.G1_GEN, rnd.randrange(1, R)) for _ in range(29)]
+    pts = (base * (n_points // len(base) + 1))[:n_points]
+    sc = [rnd.randrange(R) for _ in range(n_points)]
+    dp, ds = _dev_points(pts), _dev_scalars(sc)
+    first = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n_points)
+    assert first == ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n_points)
+    pts[which] = (pts[which][0], Q - pts[which][1])
+    dp.copy_(_dev_points(pts))
+    torch.cuda.synchronize()
+    got = ctx.msm_g1_fixed_dev(dp.data_ptr(), n_points, ds.data_ptr(), n_points)
+    assert got == ctx.msm_g1_dev(dp.data_ptr(), ds.data_ptr(), n_points)
+    assert got != first
+
+
 @pytest.mark.parametrize("n_points,n", [(300, 255), (300, 256), (300, 300), (70001, 70001), (70001, 69000)])
 def test_fixed_base_digit_sort_matches_windowed(ctx, n_points, n):
     """The MSM sorts' first pass from 16-bit digit codes (msm_sort.hpp RsDigits; fixed-base and
