@@ -1832,11 +1832,10 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
   PBF_HIP(hipMemsetAsync(coef, 0, (pk_on ? 3 : 11) * CS * E, s));
   if (pk_on && !pk_hit) PBF_HIP(hipMemsetAsync(pkcoef, 0, 8 * CS * E, s));
-  // a b c: one batched INTT of the (contiguous) witness columns into the work buffer, then
-  // into their padded coefficient slots
-  if ((rc = P.ntt(P.w_plain, d_abc, W0, n, 3, 1))) return rc;
+  // a b c: INTTs of the witness columns straight into their padded coefficient slots (round 6:
+  // one batched INTT into the work buffer and three n-element copies before)
   for (int k = 0; k < 3; ++k)
-    PBF_HIP(hipMemcpyAsync(C(k), W0 + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
+    if ((rc = P.ntt(P.w_plain, d_abc + 4 * n * k, C(k), n, 1, 1))) return rc;
   if (!pk_hit) {
     for (int k = 0; k < 5; ++k)
       PBF_HIP(hipMemcpyAsync(C(3 + k), d_q + 4 * n * k, n * E, hipMemcpyDeviceToDevice, s));
