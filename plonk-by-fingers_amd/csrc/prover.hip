@@ -148,22 +148,6 @@ __global__ void k_interleave(const uint64_t* in, uint64_t* out, uint64_t nl, uin
   for (int q = 0; q < 4; ++q) out[4 * (g + G * m) + q] = in[4 * id + q];
 }
 
-// out[i] = start * base^i. Round 6: a thread's first power comes from the k_scale_pow tables
-// (powers_tab) instead of a square-and-multiply chain per thread (~36 dependent products, about
-// half of the kernel at 2^24 rows)
-__global__ void k_powers(uint64_t* out, uint64_t count, ScalePow sp) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t i0 = chunk_first(t);
-  if (i0 >= count) return;
-  U256 x = Fr::mul_tp(sp.x0, sp.tl[t % 64]);
-  for (uint64_t v = t / 64, k = 0; v; v >>= 1, ++k)
-    if (v & 1) x = Fr::mul_tp(x, sp.tv[k]);
-  const U256 step = sp.step;
-  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
-    str(out + 4 * i, x);
-    x = Fr::mul_tp(x, step);
-  }
-}
 // host Montgomery power a^e (a in Montgomery form)
 static U256 h_pow(U256 a, uint64_t e) {
   U256 r = fr_one_m();
@@ -171,7 +155,7 @@ static U256 h_pow(U256 a, uint64_t e) {
     if (e & 1) r = Fr::mul(r, a);
   return r;
 }
-// the start-power tables of x0 base^(e_off + e_mult i) (k_scale_pow, k_powers), host products
+// the start-power tables of x0 base^(e_off + e_mult i) (k_scale_pow, k_powers29), host products
 static ScalePow scale_pow_tab(const U256& x0, const U256& base, uint64_t e_off, uint64_t e_mult) {
   ScalePow sp;
   sp.x0 = Fr::mul(x0, h_pow(base, e_off));
@@ -574,6 +558,69 @@ static U256 h_times32(U256 a, int e) {
   for (int k = 0; k < e; ++k) a = Fr::mul(a, c32m);
   return a;
 }
+// Round 6: the coset scaling and power kernels on 29-bit limbs (fr29.hpp: the product ~1.39x
+// cheaper than the 32-bit one; both kernels are product-bound). The tables hold the 32-bit
+// kernels' numbers times 32 (x 2^261 where those hold x 2^256), so every output is the same
+// canonical integer. Bounds: tables canonical; the running power stays below 1.01 r (a product
+// is below a b / 2^261 + r); an input below 2^256 times it is below 1.04 r, canon() takes it to
+// [0, r).
+struct ScalePow29 {
+  L29 x0, step;
+  L29 tl[64];
+  L29 tv[SP_WBITS];
+};
+static_assert(sizeof(ScalePow29) + 64 <= 4096, "kernel argument limit");
+static ScalePow29 to29(const ScalePow& sp) {
+  auto c = [](const U256& a) { return h_relimb(h_times32(a, 1)); };
+  ScalePow29 r;
+  r.x0 = c(sp.x0);
+  r.step = c(sp.step);
+  for (int l = 0; l < 64; ++l) r.tl[l] = c(sp.tl[l]);
+  for (int k = 0; k < SP_WBITS; ++k) r.tv[k] = c(sp.tv[k]);
+  return r;
+}
+static ScalePow29 powers_tab29(const U256& base, const U256& start) { return to29(powers_tab(base, start)); }
+__device__ __forceinline__ L29 sp29_first(const ScalePow29& sp, uint64_t t) {
+  L29 x = fr29::mul(sp.x0, sp.tl[t % 64]);
+  for (uint64_t v = t / 64, k = 0; v; v >>= 1, ++k)
+    if (v & 1) x = fr29::mul(x, sp.tv[k]);
+  return x;
+}
+// k_scale_pow on 29-bit limbs
+__global__ void k_scale_pow29(const uint64_t* in, uint64_t in_off, uint64_t in_stride, uint64_t len, uint64_t* out,
+                              uint64_t count, ScalePow29 sp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = chunk_first(t);
+  if (i0 >= count) return;
+  if (in_off + in_stride * i0 >= len) {
+    for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64)
+      for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
+    return;
+  }
+  L29 x = sp29_first(sp, t);
+  const L29 step = sp.step;
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
+    const uint64_t j = in_off + in_stride * i;
+    if (j < len) u256_to_u64(fr29::canon(fr29::mul(l29::from_u256(u256_from_u64(in + 4 * j)), x)), out + 4 * i);
+    else for (int q = 0; q < 4; ++q) out[4 * i + q] = 0;
+    x = fr29::mul(x, step);
+  }
+}
+// k_powers on 29-bit limbs: out[i] = start base^i (canonical: the running power times 1)
+__global__ void k_powers29(uint64_t* out, uint64_t count, ScalePow29 sp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i0 = chunk_first(t);
+  if (i0 >= count) return;
+  L29 one{};
+  one.l[0] = 1;
+  L29 x = sp29_first(sp, t);
+  const L29 step = sp.step;
+  for (uint64_t i = i0, k = 0; k < PV_CHUNK && i < count; ++k, i += 64) {
+    u256_to_u64(fr29::canon(fr29::mul(x, one)), out + 4 * i);
+    x = fr29::mul(x, step);
+  }
+}
+
 static void launch_quotient(const QuotArgs& qa, uint64_t* out, bool l29, hipStream_t s) {
   const char* qc = ab_env("PBF_QUOT_CHUNK");
   const uint32_t qch = qc && atoi(qc) > 0 ? (uint32_t)atoi(qc) : 32;
@@ -1037,8 +1084,12 @@ struct Prover {
     U256 c0 = Fr::one_plain();
     for (int d = 0; d <= deg; ++d) c0 = Fr::to_mont(c0);
     const ScalePow sp = scale_pow_tab(deg != 0 ? c0 : fr_one_m(), base, e_off, e_mult);
-    hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
-                       in_stride, len, out, cnt, sp);
+    if (ctx->options.num("ntt256.l29", 1) != 0)
+      hipLaunchKernelGGL(k_scale_pow29, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
+                         in_stride, len, out, cnt, to29(sp));
+    else
+      hipLaunchKernelGGL(k_scale_pow, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, in, in_off,
+                         in_stride, len, out, cnt, sp);
   }
   // k coset NTTs of size N: slot i = evaluations of sum_j srcs[i][j] (bases[i] x)^j at g w_N^e
   // (this rank's blocks when sharded), slots count() apart in `out`, at R-degree degs[i]
@@ -1338,7 +1389,7 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
   if ((rc = P.agree("constraints not satisfied by the assignment (constraints.rs:198)"))) return rc;
   P.mark("satisfies (rows)");
   // ---- h = w^i (all of H: copy labels point anywhere)
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, powers_tab(P.omega, one));
+  hipLaunchKernelGGL(k_powers29, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, n, powers_tab29(P.omega, one));
   PBF_HIP(hipGetLastError());
   const U256 ninv = hinvm(hm64(n));
   // ---- proving key, sharded like the witness (once per circuit; every proof without the key):
@@ -1361,8 +1412,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
     if ((rc = P.a2a(8 * Sn * E))) return rc;
     if ((rc = pbf_ntt_fr256_shard_local_dev(ctx, P.w_plain, (uint32_t)G, recv, Yk, Bn, 8, 1, s))) return rc;
     uint64_t* l1_ss = Xk;  // the blocked evaluations are consumed
-    hipLaunchKernelGGL(k_powers, dim3(blocks_for((Bn + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1_ss, Bn,
-                       powers_tab(one, ninv));
+    hipLaunchKernelGGL(k_powers29, dim3(blocks_for((Bn + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1_ss, Bn,
+                       powers_tab29(one, ninv));
     PBF_HIP(hipGetLastError());
     const uint64_t lens[5] = {n, n, n, n, n};
     const U256 bases[5] = {P.g, P.g, P.g, P.g, P.g};
@@ -1387,8 +1438,8 @@ static int prove_sharded(Prover& P, ProverBufs& B, int mode, bool pk_on, bool pk
     PBF_HIP(hipMemsetAsync(l1, 0, CRS * E, s));
     const uint64_t cnt = P.cr_count(n);
     if (cnt)
-      hipLaunchKernelGGL(k_powers, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, cnt,
-                         powers_tab(one, ninv));
+      hipLaunchKernelGGL(k_powers29, dim3(blocks_for((cnt + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, cnt,
+                         powers_tab29(one, ninv));
     PBF_HIP(hipGetLastError());
   }
   P.mark(pk_hit ? "proving key (cached)" : "proving key (built)");
@@ -1824,8 +1875,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   P.mark("satisfies");
 
   // ---- h = w^i, sigma labels (plonk.rs:124, 181-189, 222-224)
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
-                     powers_tab(P.omega, one));
+  hipLaunchKernelGGL(k_powers29, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, hpow, (uint64_t)n,
+                     powers_tab29(P.omega, one));
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hpow, (uint64_t)n,
                      (uint64_t)0, (uint64_t)n, k1, k2, sigma, P.d_bad);
   PBF_HIP(hipGetLastError());
@@ -1910,8 +1961,8 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   const U256 ninv = hinvm(hm64(n));
   {
     uint64_t* l1 = (uint64_t*)B.tmp0.p;
-    hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, (uint64_t)n,
-                       powers_tab(one, ninv));
+    hipLaunchKernelGGL(k_powers29, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, l1, (uint64_t)n,
+                       powers_tab29(one, ninv));
     PBF_HIP(hipGetLastError());
   }
   {
@@ -2247,8 +2298,8 @@ extern "C" int pbf_plonk_verify_bn254_dev(pbf_ctx* ctx, size_t n, const uint64_t
   uint64_t w_plain[4];
   hout(w_plain, omega);
   PBF_HIP(hipMemsetAsync(fl.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
-                     (uint64_t)n, powers_tab(omega, one));
+  hipLaunchKernelGGL(k_powers29, dim3(blocks_for((n + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, s, (uint64_t*)hp.p,
+                     (uint64_t)n, powers_tab29(omega, one));
   hipLaunchKernelGGL(k_sigma, dim3(blocks_for(3 * n)), dim3(256), 0, s, d_copies, (const uint64_t*)hp.p, (uint64_t)n,
                      (uint64_t)0, (uint64_t)n, k1, k2, (uint64_t*)sg.p, (int*)fl.p);
   PBF_HIP(hipGetLastError());
@@ -2468,8 +2519,8 @@ extern "C" int pbf_srs_create_bn254_dev(pbf_ctx* ctx, const uint64_t* s, size_t 
   DevBuf& pw = ctx->buf("srs.pows");
   int rc = pw.ensure((n + 1) * 32);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_powers, dim3(blocks_for((n + 1 + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, st, (uint64_t*)pw.p,
-                     (uint64_t)(n + 1), powers_tab(hm(s), fr_one_m()));
+  hipLaunchKernelGGL(k_powers29, dim3(blocks_for((n + 1 + PV_CHUNK - 1) / PV_CHUNK)), dim3(256), 0, st, (uint64_t*)pw.p,
+                     (uint64_t)(n + 1), powers_tab29(hm(s), fr_one_m()));
   PBF_HIP(hipGetLastError());
   return pbf_g1_bn254_mul_base_dev(ctx, (const uint64_t*)pw.p, d_out, n + 1, stream);
 }
