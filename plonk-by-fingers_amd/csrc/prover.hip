@@ -344,10 +344,11 @@ __global__ void __launch_bounds__(SCAN_T) k_scan1(const uint64_t* in, uint64_t* 
   sh[t] = acc;
   __syncthreads();
   block_scan_mul(sh, t);
-  const U256 pre = t ? sh[t - 1] : fr_one_m();
+  // canonical prefix times a Montgomery-form product: the canonical output in one product
+  const U256 pre = Fr::from_mont(t ? sh[t - 1] : fr_one_m());
   for (int k = 0; k < SCAN_PER; ++k) {
     const uint64_t i = base + k;
-    if (i < count) str(out + 4 * i, Fr::mul_tp(pre, v[k]));
+    if (i < count) u256_to_u64(Fr::mul_tp(pre, v[k]), out + 4 * i);
   }
   if (t == SCAN_T - 1) str(totals + 4 * blockIdx.x, sh[t]);
 }
@@ -381,7 +382,8 @@ __global__ void k_scan3(const uint64_t* incl, uint64_t* out, uint64_t count, con
   if (i == 0) { str(out, fr_one_m()); return; }
   const uint64_t j = i - 1;
   const uint64_t blk = j / SCAN_BLK;
-  str(out + 4 * i, Fr::mul_tp(ldr(totals + 4 * blk), ldr(incl + 4 * j)));
+  // Montgomery-form total times the canonical inclusive product: canonical (2 products, not 4)
+  u256_to_u64(Fr::mul_tp(ldr(totals + 4 * blk), u256_from_u64(incl + 4 * j)), out + 4 * i);
 }
 
 // coeff[idx] += delta (blinding: (b_lo + b_hi x [+ b x^2]) * (x^n - 1), plonk.rs:250-252, 304)
