@@ -1883,8 +1883,10 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
                      (uint64_t)0, (uint64_t)n, k1, k2, sigma, P.d_bad);
   PBF_HIP(hipGetLastError());
   // ---- interpolate_at_h of a b c q_l q_r q_o q_m q_c s1 s2 s3 = INTT (plonk.rs:233-243)
-  PBF_HIP(hipMemsetAsync(coef, 0, (pk_on ? 3 : 11) * CS * E, s));
-  if (pk_on && !pk_hit) PBF_HIP(hipMemsetAsync(pkcoef, 0, 8 * CS * E, s));
+  // every slot's first n coefficients are written below (INTT outputs): only the tails [n, CS)
+  // are cleared (round 6: the whole slots were, 1.5 GB at 2^24 rows)
+  PBF_HIP(hipMemset2DAsync(coef + 4 * n, CS * E, 0, (CS - n) * E, pk_on ? 3 : 11, s));
+  if (pk_on && !pk_hit) PBF_HIP(hipMemset2DAsync(pkcoef + 4 * n, CS * E, 0, (CS - n) * E, 8, s));
   // a b c: INTTs of the witness columns straight into their padded coefficient slots (round 6:
   // one batched INTT into the work buffer and three n-element copies before)
   for (int k = 0; k < 3; ++k)
@@ -1922,7 +1924,7 @@ static int prove_impl(pbf_ctx* ctx, const pbf_comm* comm, size_t n, const uint64
   uint64_t* acc = (uint64_t*)B.acc.p;
   uint64_t* num = (uint64_t*)B.tmp0.p;
   uint64_t* den = (uint64_t*)B.tmp1.p;
-  PBF_HIP(hipMemsetAsync(acc, 0, CS * E, s));
+  PBF_HIP(hipMemsetAsync(acc + 4 * n, 0, (CS - n) * E, s));  // k_scan3 writes the first n
   hipLaunchKernelGGL(k_perm_terms, dim3(blocks_for(n)), dim3(256), 0, s, d_abc, (const uint64_t*)sigma,
                      (const uint64_t*)hpow, (uint64_t)n, (uint64_t)0, (uint64_t)n, beta, Fr::from_mont(gamma), k1, k2, num,
                      den);
